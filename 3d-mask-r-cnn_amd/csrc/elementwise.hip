@@ -1,0 +1,364 @@
+// Bandwidth-bound kernels of the backbone/FPN/RPN graph (gfx950).
+//   maxpool3d fwd/bwd   KL.MaxPooling3D (core/models.py:245 stem pool, 3211 P6)
+//   upsample221 bwd     KL.UpSampling3D((2,2,1)) adjoint (core/models.py:3193-3204)
+//   subsample221        P6 = MaxPool(1, strides (2,2,1)) (core/models.py:3211)
+//   bn_act_bwd          backward of act(BN_frozen(z) [+ residual]) with the
+//                       per-channel reductions for gamma/beta/bias
+//   sgd_keras           Keras 2.3.1 SGD + clipnorm + decay + the RPN L2 term
+//                       (core/models.py:3340-3387)
+// All channels-last with C innermost; threads map to consecutive channels so
+// every access is coalesced; float4 where C % 4 == 0.
+#include "common.h"
+
+namespace m3d {
+
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, int B, int H, int W, int D, int C,
+                                   int kh, int kw, int kd, int sy, int sx, int sz, int py, int px,
+                                   int pz, int OH, int OW, int OD, float* __restrict__ y,
+                                   uint8_t* __restrict__ am) {
+    const int64_t total = (int64_t)B * OH * OW * OD * C;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        int64_t t = i / C;
+        const int oz = (int)(t % OD); t /= OD;
+        const int ox = (int)(t % OW); t /= OW;
+        const int oy = (int)(t % OH);
+        const int b = (int)(t / OH);
+        float best = -INFINITY;
+        int bi = 0;
+        bool any = false;
+        for (int ky = 0; ky < kh; ++ky) {
+            const int iy = oy * sy - py + ky;
+            if (iy < 0 || iy >= H) continue;
+            for (int kx = 0; kx < kw; ++kx) {
+                const int ix = ox * sx - px + kx;
+                if (ix < 0 || ix >= W) continue;
+                for (int kz = 0; kz < kd; ++kz) {
+                    const int iz = oz * sz - pz + kz;
+                    if (iz < 0 || iz >= D) continue;
+                    const float v = x[((((int64_t)b * H + iy) * W + ix) * D + iz) * C + c];
+                    if (!any || v > best) { best = v; bi = (ky * kw + kx) * kd + kz; any = true; }
+                }
+            }
+        }
+        y[i] = best;
+        if (am) am[i] = (uint8_t)bi;
+    }
+}
+
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ am,
+                                   int B, int H, int W, int D, int C, int kh, int kw, int kd,
+                                   int sy, int sx, int sz, int py, int px, int pz, int OH, int OW,
+                                   int OD, float* __restrict__ dx) {
+    const int64_t total = (int64_t)B * H * W * D * C;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        int64_t t = i / C;
+        const int iz = (int)(t % D); t /= D;
+        const int ix = (int)(t % W); t /= W;
+        const int iy = (int)(t % H);
+        const int b = (int)(t / H);
+        float acc = 0.0f;
+        // outputs o with o*s - p <= i <= o*s - p + k - 1
+        const int oy_lo = max(0, (iy + py - kh + 1 + sy - 1) / sy), oy_hi = min(OH - 1, (iy + py) / sy);
+        const int ox_lo = max(0, (ix + px - kw + 1 + sx - 1) / sx), ox_hi = min(OW - 1, (ix + px) / sx);
+        const int oz_lo = max(0, (iz + pz - kd + 1 + sz - 1) / sz), oz_hi = min(OD - 1, (iz + pz) / sz);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const int ky = iy - (oy * sy - py);
+            if (ky < 0 || ky >= kh) continue;
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int kx = ix - (ox * sx - px);
+                if (kx < 0 || kx >= kw) continue;
+                for (int oz = oz_lo; oz <= oz_hi; ++oz) {
+                    const int kz = iz - (oz * sz - pz);
+                    if (kz < 0 || kz >= kd) continue;
+                    const int64_t o = ((((int64_t)b * OH + oy) * OW + ox) * OD + oz) * C + c;
+                    if (am[o] == (uint8_t)((ky * kw + kx) * kd + kz)) acc += dy[o];
+                }
+            }
+        }
+        dx[i] = acc;
+    }
+}
+
+__global__ void upsample221_bwd_kernel(const float4* __restrict__ dup, int B, int H, int W, int D,
+                                       int C4, float4* __restrict__ dsrc, int accumulate) {
+    const int64_t total = (int64_t)B * H * W * D * C4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4);
+        int64_t t = i / C4;
+        const int z = (int)(t % D); t /= D;
+        const int x = (int)(t % W); t /= W;
+        const int y = (int)(t % H);
+        const int b = (int)(t / H);
+        float4 acc = accumulate ? dsrc[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int a = 0; a < 2; ++a)
+            for (int q = 0; q < 2; ++q) {
+                const float4 v = dup[((((int64_t)b * 2 * H + 2 * y + a) * 2 * W + 2 * x + q) * D + z) * C4 + c];
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+        dsrc[i] = acc;
+    }
+}
+
+__global__ void subsample221_kernel(const float4* __restrict__ src, int B, int H, int W, int D,
+                                    int C4, float4* __restrict__ dst, int bwd) {
+    const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+    const int64_t total = (int64_t)B * OH * OW * D * C4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4);
+        int64_t t = i / C4;
+        const int z = (int)(t % D); t /= D;
+        const int x = (int)(t % OW); t /= OW;
+        const int y = (int)(t % OH);
+        const int b = (int)(t / OH);
+        const int64_t full = ((((int64_t)b * H + 2 * y) * W + 2 * x) * D + z) * C4 + c;
+        if (!bwd) {
+            dst[i] = src[full];
+        } else {
+            float4 a = dst[full];
+            const float4 v = src[i];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+            dst[full] = a;
+        }
+    }
+}
+
+// Thread layout: T threads per row cover T channel quads; R = 256/T rows per
+// block pass; gridDim.y channel groups of 4*T channels.
+__global__ __launch_bounds__(256) void bn_act_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ z,
+    int64_t M, int C, int T, int relu, const float* __restrict__ scale,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dz,
+    float* __restrict__ dres, int accumulate_res, float* __restrict__ sum_dpre,
+    float* __restrict__ sum_xhat, float* __restrict__ sum_dz) {
+    const int R = 256 / T;
+    const int tx = threadIdx.x % T, ty = threadIdx.x / T;
+    const int c = (blockIdx.y * T + tx) * 4;
+    float s_p[4] = {0, 0, 0, 0}, s_x[4] = {0, 0, 0, 0}, s_z[4] = {0, 0, 0, 0};
+    if (c < C) {
+        float sc[4] = {1, 1, 1, 1}, mu[4] = {0, 0, 0, 0}, rs[4] = {1, 1, 1, 1};
+        if (scale) { const float4 v = *(const float4*)(scale + c); sc[0] = v.x; sc[1] = v.y; sc[2] = v.z; sc[3] = v.w; }
+        if (mean) { const float4 v = *(const float4*)(mean + c); mu[0] = v.x; mu[1] = v.y; mu[2] = v.z; mu[3] = v.w; }
+        if (rstd) { const float4 v = *(const float4*)(rstd + c); rs[0] = v.x; rs[1] = v.y; rs[2] = v.z; rs[3] = v.w; }
+        for (int64_t r = (int64_t)blockIdx.x * R + ty; r < M; r += (int64_t)gridDim.x * R) {
+            const int64_t off = r * C + c;
+            const float4 g4 = *(const float4*)(dy + off);
+            float g[4] = {g4.x, g4.y, g4.z, g4.w};
+            if (relu) {
+                const float4 y4 = *(const float4*)(y + off);
+                if (!(y4.x > 0.f)) g[0] = 0.f;
+                if (!(y4.y > 0.f)) g[1] = 0.f;
+                if (!(y4.z > 0.f)) g[2] = 0.f;
+                if (!(y4.w > 0.f)) g[3] = 0.f;
+            }
+            float zz[4] = {0, 0, 0, 0};
+            if (z && sum_xhat) { const float4 v = *(const float4*)(z + off); zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w; }
+            float d[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                d[q] = g[q] * sc[q];
+                s_p[q] += g[q];
+                s_x[q] += g[q] * ((zz[q] - mu[q]) * rs[q]);
+                s_z[q] += d[q];
+            }
+            if (dz) *(float4*)(dz + off) = make_float4(d[0], d[1], d[2], d[3]);
+            if (dres) {
+                float4 o = make_float4(g[0], g[1], g[2], g[3]);
+                if (accumulate_res) {
+                    const float4 a = *(const float4*)(dres + off);
+                    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+                }
+                *(float4*)(dres + off) = o;
+            }
+        }
+    }
+    // block reduction over the R rows sharing a channel quad
+    __shared__ float red[3][256][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        red[0][threadIdx.x][q] = s_p[q];
+        red[1][threadIdx.x][q] = s_x[q];
+        red[2][threadIdx.x][q] = s_z[q];
+    }
+    __syncthreads();
+    for (int step = R / 2; step > 0; step >>= 1) {
+        if (ty < step) {
+            const int o = threadIdx.x + step * T;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                red[0][threadIdx.x][q] += red[0][o][q];
+                red[1][threadIdx.x][q] += red[1][o][q];
+                red[2][threadIdx.x][q] += red[2][o][q];
+            }
+        }
+        __syncthreads();
+    }
+    if (ty == 0 && c < C) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (sum_dpre) unsafeAtomicAdd(sum_dpre + c + q, red[0][tx][q]);
+            if (sum_xhat) unsafeAtomicAdd(sum_xhat + c + q, red[1][tx][q]);
+            if (sum_dz) unsafeAtomicAdd(sum_dz + c + q, red[2][tx][q]);
+        }
+    }
+}
+
+// ---- Keras SGD over a flat parameter buffer split into segments padded to
+// multiples of 1024 floats; chunk c (1024 floats) belongs to seg_of_chunk[c].
+__global__ __launch_bounds__(256) void sgd_norm_kernel(const float* __restrict__ w,
+                                                       const float* __restrict__ g,
+                                                       const int32_t* __restrict__ seg_of_chunk,
+                                                       const float* __restrict__ l2,
+                                                       float* __restrict__ norms) {
+    const int64_t ch = blockIdx.x;
+    const int seg = seg_of_chunk[ch];
+    const float lc = l2[seg];
+    const int64_t off = ch * 1024 + threadIdx.x * 4;
+    const float4 wv = *(const float4*)(w + off), gv = *(const float4*)(g + off);
+    const float a = gv.x + lc * wv.x, b = gv.y + lc * wv.y, c = gv.z + lc * wv.z, d = gv.w + lc * wv.w;
+    float s = a * a + b * b + c * c + d * d;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) unsafeAtomicAdd(norms + seg, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ w,
+                                                         const float* __restrict__ g,
+                                                         float* __restrict__ v,
+                                                         const int32_t* __restrict__ seg_of_chunk,
+                                                         const float* __restrict__ l2,
+                                                         const float* __restrict__ norms, float lr,
+                                                         float momentum, float clipnorm) {
+    const int64_t ch = blockIdx.x;
+    const int seg = seg_of_chunk[ch];
+    const float lc = l2[seg];
+    const float nrm = clipnorm > 0.f ? sqrtf(norms[seg]) : 0.0f;
+    const float den = clipnorm > 0.f ? (nrm > clipnorm ? nrm : clipnorm) : 1.0f;
+    const float num = clipnorm > 0.f ? clipnorm : 1.0f;
+    const int64_t off = ch * 1024 + threadIdx.x * 4;
+    float4 wv = *(float4*)(w + off), vv = *(float4*)(v + off);
+    const float4 gv = *(const float4*)(g + off);
+    float gg[4] = {gv.x + lc * wv.x, gv.y + lc * wv.y, gv.z + lc * wv.z, gv.w + lc * wv.w};
+    float* wp = &wv.x;
+    float* vp = &vv.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float gc = (gg[q] * num) / den;          // tf.clip_by_norm
+        vp[q] = momentum * vp[q] - lr * gc;            // Keras SGD velocity
+        wp[q] = wp[q] + vp[q];
+    }
+    *(float4*)(w + off) = wv;
+    *(float4*)(v + off) = vv;
+}
+
+}  // namespace m3d
+
+using namespace m3d;
+
+static unsigned ew_grid(int64_t n) { return grid_for(n, 256, 256 * 32); }
+
+extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                 int64_t C, int32_t kh, int32_t kw, int32_t kd, int32_t sy,
+                                 int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                                 int64_t OH, int64_t OW, int64_t OD, float* y, uint8_t* argmax,
+                                 m3d_stream_t s) {
+    if (kh * kw * kd > 255) return einval("maxpool3d: window larger than 255");
+    const int64_t total = B * OH * OW * OD * C;
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), x, (int)B,
+                       (int)H, (int)W, (int)D, (int)C, kh, kw, kd, sy, sx, sz, py, px, pz, (int)OH,
+                       (int)OW, (int)OD, y, argmax);
+    return check_launch("maxpool_fwd_kernel");
+}
+
+extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t B, int64_t H,
+                                 int64_t W, int64_t D, int64_t C, int32_t kh, int32_t kw,
+                                 int32_t kd, int32_t sy, int32_t sx, int32_t sz, int32_t py,
+                                 int32_t px, int32_t pz, int64_t OH, int64_t OW, int64_t OD,
+                                 float* dx, m3d_stream_t s) {
+    const int64_t total = B * H * W * D * C;
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), dy, argmax,
+                       (int)B, (int)H, (int)W, (int)D, (int)C, kh, kw, kd, sy, sx, sz, py, px, pz,
+                       (int)OH, (int)OW, (int)OD, dx);
+    return check_launch("maxpool_bwd_kernel");
+}
+
+extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D,
+                                   int64_t C, float* d_src, int32_t accumulate, m3d_stream_t s) {
+    if (C % 4) return einval("upsample221_bwd: C must be a multiple of 4");
+    const int64_t total = B * H * W * D * (C / 4);
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(upsample221_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
+                       (const float4*)d_up, (int)B, (int)H, (int)W, (int)D, (int)(C / 4),
+                       (float4*)d_src, accumulate);
+    return check_launch("upsample221_bwd_kernel");
+}
+
+extern "C" int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                    int64_t C, float* y, m3d_stream_t s) {
+    if (C % 4) return einval("subsample221: C must be a multiple of 4");
+    const int64_t total = B * ((H + 1) / 2) * ((W + 1) / 2) * D * (C / 4);
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(subsample221_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
+                       (const float4*)x, (int)B, (int)H, (int)W, (int)D, (int)(C / 4), (float4*)y, 0);
+    return check_launch("subsample221_kernel");
+}
+
+extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64_t D,
+                                    int64_t C, float* dx, m3d_stream_t s) {
+    if (C % 4) return einval("subsample221: C must be a multiple of 4");
+    const int64_t total = B * ((H + 1) / 2) * ((W + 1) / 2) * D * (C / 4);
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(subsample221_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
+                       (const float4*)dy, (int)B, (int)H, (int)W, (int)D, (int)(C / 4), (float4*)dx, 1);
+    return check_launch("subsample221_kernel(bwd)");
+}
+
+extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M,
+                              int64_t C, int32_t relu, const float* scale, const float* mean,
+                              const float* rstd, float* dz, float* dres, int32_t accumulate_res,
+                              float* sum_dpre, float* sum_dpre_xhat, float* sum_dz,
+                              m3d_stream_t s) {
+    if (C % 4) return einval("bn_act_bwd: C must be a multiple of 4");
+    if (relu && !y) return einval("bn_act_bwd: relu needs y");
+    if (sum_dpre_xhat && !z) return einval("bn_act_bwd: xhat sums need z");
+    if (M == 0) return M3D_OK;
+    const int quads = (int)(C / 4);
+    int T = 1;
+    while (T < quads && T < 256) T <<= 1;
+    const int groups = (quads + T - 1) / T;
+    const int R = 256 / T;
+    int64_t gx = (M + R - 1) / R;
+    const int64_t cap = 2048 / groups + 1;
+    if (gx > cap) gx = cap;
+    hipLaunchKernelGGL(bn_act_bwd_kernel, dim3((unsigned)gx, (unsigned)groups), dim3(256), 0, st(s),
+                       dy, y, z, M, (int)C, T, relu, scale, mean, rstd, dz, dres, accumulate_res,
+                       sum_dpre, sum_dpre_xhat, sum_dz);
+    return check_launch("bn_act_bwd_kernel");
+}
+
+extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
+                             const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
+                             float lr, float momentum, float clipnorm, float* norms,
+                             m3d_stream_t s) {
+    if (n_chunks <= 0) return M3D_OK;
+    if (clipnorm > 0.f) {
+        if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
+            return check_launch("memset norms");
+        hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params,
+                           grads, seg_of_chunk, l2_coef, norms);
+        int rc = check_launch("sgd_norm_kernel");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(sgd_update_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params,
+                       grads, moments, seg_of_chunk, l2_coef, norms, lr, momentum, clipnorm);
+    return check_launch("sgd_update_kernel");
+}

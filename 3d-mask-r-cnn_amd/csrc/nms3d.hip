@@ -1,0 +1,393 @@
+// 3-D non-max suppression and ProposalLayer kernels for gfx950.
+//
+// Replaces NonMaxSuppression3D of the vendored wheel (CPU-only; SURVEY.md
+// 2.1, Appendix A.3) and the per-image TF glue of ProposalLayer
+// (core/models.py:369-503).
+//
+// Pipeline for m3d_nms3d (all stream-ordered, no host sync):
+//   1. keys:   64-bit (desc-orderable score << 32 | index); candidates with
+//              score <= -FLT_MAX or NaN get the all-ones key (sorted last);
+//              -0.0 is folded onto +0.0 so ties compare like floats.
+//   2. sort:   bitonic sort ascending == (score desc, index asc), i.e. the
+//              pop order of the reference's priority queue (A.3).  One
+//              1024-thread workgroup in LDS up to 16384 keys, global
+//              compare-exchange passes beyond.
+//   3. mask:   64x64 tiles, one wave per tile, boxes of the column block
+//              staged in LDS; bit j of word (i, jb) = IoU(i, j) > thr, j > i.
+//              IoU op order is IOU<float> @0xb500 (compiled -ffp-contract=off,
+//              IEEE divide) so the bits are identical to the reference's
+//              comparisons.
+//   4. reduce: one workgroup; per 64-row block wave 0 resolves the
+//              intra-block dependencies in registers (readlane loop), then
+//              all threads OR the kept rows into the LDS-resident removed
+//              mask.  Kept original indices are written in selection order.
+#include <float.h>
+
+#include "common.h"
+
+namespace m3d {
+
+__device__ __forceinline__ uint32_t float_ord(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void nms_keys_kernel(const float* __restrict__ scores, int64_t N, int64_t Npad,
+                                uint64_t* __restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Npad) return;
+    uint64_t k = ~0ull;
+    if (i < N) {
+        float s = scores[i];
+        if (s > -FLT_MAX) {
+            if (s == 0.0f) s = 0.0f;  // fold -0.0
+            k = ((uint64_t)(~float_ord(s)) << 32) | (uint64_t)(uint32_t)i;
+        }
+    }
+    keys[i] = k;
+}
+
+// Single-workgroup bitonic sort of n (power of two, <= 16384) keys in LDS.
+__global__ __launch_bounds__(1024) void bitonic_lds_kernel(uint64_t* __restrict__ keys, int n) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sk[i] = keys[i];
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < (n >> 1); t += blockDim.x) {
+                const int i = 2 * t - (t & (j - 1));   // lower index of the pair
+                const int p = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t a = sk[i], b = sk[p];
+                if ((a > b) == up) { sk[i] = b; sk[p] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = sk[i];
+}
+
+__global__ void bitonic_global_kernel(uint64_t* __restrict__ keys, int64_t n, int64_t k,
+                                      int64_t j) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (n >> 1)) return;
+    const int64_t i = 2 * t - (t & (j - 1));
+    const int64_t p = i + j;
+    const bool up = (i & k) == 0;
+    const uint64_t a = keys[i], b = keys[p];
+    if ((a > b) == up) { keys[i] = b; keys[p] = a; }
+}
+
+__global__ void nms_gather_kernel(const float* __restrict__ boxes, const uint64_t* __restrict__ keys,
+                                  int64_t N, int cols, float* __restrict__ sboxes) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint64_t k = keys[i];
+    const uint32_t idx = (uint32_t)k;
+    const bool valid = (k >> 32) != 0xFFFFFFFFull;
+    for (int q = 0; q < 6; ++q)
+        sboxes[i * 6 + q] = (valid && q < cols) ? boxes[(int64_t)idx * cols + q] : 0.0f;
+}
+
+// IOU<float> (@0xb500-0xb656) -- op order is load-bearing.
+__device__ __forceinline__ float iou3d(const float* bi, const float* bj) {
+    const float ymin_i = smin(bi[0], bi[3]), ymax_i = smax(bi[0], bi[3]);
+    const float xmin_i = smin(bi[1], bi[4]), xmax_i = smax(bi[1], bi[4]);
+    const float zmin_i = smin(bi[2], bi[5]), zmax_i = smax(bi[2], bi[5]);
+    const float ymin_j = smin(bj[0], bj[3]), ymax_j = smax(bj[0], bj[3]);
+    const float xmin_j = smin(bj[1], bj[4]), xmax_j = smax(bj[1], bj[4]);
+    const float zmin_j = smin(bj[2], bj[5]), zmax_j = smax(bj[2], bj[5]);
+    const float area_i = ((ymax_i - ymin_i) * (xmax_i - xmin_i)) * (zmax_i - zmin_i);
+    const float area_j = ((ymax_j - ymin_j) * (xmax_j - xmin_j)) * (zmax_j - zmin_j);
+    if (area_i <= 0 || area_j <= 0) return 0.0f;
+    const float iymin = smax(ymin_i, ymin_j), iymax = smin(ymax_i, ymax_j);
+    const float ixmin = smax(xmin_i, xmin_j), ixmax = smin(xmax_i, xmax_j);
+    const float izmin = smax(zmin_i, zmin_j), izmax = smin(zmax_i, zmax_j);
+    const float inter =
+        (smax(iymax - iymin, 0.0f) * smax(ixmax - ixmin, 0.0f)) * smax(izmax - izmin, 0.0f);
+    return inter / ((area_i + area_j) - inter);
+}
+
+// TF 2.2 IOU<float> on (y1,x1,y2,x2) rows (stored in the first 4 of 6 slots).
+__device__ __forceinline__ float iou2d(const float* bi, const float* bj) {
+    const float ymin_i = smin(bi[0], bi[2]), ymax_i = smax(bi[0], bi[2]);
+    const float xmin_i = smin(bi[1], bi[3]), xmax_i = smax(bi[1], bi[3]);
+    const float ymin_j = smin(bj[0], bj[2]), ymax_j = smax(bj[0], bj[2]);
+    const float xmin_j = smin(bj[1], bj[3]), xmax_j = smax(bj[1], bj[3]);
+    const float area_i = (ymax_i - ymin_i) * (xmax_i - xmin_i);
+    const float area_j = (ymax_j - ymin_j) * (xmax_j - xmin_j);
+    if (area_i <= 0 || area_j <= 0) return 0.0f;
+    const float iymin = smax(ymin_i, ymin_j), iymax = smin(ymax_i, ymax_j);
+    const float ixmin = smax(xmin_i, xmin_j), ixmax = smin(xmax_i, xmax_j);
+    const float inter = smax(iymax - iymin, 0.0f) * smax(ixmax - ixmin, 0.0f);
+    return inter / ((area_i + area_j) - inter);
+}
+
+__global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ sboxes, int64_t N,
+                                                      int64_t cb, float thr, int mode,
+                                                      uint64_t* __restrict__ mask) {
+    const int64_t ib = blockIdx.y, jb = blockIdx.x;
+    if (jb < ib) return;
+    __shared__ float cbox[64 * 6];
+    const int t = threadIdx.x;
+    const int64_t j0 = jb * 64;
+    for (int q = t; q < 64 * 6; q += 64) {
+        const int64_t g = j0 * 6 + q;
+        cbox[q] = (g < N * 6) ? sboxes[g] : 0.0f;
+    }
+    __syncthreads();
+    const int64_t i = ib * 64 + t;
+    if (i >= N) return;
+    float bi[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) bi[q] = sboxes[i * 6 + q];
+    uint64_t bits = 0;
+    const int start = (jb == ib) ? t + 1 : 0;
+    for (int q = start; q < 64; ++q) {
+        const int64_t j = j0 + q;
+        if (j >= N) break;
+        const float sim = mode == 1 ? iou2d(bi, cbox + q * 6) : iou3d(bi, cbox + q * 6);
+        if (sim > thr) bits |= (1ull << q);
+    }
+    mask[i * cb + jb] = bits;
+}
+
+// Greedy reduction.  removed[] lives in LDS (cb words, cb <= 16384).
+__global__ __launch_bounds__(1024) void nms_reduce_kernel(const uint64_t* __restrict__ mask,
+                                                          const uint64_t* __restrict__ keys,
+                                                          int64_t N, int64_t cb, int max_out,
+                                                          int32_t* __restrict__ keep,
+                                                          int32_t* __restrict__ num_keep) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t removed[];
+    __shared__ uint64_t kept_sh;
+    __shared__ int nkeep_sh, stop_sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t w = tid; w < cb; w += blockDim.x) removed[w] = 0;
+    if (tid == 0) { nkeep_sh = 0; stop_sh = 0; }
+    __syncthreads();
+    for (int64_t blk = 0; blk < cb; ++blk) {
+        if (wave == 0) {
+            const int64_t row = blk * 64 + lane;
+            uint64_t key = row < N ? keys[row] : ~0ull;
+            const bool valid = row < N && (key >> 32) != 0xFFFFFFFFull;
+            const uint64_t diag = valid ? mask[row * cb + blk] : 0ull;
+            const uint64_t vmask = __ballot(valid);
+            uint64_t rem = removed[blk];
+            uint64_t kept = 0;
+            int nk = nkeep_sh;
+            const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+            for (int r = 0; r < 64; ++r) {
+                if (!((vmask >> r) & 1ull)) break;            // sorted: rest invalid
+                if (nk >= max_out) break;
+                if (!((rem >> r) & 1ull)) {
+                    kept |= (1ull << r);
+                    ++nk;
+                    const uint64_t d = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(dlo, r) |
+                                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(dhi, r) << 32);
+                    rem |= d;
+                }
+            }
+            if ((kept >> lane) & 1ull) {
+                const int pos = nkeep_sh + __popcll(kept & ((1ull << lane) - 1ull));
+                keep[pos] = (int32_t)(uint32_t)key;
+            }
+            if (lane == 0) {
+                kept_sh = kept;
+                nkeep_sh = nk;
+                if (nk >= max_out || vmask != ~0ull) stop_sh = 1;
+            }
+        }
+        __syncthreads();
+        if (stop_sh) break;
+        const uint64_t kept = kept_sh;
+        if (kept) {
+            for (int64_t w = blk + 1 + tid; w < cb; w += blockDim.x) {
+                uint64_t acc = removed[w];
+                uint64_t kk = kept;
+                while (kk) {
+                    const int r = __ffsll((long long)kk) - 1;
+                    kk &= kk - 1;
+                    acc |= mask[(blk * 64 + r) * cb + w];
+                }
+                removed[w] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *num_keep = nkeep_sh;
+}
+
+// ---- ProposalLayer ----------------------------------------------------------
+__global__ void score_keys_kernel(const float* __restrict__ probs, int64_t A,
+                                  int64_t* __restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A) return;
+    float s = probs[i * 2 + 1];
+    if (s == 0.0f) s = 0.0f;
+    const uint32_t o = float_ord(s) ^ 0x80000000u;   // signed-orderable
+    const uint64_t k = ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    keys[i] = (int64_t)k;
+}
+
+struct Std6 { float v[6]; };
+
+// core/models.py:391-447 with apply_box_deltas_graph (280-337).
+__global__ void proposal_decode_kernel(const float* __restrict__ probs,
+                                       const float* __restrict__ deltas,
+                                       const float* __restrict__ anchors,
+                                       const int64_t* __restrict__ order, int64_t k, Std6 sd,
+                                       float image_depth, float* __restrict__ boxes,
+                                       float* __restrict__ scores) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    const int64_t a = order[j];
+    scores[j] = probs[a * 2 + 1];
+    float d[6], an[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        float v = deltas[a * 6 + q] * sd.v[q];
+        v = smax(smin(v, 3.0f), -3.0f);     // ProposalLayer clip
+        d[q] = smax(smin(v, 3.0f), -3.0f);  // apply_box_deltas_graph clip
+        an[q] = anchors[a * 6 + q];
+    }
+    float height = an[3] - an[0], width = an[4] - an[1], depth = an[5] - an[2];
+    float cy = an[0] + 0.5f * height, cx = an[1] + 0.5f * width, cz = an[2] + 0.5f * depth;
+    cy = cy + d[0] * height;
+    cx = cx + d[1] * width;
+    cz = cz + d[2] * depth;
+    height = height * expf(d[3]);
+    width = width * expf(d[4]);
+    depth = depth * expf(d[5]);
+    const float y1 = cy - 0.5f * height, x1 = cx - 0.5f * width, z1 = cz - 0.5f * depth;
+    float r[6] = {y1, x1, z1, y1 + height, x1 + width, z1 + depth};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        r[q] = smax(smin(r[q], 1.0f), 0.0f);   // clip_by_value(result, 0, 1)
+        r[q] = smax(smin(r[q], 1.0f), 0.0f);   // clip_boxes_graph(window [0,0,0,1,1,1])
+    }
+    const float eps = 1e-6f;
+    const float img_depth = smax(image_depth, 1.0f);
+    const float min_d = smax(1.0f / img_depth, 1e-4f);
+    r[3] = smax(r[3], r[0] + eps);
+    r[4] = smax(r[4], r[1] + eps);
+    r[5] = smax(r[5], r[2] + min_d);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) boxes[j * 6 + q] = r[q];
+}
+
+__global__ void proposal_gather_kernel(const float* __restrict__ boxes,
+                                       const int32_t* __restrict__ keep,
+                                       const int32_t* __restrict__ num_keep, int P,
+                                       float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int nk = *num_keep;
+    for (int q = 0; q < 6; ++q) out[(int64_t)i * 6 + q] = i < nk ? boxes[(int64_t)keep[i] * 6 + q] : 0.0f;
+}
+
+static int64_t pow2_at_least(int64_t n) {
+    int64_t p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+struct NmsWs {
+    uint64_t* keys;
+    float* sboxes;
+    uint64_t* mask;
+    size_t bytes;
+};
+
+static NmsWs nms_ws_layout(int64_t N, void* base) {
+    NmsWs w;
+    const int64_t npad = pow2_at_least(N < 2 ? 2 : N);
+    const int64_t cb = (N + 63) / 64;
+    char* p = (char*)base;
+    size_t off = 0;
+    auto take = [&](size_t b) { size_t o = off; off += (b + 255) & ~(size_t)255; return p + o; };
+    w.keys = (uint64_t*)take(sizeof(uint64_t) * npad);
+    w.sboxes = (float*)take(sizeof(float) * 6 * (N > 0 ? N : 1));
+    w.mask = (uint64_t*)take(sizeof(uint64_t) * (size_t)(N > 0 ? N : 1) * (cb > 0 ? cb : 1));
+    w.bytes = off;
+    return w;
+}
+
+}  // namespace m3d
+
+using namespace m3d;
+
+extern "C" size_t m3d_nms3d_workspace_bytes(int64_t N) { return nms_ws_layout(N, nullptr).bytes; }
+
+extern "C" int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int32_t max_out,
+                         float iou_thr, int32_t mode, int32_t* keep, int32_t* num_keep,
+                         void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    if (!(iou_thr >= 0.0f && iou_thr <= 1.0f)) return einval("iou_threshold must be in [0, 1]");
+    if (mode != 0 && mode != 1) return einval("mode must be 0 (3-D) or 1 (2-D)");
+    if (N < 0) return einval("boxes must be 2-D");
+    if (N > (int64_t)0x7FFFFFFF) return einval("too many boxes");
+    const int64_t cb = (N + 63) / 64;
+    if (cb > 16384) return einval("too many boxes for the LDS-resident reduction (max 1048576)");
+    if (hipMemsetAsync(num_keep, 0, sizeof(int32_t), st(s)) != hipSuccess)
+        return check_launch("memset num_keep");
+    if (N == 0 || max_out <= 0) return M3D_OK;
+    NmsWs w = nms_ws_layout(N, workspace);
+    if (ws_bytes < w.bytes) return einval("workspace too small");
+    const int64_t npad = pow2_at_least(N < 2 ? 2 : N);
+    hipLaunchKernelGGL(nms_keys_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, st(s), scores, N,
+                       npad, w.keys);
+    int rc = check_launch("nms_keys_kernel");
+    if (rc) return rc;
+    if (npad <= 16384) {
+        hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(1024), sizeof(uint64_t) * npad, st(s),
+                           w.keys, (int)npad);
+        rc = check_launch("bitonic_lds_kernel");
+        if (rc) return rc;
+    } else {
+        for (int64_t k = 2; k <= npad; k <<= 1)
+            for (int64_t j = k >> 1; j > 0; j >>= 1) {
+                hipLaunchKernelGGL(bitonic_global_kernel, dim3(grid_for(npad / 2, 256)), dim3(256),
+                                   0, st(s), w.keys, npad, k, j);
+            }
+        rc = check_launch("bitonic_global_kernel");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(nms_gather_kernel, dim3(grid_for(N, 256)), dim3(256), 0, st(s), boxes,
+                       w.keys, N, mode == 1 ? 4 : 6, w.sboxes);
+    rc = check_launch("nms_gather_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nms_mask_kernel, dim3((unsigned)cb, (unsigned)cb), dim3(64), 0, st(s),
+                       w.sboxes, N, cb, iou_thr, mode, w.mask);
+    rc = check_launch("nms_mask_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nms_reduce_kernel, dim3(1), dim3(1024), sizeof(uint64_t) * cb, st(s),
+                       w.mask, w.keys, N, cb, max_out, keep, num_keep);
+    return check_launch("nms_reduce_kernel");
+}
+
+extern "C" int m3d_score_keys(const float* probs, int64_t A, int64_t* keys, m3d_stream_t s) {
+    if (A <= 0) return M3D_OK;
+    hipLaunchKernelGGL(score_keys_kernel, dim3(grid_for(A, 256)), dim3(256), 0, st(s), probs, A,
+                       keys);
+    return check_launch("score_keys_kernel");
+}
+
+extern "C" int m3d_proposal_decode(const float* probs, const float* deltas, const float* anchors,
+                                   const int64_t* order, int64_t k, const float std_dev[6],
+                                   float image_depth, float* boxes, float* scores,
+                                   m3d_stream_t s) {
+    if (k <= 0) return M3D_OK;
+    Std6 sd;
+    for (int q = 0; q < 6; ++q) sd.v[q] = std_dev[q];
+    hipLaunchKernelGGL(proposal_decode_kernel, dim3(grid_for(k, 256)), dim3(256), 0, st(s), probs,
+                       deltas, anchors, order, k, sd, image_depth, boxes, scores);
+    return check_launch("proposal_decode_kernel");
+}
+
+extern "C" int m3d_proposal_gather(const float* boxes, const int32_t* keep,
+                                   const int32_t* num_keep, int32_t P, float* proposals,
+                                   m3d_stream_t s) {
+    if (P <= 0) return M3D_OK;
+    hipLaunchKernelGGL(proposal_gather_kernel, dim3(grid_for(P, 256)), dim3(256), 0, st(s), boxes,
+                       keep, num_keep, P, proposals);
+    return check_launch("proposal_gather_kernel");
+}

@@ -1,0 +1,507 @@
+// 3-D CropAndResize / PyramidROIAlign kernels for gfx950.
+//
+// Replaces the CPU-only TF ops CropAndResize3D{,GradImage,GradBoxes} of the
+// vendored wheel and the PyramidROIAlign
+// layer glue (core/models.py:597-687).
+//
+// Mapping: one wave64 per output sample (n, y, x, z); the 64 lanes walk the
+// channel vector (C innermost, channels-last) with float4 accesses, so every
+// one of the 8 trilinear corner reads is a contiguous C*4-byte row (1 KiB per
+// wave-instruction at C=256) and every output store is coalesced.  The
+// coordinate maths runs redundantly in all lanes (wave-uniform values).
+//
+// Exactness: compiled with -ffp-contract=off; the coordinate / lerp op order
+// is the reference's, so trilinear outputs are bit-identical
+// to the CPU restatement (oracle/oracle.c).
+#include "common.h"
+
+namespace m3d {
+
+// ---- coordinate maths (whl @0x499a-0x4a62, @0x4abd, @0x5287) ----
+__device__ __forceinline__ float axis_scale(float b1, float b2, int S, int n) {
+    return n > 1 ? ((b2 - b1) * (float)(S - 1)) / (float)(n - 1) : 0.0f;
+}
+__device__ __forceinline__ float axis_coord(float b1, float b2, int S, int n, int i, float sc) {
+    if (n > 1) return b1 * (float)(S - 1) + (float)i * sc;
+    return (float)(0.5 * (double)(b1 + b2) * (double)(S - 1));
+}
+
+struct Sample {
+    int oob;              // 1 if the sample lies outside the image (extrapolate)
+    int ty, by, lx, rx, fz, kz;
+    float yl, xl, zl;
+    int ny, nx, nz;       // nearest indices
+};
+
+__device__ __forceinline__ Sample make_sample(const float* box, int H, int W, int D, int ch, int cw,
+                                              int cd, int y, int x, int z) {
+    Sample s;
+    const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
+    const float in_y = axis_coord(y1, y2, H, ch, y, axis_scale(y1, y2, H, ch));
+    const float in_x = axis_coord(x1, x2, W, cw, x, axis_scale(x1, x2, W, cw));
+    const float in_z = axis_coord(z1, z2, D, cd, z, axis_scale(z1, z2, D, cd));
+    s.oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1)) ||
+            (in_z < 0 || in_z > (float)(D - 1));
+    if (s.oob) return s;
+    s.ty = (int)floorf(in_y); s.by = (int)ceilf(in_y); s.yl = in_y - (float)s.ty;
+    s.lx = (int)floorf(in_x); s.rx = (int)ceilf(in_x); s.xl = in_x - (float)s.lx;
+    s.fz = (int)floorf(in_z); s.kz = (int)ceilf(in_z); s.zl = in_z - (float)s.fz;
+    s.ny = (int)roundf(in_y); s.nx = (int)roundf(in_x); s.nz = (int)roundf(in_z);
+    return s;
+}
+
+__device__ __forceinline__ float tri(float tlf, float tlk, float trf, float trk, float blf,
+                                     float blk, float brf, float brk, float yl, float xl,
+                                     float zl) {
+    // lerp order @0x4f88-0x5011: z first, then x, then y
+    const float tl = tlf + (tlk - tlf) * zl;
+    const float bl = blf + (blk - blf) * zl;
+    const float tr = trf + (trk - trf) * zl;
+    const float br = brf + (brk - brf) * zl;
+    const float top = tl + (tr - tl) * xl;
+    const float bot = bl + (br - bl) * xl;
+    return top + (bot - top) * yl;
+}
+
+__device__ __forceinline__ float scrub(float v) { return isfinite(v) ? v : 0.0f; }
+
+// Writes one output sample's C channels (lane-strided).  img points at image b.
+template <bool SCRUB>
+__device__ __forceinline__ void emit_sample(const float* __restrict__ img, int W, int D, int C,
+                                            const Sample& s, int method, float extrap,
+                                            float* __restrict__ o, int lane) {
+    if (s.oob) {
+        if ((C & 3) == 0) {
+            const float4 e = make_float4(extrap, extrap, extrap, extrap);
+            for (int c = lane; c < (C >> 2); c += 64) reinterpret_cast<float4*>(o)[c] = e;
+        } else {
+            for (int c = lane; c < C; c += 64) o[c] = extrap;
+        }
+        return;
+    }
+    const size_t rowD = (size_t)D * C, rowW = (size_t)W * rowD;
+    if (method == 1) {
+        const float* v = img + s.ny * rowW + s.nx * rowD + (size_t)s.nz * C;
+        for (int c = lane; c < C; c += 64) o[c] = SCRUB ? scrub(v[c]) : v[c];
+        return;
+    }
+    const float* tl = img + s.ty * rowW + s.lx * rowD;
+    const float* tr = img + s.ty * rowW + s.rx * rowD;
+    const float* bl = img + s.by * rowW + s.lx * rowD;
+    const float* br = img + s.by * rowW + s.rx * rowD;
+    const size_t f = (size_t)s.fz * C, k = (size_t)s.kz * C;
+    if ((C & 3) == 0) {
+        const float4 *tlf = (const float4*)(tl + f), *tlk = (const float4*)(tl + k);
+        const float4 *trf = (const float4*)(tr + f), *trk = (const float4*)(tr + k);
+        const float4 *blf = (const float4*)(bl + f), *blk = (const float4*)(bl + k);
+        const float4 *brf = (const float4*)(br + f), *brk = (const float4*)(br + k);
+        for (int c = lane; c < (C >> 2); c += 64) {
+            const float4 a = tlf[c], b = tlk[c], cc = trf[c], d = trk[c];
+            const float4 e = blf[c], g = blk[c], h = brf[c], i = brk[c];
+            float4 r;
+            r.x = tri(a.x, b.x, cc.x, d.x, e.x, g.x, h.x, i.x, s.yl, s.xl, s.zl);
+            r.y = tri(a.y, b.y, cc.y, d.y, e.y, g.y, h.y, i.y, s.yl, s.xl, s.zl);
+            r.z = tri(a.z, b.z, cc.z, d.z, e.z, g.z, h.z, i.z, s.yl, s.xl, s.zl);
+            r.w = tri(a.w, b.w, cc.w, d.w, e.w, g.w, h.w, i.w, s.yl, s.xl, s.zl);
+            if (SCRUB) { r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w); }
+            reinterpret_cast<float4*>(o)[c] = r;
+        }
+    } else {
+        for (int c = lane; c < C; c += 64) {
+            float r = tri(tl[f + c], tl[k + c], tr[f + c], tr[k + c], bl[f + c], bl[k + c],
+                          br[f + c], br[k + c], s.yl, s.xl, s.zl);
+            o[c] = SCRUB ? scrub(r) : r;
+        }
+    }
+}
+
+// Atomic scatter of one sample's gradient into the 8 corners (A.2 weights).
+__device__ __forceinline__ void scatter_sample(float* __restrict__ img, int W, int D, int C,
+                                               const Sample& s, int method,
+                                               const float* __restrict__ g, int lane) {
+    if (s.oob) return;
+    const size_t rowD = (size_t)D * C, rowW = (size_t)W * rowD;
+    if (method == 1) {
+        float* v = img + s.ny * rowW + s.nx * rowD + (size_t)s.nz * C;
+        for (int c = lane; c < C; c += 64) unsafeAtomicAdd(v + c, g[c]);
+        return;
+    }
+    const float wy[2] = {1.0f - s.yl, s.yl}, wx[2] = {1.0f - s.xl, s.xl},
+                wz[2] = {1.0f - s.zl, s.zl};
+    const int iy[2] = {s.ty, s.by}, ix[2] = {s.lx, s.rx}, iz[2] = {s.fz, s.kz};
+    float w[8];
+    float* dst[8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                w[a * 4 + b * 2 + c] = (wy[a] * wx[b]) * wz[c];
+                dst[a * 4 + b * 2 + c] = img + iy[a] * rowW + ix[b] * rowD + (size_t)iz[c] * C;
+            }
+    for (int c = lane; c < C; c += 64) {
+        const float gv = g[c];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) unsafeAtomicAdd(dst[q] + c, gv * w[q]);
+    }
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(256) void crop_fwd_kernel(const float* __restrict__ image, int B,
+                                                       int H, int W, int D, int C,
+                                                       const float* __restrict__ boxes,
+                                                       const int32_t* __restrict__ box_ind,
+                                                       int64_t total, int ch, int cw, int cd,
+                                                       int method, float extrap,
+                                                       float* __restrict__ crops) {
+    const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sidx >= total) return;
+    int64_t t = sidx;
+    const int z = (int)(t % cd); t /= cd;
+    const int x = (int)(t % cw); t /= cw;
+    const int y = (int)(t % ch);
+    const int64_t n = t / ch;
+    const Sample s = make_sample(boxes + n * 6, H, W, D, ch, cw, cd, y, x, z);
+    const float* img = image + (size_t)box_ind[n] * H * W * D * C;
+    emit_sample<false>(img, W, D, C, s, method, extrap, crops + sidx * C, lane);
+}
+
+__global__ __launch_bounds__(256) void crop_bwd_atomic_kernel(
+    const float* __restrict__ grads, const float* __restrict__ boxes,
+    const int32_t* __restrict__ box_ind, int64_t total, int ch, int cw, int cd, int H, int W,
+    int D, int C, int method, float* __restrict__ gimg) {
+    const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sidx >= total) return;
+    int64_t t = sidx;
+    const int z = (int)(t % cd); t /= cd;
+    const int x = (int)(t % cw); t /= cw;
+    const int y = (int)(t % ch);
+    const int64_t n = t / ch;
+    const Sample s = make_sample(boxes + n * 6, H, W, D, ch, cw, cd, y, x, z);
+    float* img = gimg + (size_t)box_ind[n] * H * W * D * C;
+    scatter_sample(img, W, D, C, s, method, grads + sidx * C, lane);
+}
+
+// Deterministic replay: one thread per (image b, channel c) walks every box of
+// image b in the reference order box -> y -> x -> z and accumulates the 8
+// corners sequentially (bit-identical to the reference summation order).
+__global__ __launch_bounds__(256) void crop_bwd_serial_kernel(
+    const float* __restrict__ grads, const float* __restrict__ boxes,
+    const int32_t* __restrict__ box_ind, int64_t N, int ch, int cw, int cd, int B, int H, int W,
+    int D, int C, int method, float* __restrict__ gimg) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (int64_t)B * C) return;
+    const int b = (int)(tid / C), c = (int)(tid % C);
+    float* img = gimg + (size_t)b * H * W * D * C;
+    const size_t rowD = (size_t)D * C, rowW = (size_t)W * rowD;
+    for (int64_t n = 0; n < N; ++n) {
+        if (box_ind[n] != b) continue;
+        for (int y = 0; y < ch; ++y)
+            for (int x = 0; x < cw; ++x)
+                for (int z = 0; z < cd; ++z) {
+                    const Sample s = make_sample(boxes + n * 6, H, W, D, ch, cw, cd, y, x, z);
+                    if (s.oob) continue;
+                    const float gv = grads[((((size_t)n * ch + y) * cw + x) * cd + z) * C + c];
+                    if (method == 1) {
+                        img[s.ny * rowW + s.nx * rowD + (size_t)s.nz * C + c] += gv;
+                        continue;
+                    }
+                    const float wy[2] = {1.0f - s.yl, s.yl}, wx[2] = {1.0f - s.xl, s.xl},
+                                wz[2] = {1.0f - s.zl, s.zl};
+                    const int iy[2] = {s.ty, s.by}, ix[2] = {s.lx, s.rx}, iz[2] = {s.fz, s.kz};
+                    for (int a = 0; a < 2; ++a)
+                        for (int bb = 0; bb < 2; ++bb)
+                            for (int cc = 0; cc < 2; ++cc) {
+                                const float w = (wy[a] * wx[bb]) * wz[cc];
+                                img[iy[a] * rowW + ix[bb] * rowD + (size_t)iz[cc] * C + c] +=
+                                    gv * w;
+                            }
+                }
+    }
+}
+
+// grad wrt boxes (TF CropAndResizeBackpropBoxes generalised to 3-D), one
+// workgroup per box, block reduction of the 6 partial sums.
+__global__ __launch_bounds__(256) void crop_bwd_boxes_kernel(
+    const float* __restrict__ grads, const float* __restrict__ image, int B, int H, int W, int D,
+    int C, const float* __restrict__ boxes, const int32_t* __restrict__ box_ind, int ch, int cw,
+    int cd, float* __restrict__ gboxes) {
+    const int n = blockIdx.x;
+    const float* bx = boxes + (size_t)n * 6;
+    const float y1 = bx[0], x1 = bx[1], z1 = bx[2], y2 = bx[3], x2 = bx[4], z2 = bx[5];
+    const float* img = image + (size_t)box_ind[n] * H * W * D * C;
+    const float hr = ch > 1 ? (float)(H - 1) / (float)(ch - 1) : 0.0f;
+    const float wr = cw > 1 ? (float)(W - 1) / (float)(cw - 1) : 0.0f;
+    const float dr = cd > 1 ? (float)(D - 1) / (float)(cd - 1) : 0.0f;
+    const float hs = ch > 1 ? (y2 - y1) * hr : 0.0f;
+    const float ws = cw > 1 ? (x2 - x1) * wr : 0.0f;
+    const float ds = cd > 1 ? (z2 - z1) * dr : 0.0f;
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    const size_t rowD = (size_t)D * C, rowW = (size_t)W * rowD;
+    const int64_t total = (int64_t)ch * cw * cd * C;
+    for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
+        const int c = (int)(e % C);
+        int64_t t = e / C;
+        const int z = (int)(t % cd); t /= cd;
+        const int x = (int)(t % cw);
+        const int y = (int)(t / cw);
+        const float in_y = axis_coord(y1, y2, H, ch, y, hs);
+        const float in_x = axis_coord(x1, x2, W, cw, x, ws);
+        const float in_z = axis_coord(z1, z2, D, cd, z, ds);
+        if (in_y < 0 || in_y > (float)(H - 1) || in_x < 0 || in_x > (float)(W - 1) ||
+            in_z < 0 || in_z > (float)(D - 1))
+            continue;
+        const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
+        const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+        const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+        const float yl = in_y - (float)ty, xl = in_x - (float)lx, zl = in_z - (float)fz;
+        const float tlf = img[ty * rowW + lx * rowD + (size_t)fz * C + c];
+        const float tlk = img[ty * rowW + lx * rowD + (size_t)kz * C + c];
+        const float trf = img[ty * rowW + rx * rowD + (size_t)fz * C + c];
+        const float trk = img[ty * rowW + rx * rowD + (size_t)kz * C + c];
+        const float blf = img[by * rowW + lx * rowD + (size_t)fz * C + c];
+        const float blk = img[by * rowW + lx * rowD + (size_t)kz * C + c];
+        const float brf = img[by * rowW + rx * rowD + (size_t)fz * C + c];
+        const float brk = img[by * rowW + rx * rowD + (size_t)kz * C + c];
+        const float tl = tlf + (tlk - tlf) * zl, tr = trf + (trk - trf) * zl;
+        const float bl = blf + (blk - blf) * zl, br = brf + (brk - brf) * zl;
+        float gy = (1 - xl) * (bl - tl) + xl * (br - tr);
+        float gx = (1 - yl) * (tr - tl) + yl * (br - bl);
+        const float dtl = tlk - tlf, dtr = trk - trf, dbl = blk - blf, dbr = brk - brf;
+        const float dtop = dtl + (dtr - dtl) * xl, dbot = dbl + (dbr - dbl) * xl;
+        float gz = dtop + (dbot - dtop) * yl;
+        const float tg = grads[((((size_t)n * ch + y) * cw + x) * cd + z) * C + c];
+        gy *= tg; gx *= tg; gz *= tg;
+        if (ch > 1) { acc[0] += gy * ((float)(H - 1) - (float)y * hr); acc[3] += gy * ((float)y * hr); }
+        else { acc[0] += gy * 0.5f * (float)(H - 1); acc[3] += gy * 0.5f * (float)(H - 1); }
+        if (cw > 1) { acc[1] += gx * ((float)(W - 1) - (float)x * wr); acc[4] += gx * ((float)x * wr); }
+        else { acc[1] += gx * 0.5f * (float)(W - 1); acc[4] += gx * 0.5f * (float)(W - 1); }
+        if (cd > 1) { acc[2] += gz * ((float)(D - 1) - (float)z * dr); acc[5] += gz * ((float)z * dr); }
+        else { acc[2] += gz * 0.5f * (float)(D - 1); acc[5] += gz * 0.5f * (float)(D - 1); }
+    }
+    __shared__ float red[6][256];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = acc[q];
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) gboxes[(size_t)n * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// ---- PyramidROIAlign ----------------------------------------------------------
+struct Pyr {
+    const float* fmaps[4];
+    float* gmaps[4];
+    int H[4], W[4], D[4];
+};
+
+// Box preparation + level assignment (core/models.py:611-649), one thread per (b,n).
+__global__ void pyramid_prep_kernel(const float* __restrict__ boxes,
+                                    const float* __restrict__ meta, int64_t meta_stride,
+                                    int64_t B, int64_t N, float* __restrict__ boxes_adj,
+                                    int32_t* __restrict__ levels) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * N) return;
+    const int64_t b = i / N;
+    const float* bx = boxes + i * 6;
+    float v[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) v[q] = smax(smin(bx[q], 1.0f), 0.0f);   // tf.clip_by_value
+    const float eps = 1e-6f;
+    v[3] = smax(v[3], v[0] + eps);
+    v[4] = smax(v[4], v[1] + eps);
+    const float* m = meta + b * meta_stride;
+    const float H = m[5], W = m[6], D = m[7];
+    const float min_dz = 1.0f / smax(D, 1.0f);
+    v[5] = smax(v[5], v[2] + min_dz);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) boxes_adj[i * 6 + q] = v[q];
+    const float h = v[3] - v[0], w = v[4] - v[1], d = v[5] - v[2];
+    const float image_area = (H * W) * D;
+    const float vol = (h * w) * d;
+    const float third = 0.333333343267440796f;          // (float)(1.0/3.0)
+    const float r = powf(vol, third) / (224.0f / powf(image_area, third));
+    const float ln2 = 0.693147182464599609375f;         // logf(2.0f)
+    const float lvl = rintf(logf(r) / ln2);              // tf.round: half to even
+    int li;
+    if (!isfinite(lvl)) li = 2;                          // (int)NaN/inf -> INT_MIN -> clamp 2
+    else {
+        int64_t l64 = 4 + (int64_t)lvl;
+        li = (int)(l64 < 2 ? 2 : (l64 > 5 ? 5 : l64));
+    }
+    levels[i] = li;
+}
+
+__global__ __launch_bounds__(256) void pyramid_fwd_kernel(Pyr P, int C,
+                                                          const float* __restrict__ boxes_adj,
+                                                          const int32_t* __restrict__ levels,
+                                                          int64_t N, int64_t total, int ph,
+                                                          int pw, int pd,
+                                                          float* __restrict__ out) {
+    const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sidx >= total) return;
+    int64_t t = sidx;
+    const int z = (int)(t % pd); t /= pd;
+    const int x = (int)(t % pw); t /= pw;
+    const int y = (int)(t % ph);
+    const int64_t bn = t / ph;
+    const int64_t b = bn / N;
+    const int l = levels[bn] - 2;
+    const int H = P.H[l], W = P.W[l], D = P.D[l];
+    const Sample s = make_sample(boxes_adj + bn * 6, H, W, D, ph, pw, pd, y, x, z);
+    const float* img = P.fmaps[l] + (size_t)b * H * W * D * C;
+    emit_sample<true>(img, W, D, C, s, 0, 0.0f, out + sidx * C, lane);
+}
+
+__global__ __launch_bounds__(256) void pyramid_bwd_kernel(Pyr P, int C,
+                                                          const float* __restrict__ boxes_adj,
+                                                          const int32_t* __restrict__ levels,
+                                                          int64_t N, int64_t total, int ph,
+                                                          int pw, int pd,
+                                                          const float* __restrict__ gout) {
+    const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sidx >= total) return;
+    int64_t t = sidx;
+    const int z = (int)(t % pd); t /= pd;
+    const int x = (int)(t % pw); t /= pw;
+    const int y = (int)(t % ph);
+    const int64_t bn = t / ph;
+    const int64_t b = bn / N;
+    const int l = levels[bn] - 2;
+    const int H = P.H[l], W = P.W[l], D = P.D[l];
+    const Sample s = make_sample(boxes_adj + bn * 6, H, W, D, ph, pw, pd, y, x, z);
+    float* img = P.gmaps[l] + (size_t)b * H * W * D * C;
+    scatter_sample(img, W, D, C, s, 0, gout + sidx * C, lane);
+}
+
+}  // namespace m3d
+
+using namespace m3d;
+
+static int check_crop_args(int64_t B, int64_t H, int64_t W, int64_t D, int64_t C, int32_t ch,
+                           int32_t cw, int32_t cd, int32_t method) {
+    if (B < 0 || H <= 0 || W <= 0 || D <= 0 || C <= 0)
+        return einval("image dimensions must be positive");
+    if (ch <= 0 || cw <= 0 || cd <= 0) return einval("crop dimensions must be positive");
+    if (method != 0 && method != 1) return einval("method must be 'trilinear' or 'nearest'");
+    return M3D_OK;
+}
+
+extern "C" int m3d_crop_and_resize3d_fwd(const float* image, int64_t B, int64_t H, int64_t W,
+                                         int64_t D, int64_t C, const float* boxes,
+                                         const int32_t* box_ind, int64_t N, int32_t ch,
+                                         int32_t cw, int32_t cd, int32_t method,
+                                         float extrapolation, float* crops, m3d_stream_t s) {
+    int rc = check_crop_args(B, H, W, D, C, ch, cw, cd, method);
+    if (rc) return rc;
+    const int64_t total = N * ch * cw * cd;
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(crop_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), image,
+                       (int)B, (int)H, (int)W, (int)D, (int)C, boxes, box_ind, total, ch, cw, cd,
+                       method, extrapolation, crops);
+    return check_launch("crop_fwd_kernel");
+}
+
+extern "C" int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* boxes,
+                                               const int32_t* box_ind, int64_t N, int32_t ch,
+                                               int32_t cw, int32_t cd, int64_t B, int64_t H,
+                                               int64_t W, int64_t D, int64_t C, int32_t method,
+                                               int32_t deterministic, float* grad_image,
+                                               m3d_stream_t s) {
+    int rc = check_crop_args(B, H, W, D, C, ch, cw, cd, method);
+    if (rc) return rc;
+    if (hipMemsetAsync(grad_image, 0, sizeof(float) * (size_t)(B * H * W * D * C), st(s)) !=
+        hipSuccess)
+        return check_launch("memset grad_image");
+    const int64_t total = N * ch * cw * cd;
+    if (total == 0 || B == 0) return M3D_OK;
+    if (deterministic) {
+        hipLaunchKernelGGL(crop_bwd_serial_kernel, dim3(grid_for(B * C, 256)), dim3(256), 0,
+                           st(s), grads, boxes, box_ind, N, ch, cw, cd, (int)B, (int)H, (int)W,
+                           (int)D, (int)C, method, grad_image);
+        return check_launch("crop_bwd_serial_kernel");
+    }
+    hipLaunchKernelGGL(crop_bwd_atomic_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s),
+                       grads, boxes, box_ind, total, ch, cw, cd, (int)H, (int)W, (int)D, (int)C,
+                       method, grad_image);
+    return check_launch("crop_bwd_atomic_kernel");
+}
+
+extern "C" int m3d_crop_and_resize3d_bwd_boxes(const float* grads, const float* image, int64_t B,
+                                               int64_t H, int64_t W, int64_t D, int64_t C,
+                                               const float* boxes, const int32_t* box_ind,
+                                               int64_t N, int32_t ch, int32_t cw, int32_t cd,
+                                               float* grad_boxes, m3d_stream_t s) {
+    int rc = check_crop_args(B, H, W, D, C, ch, cw, cd, 0);
+    if (rc) return rc;
+    if (N == 0) return M3D_OK;
+    hipLaunchKernelGGL(crop_bwd_boxes_kernel, dim3((unsigned)N), dim3(256), 0, st(s), grads,
+                       image, (int)B, (int)H, (int)W, (int)D, (int)C, boxes, box_ind, ch, cw, cd,
+                       grad_boxes);
+    return check_launch("crop_bwd_boxes_kernel");
+}
+
+static int make_pyr(Pyr& P, const float* const fmaps[4], float* const gmaps[4],
+                    const int64_t fshape[4][3]) {
+    for (int l = 0; l < 4; ++l) {
+        P.fmaps[l] = fmaps ? fmaps[l] : nullptr;
+        P.gmaps[l] = gmaps ? gmaps[l] : nullptr;
+        P.H[l] = (int)fshape[l][0];
+        P.W[l] = (int)fshape[l][1];
+        P.D[l] = (int)fshape[l][2];
+        if (P.H[l] <= 0 || P.W[l] <= 0 || P.D[l] <= 0)
+            return einval("feature map dimensions must be positive");
+    }
+    return M3D_OK;
+}
+
+extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
+                                           const int64_t fshape[4][3], int64_t C,
+                                           const float* boxes, const float* image_meta,
+                                           int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
+                                           int32_t pw, int32_t pd, float* out, float* boxes_adj,
+                                           int32_t* levels, m3d_stream_t s) {
+    Pyr P;
+    int rc = make_pyr(P, fmaps, nullptr, fshape);
+    if (rc) return rc;
+    if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
+    if (meta_stride < 8) return einval("image_meta must have at least 8 columns");
+    if (B * N == 0) return M3D_OK;
+    hipLaunchKernelGGL(pyramid_prep_kernel, dim3(grid_for(B * N, 256)), dim3(256), 0, st(s),
+                       boxes, image_meta, meta_stride, B, N, boxes_adj, levels);
+    rc = check_launch("pyramid_prep_kernel");
+    if (rc) return rc;
+    const int64_t total = B * N * ph * pw * pd;
+    hipLaunchKernelGGL(pyramid_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
+                       (int)C, boxes_adj, levels, N, total, ph, pw, pd, out);
+    return check_launch("pyramid_fwd_kernel");
+}
+
+extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
+                                           const int32_t* levels, int64_t B, int64_t N,
+                                           int32_t ph, int32_t pw, int32_t pd,
+                                           float* const gmaps[4], const int64_t fshape[4][3],
+                                           int64_t C, m3d_stream_t s) {
+    Pyr P;
+    int rc = make_pyr(P, nullptr, gmaps, fshape);
+    if (rc) return rc;
+    for (int l = 0; l < 4; ++l)
+        if (hipMemsetAsync(gmaps[l], 0,
+                           sizeof(float) * (size_t)(B * P.H[l] * P.W[l] * P.D[l] * C),
+                           st(s)) != hipSuccess)
+            return check_launch("memset gmaps");
+    const int64_t total = B * N * ph * pw * pd;
+    if (total == 0) return M3D_OK;
+    hipLaunchKernelGGL(pyramid_bwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
+                       (int)C, boxes_adj, levels, N, total, ph, pw, pd, grad_out);
+    return check_launch("pyramid_bwd_kernel");
+}

@@ -1,0 +1,109 @@
+"""ctypes binding of libm3d.so (the C-ABI declared in include/m3d.h).
+
+torch is imported first on purpose: libm3d.so links libamdhip64.so.7 and must
+bind to the HIP runtime torch already loaded (same SONAME), never to a second
+copy from /opt/rocm.  There is no fallback: if the library is missing or fails
+to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libm3d.so")
+
+_lib = None
+
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_f = ctypes.c_float
+c_p = ctypes.c_void_p
+c_sz = ctypes.c_size_t
+
+# name -> argtypes (all return int unless listed in _RESTYPES)
+_SIGS = {
+    "m3d_last_error": [],
+    "m3d_abi_version": [],
+    "m3d_crop_and_resize3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64,
+                                  c_i32, c_i32, c_i32, c_i32, c_f, c_p, c_p],
+    "m3d_crop_and_resize3d_bwd_image": [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64,
+                                        c_i64, c_i64, c_i64, c_i32, c_i32, c_p, c_p],
+    "m3d_crop_and_resize3d_bwd_boxes": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
+                                        c_i64, c_i32, c_i32, c_i32, c_p, c_p],
+    "m3d_pyramid_roi_align3d_fwd": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_i32,
+                                    c_i32, c_p, c_p, c_p, c_p],
+    "m3d_pyramid_roi_align3d_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p,
+                                    c_i64, c_p],
+    "m3d_nms3d_workspace_bytes": [c_i64],
+    "m3d_nms3d": [c_p, c_p, c_i64, c_i32, c_f, c_i32, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_score_keys": [c_p, c_i64, c_p, c_p],
+    "m3d_proposal_decode": [c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p],
+    "m3d_proposal_gather": [c_p, c_p, c_p, c_i32, c_p, c_p],
+    "m3d_conv3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_i32, c_i64,
+                       c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p,
+                       c_p, c_p, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_i64, c_i64, c_p],
+    "m3d_conv3d_bwd_data": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
+                            c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                            c_p, c_i32, c_p],
+    "m3d_conv3d_bwd_weight": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
+                              c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                              c_p, c_p],
+    "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
+                          c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
+    "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
+                          c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p],
+    "m3d_upsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p],
+    "m3d_subsample221_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "m3d_subsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
+                       c_p, c_p, c_p],
+    "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p],
+}
+_RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz}
+
+EXPORTED = tuple(_SIGS)
+
+
+class M3DError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libm3d.so and attach signatures.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise M3DError(
+            f"libm3d.so not found at {path}: build it with `make -C 3d-mask-r-cnn_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == 0:
+        return
+    msg = load().m3d_last_error().decode()
+    if rc == -1:
+        raise ValueError(msg)
+    raise M3DError(f"{what}: {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (0/None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

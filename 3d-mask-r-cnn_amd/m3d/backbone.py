@@ -1,0 +1,166 @@
+"""ResNet-3D backbone, FPN and RPN head on the libm3d kernels.
+
+Structure and layer names follow the reference exactly:
+  resnet_graph / conv_block / identity_block / BatchNorm  core/models.py:102-273
+  FPN top-down + smoothing + P6                             core/models.py:3190-3214
+  rpn_graph / build_rpn_model                               core/models.py:512-584
+Depth is never strided (all strides (2,2,1)), BN runs in inference mode with
+trainable gamma/beta (TRAIN_BN=False), every conv has a bias.
+"""
+from __future__ import annotations
+
+import torch
+
+from .nn import _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
+from .params import BNLayer, ConvLayer
+
+
+class _Unit:
+    """Conv3D + BatchNorm pair with its geometry chosen at call time."""
+
+    def __init__(self, store, conv_name, bn_name, k, cin, cout, stride, padding):
+        self.conv = ConvLayer(store, conv_name, k, cin, cout)
+        self.bn = BNLayer(store, bn_name, cout)
+        self.stride, self.padding = tuple(stride), padding
+
+    def __call__(self, x, relu, residual=None, need_dx=True):
+        geo = conv_geom(tuple(x.shape[1:4]), self.conv.k, self.stride, self.padding)
+        return conv_bn_act(x, self.conv, geo, relu, residual=residual,
+                           res_mode=1 if residual is not None else 0, bn=self.bn, need_dx=need_dx)
+
+
+class _Block:
+    """conv_block (shortcut conv) or identity_block (core/models.py:157-232)."""
+
+    def __init__(self, store, cin, filters, stage, block, strides, shortcut):
+        f1, f2, f3 = filters
+        c, b = f"res{stage}{block}_branch", f"bn{stage}{block}_branch"
+        self.a = _Unit(store, c + "2a", b + "2a", (1, 1, 1), cin, f1, strides, "valid")
+        self.b = _Unit(store, c + "2b", b + "2b", (3, 3, 3), f1, f2, (1, 1, 1), "same")
+        self.c = _Unit(store, c + "2c", b + "2c", (1, 1, 1), f2, f3, (1, 1, 1), "valid")
+        self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
+
+    def __call__(self, x):
+        short = self.sc(x, relu=False) if self.sc is not None else x
+        y = self.a(x, relu=True)
+        y = self.b(y, relu=True)
+        return self.c(y, relu=True, residual=short)
+
+
+class ResNet3D:
+    """resnet_graph(input_image, architecture, stage5, train_bn) -> [C1..C5]."""
+
+    def __init__(self, store, architecture="resnet50", stage5=True, train_bn=False):
+        assert architecture in ("resnet50", "resnet101")
+        if train_bn:
+            raise NotImplementedError("TRAIN_BN=True (batch-statistics BN) is not on the hot path")
+        self.stem = _Unit(store, "conv1", "bn_conv1", (7, 7, 7), 1, 64, (2, 2, 1), 3)
+        s = (2, 2, 1)
+        self.stages = []
+        spec = [(2, [64, 64, 256], 3, (1, 1, 1)), (3, [128, 128, 512], 4, s),
+                (4, [256, 256, 1024], {"resnet50": 6, "resnet101": 23}[architecture], s)]
+        if stage5:
+            spec.append((5, [512, 512, 2048], 3, s))
+        cin = 64
+        for stage, filters, n, strides in spec:
+            blocks = [_Block(store, cin, filters, stage, "a", strides, True)]
+            for i in range(n - 1):
+                blocks.append(_Block(store, filters[2], filters, stage, chr(98 + i), (1, 1, 1), False))
+            cin = filters[2]
+            self.stages.append(blocks)
+        self.stage5 = stage5
+
+    def __call__(self, image):
+        x = self.stem(image, relu=True, need_dx=False)
+        c1 = x = max_pool3d(x, (3, 3, 3), (2, 2, 1), "same")
+        outs = [c1]
+        for blocks in self.stages:
+            for blk in blocks:
+                x = blk(x)
+            outs.append(x)
+        if not self.stage5:
+            outs.append(None)
+        return outs
+
+
+def resnet_graph(input_image, architecture, stage5=False, train_bn=False, store=None, model=None):
+    """Functional form of the reference's resnet_graph; pass a built ResNet3D as ``model``."""
+    if model is None:
+        raise ValueError("resnet_graph needs a ResNet3D built on a ParamStore (model=...)")
+    return model(input_image)
+
+
+class FPN:
+    """Top-down pathway of RPN.build (core/models.py:3190-3214)."""
+
+    def __init__(self, store, size=256, c_channels=(256, 512, 1024, 2048)):
+        c2, c3, c4, c5 = c_channels
+        self.c5p5 = ConvLayer(store, "fpn_c5p5", (1, 1, 1), c5, size)
+        self.c4p4 = ConvLayer(store, "fpn_c4p4", (1, 1, 1), c4, size)
+        self.c3p3 = ConvLayer(store, "fpn_c3p3", (1, 1, 1), c3, size)
+        self.c2p2 = ConvLayer(store, "fpn_c2p2", (1, 1, 1), c2, size)
+        self.p = [ConvLayer(store, f"fpn_p{i}", (3, 3, 3), size, size) for i in (2, 3, 4, 5)]
+
+    @staticmethod
+    def _c(x, layer, k, padding, residual=None):
+        geo = conv_geom(tuple(x.shape[1:4]), k, (1, 1, 1), padding)
+        return conv_bn_act(x, layer, geo, relu=False, residual=residual,
+                           res_mode=2 if residual is not None else 0)
+
+    def __call__(self, C2, C3, C4, C5):
+        P5 = self._c(C5, self.c5p5, (1, 1, 1), "valid")
+        P4 = self._c(C4, self.c4p4, (1, 1, 1), "valid", residual=P5)   # up(P5) + c4p4(C4)
+        P3 = self._c(C3, self.c3p3, (1, 1, 1), "valid", residual=P4)
+        P2 = self._c(C2, self.c2p2, (1, 1, 1), "valid", residual=P3)
+        P2, P3, P4, P5 = (self._c(x, l, (3, 3, 3), "same") for x, l in zip((P2, P3, P4, P5), self.p))
+        P6 = subsample221(P5)
+        return [P2, P3, P4, P5, P6]
+
+
+class RPNHead:
+    """build_rpn_model(anchor_stride, anchors_per_location, channel): one shared
+    head applied to every pyramid level (core/models.py:512-584)."""
+
+    def __init__(self, store, anchor_stride, anchors_per_location, channel):
+        if anchor_stride != 1:
+            raise NotImplementedError("RPN_ANCHOR_STRIDE != 1")
+        self.apl = anchors_per_location
+        self.shared1 = ConvLayer(store, "rpn_conv_shared1", (3, 3, 3), channel, 512)
+        self.shared2 = ConvLayer(store, "rpn_conv_shared2", (1, 1, 1), 512, 256)
+        self.cls = ConvLayer(store, "rpn_class_raw", (1, 1, 1), 256, 2 * self.apl)
+        self.bbox = ConvLayer(store, "rpn_bbox_pred", (1, 1, 1), 256, 6 * self.apl,
+                              kernel_init=("normal", 0.001))
+        self.w_grad = None
+        self.b_grad = None
+
+    def __call__(self, feature_maps):
+        shared = []
+        for p in feature_maps:
+            g1 = conv_geom(tuple(p.shape[1:4]), (3, 3, 3), (1, 1, 1), "same")
+            s = conv_bn_act(p, self.shared1, g1, relu=True)
+            g2 = conv_geom(tuple(s.shape[1:4]), (1, 1, 1), (1, 1, 1), "valid")
+            shared.append(conv_bn_act(s, self.shared2, g2, relu=True))
+        apl = self.apl
+        cin = 256
+        w24 = torch.cat([self.cls.kernel.data.reshape(cin, 2 * apl),
+                         self.bbox.kernel.data.reshape(cin, 6 * apl)], dim=1).contiguous()
+        b24 = torch.cat([self.cls.bias.data, self.bbox.bias.data]).contiguous()
+        npad = -(-8 * apl // 32) * 32
+        self.w_grad = torch.zeros((cin, npad), device=w24.device, dtype=torch.float32)
+        self.b_grad = torch.zeros((npad,), device=w24.device, dtype=torch.float32)
+        logits, bbox = _RPNOut.apply(w24, b24, {"kernel": self.w_grad, "bias": self.b_grad}, apl,
+                                     *shared)
+        probs = torch.softmax(logits, dim=-1)
+        return logits, probs, bbox
+
+    def finish_backward(self):
+        """Fold the padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
+        if self.w_grad is None:
+            return
+        apl, cin = self.apl, 256
+        with torch.no_grad():
+            self.cls.kernel.grad.view(cin, 2 * apl).add_(self.w_grad[:, :2 * apl])
+            self.bbox.kernel.grad.view(cin, 6 * apl).add_(self.w_grad[:, 2 * apl:8 * apl])
+            self.cls.bias.grad.add_(self.b_grad[:2 * apl])
+            self.bbox.bias.grad.add_(self.b_grad[2 * apl:8 * apl])
+        self.w_grad = self.b_grad = None

@@ -1,0 +1,65 @@
+"""Keras-layer surface of the hot path (drop-in for core/models.py callers).
+
+``ProposalLayer(proposal_count, nms_threshold, pre_nms_limit, images_per_gpu,
+rpn_bbox_std_dev, image_depth, name=...)([rpn_class, rpn_bbox, anchors])``
+and ``PyramidROIAlign(pool_shape, name=...)([boxes, image_meta, P2..P5])``
+take the reference's constructor arguments and call signature
+(core/models.py:369-503, 597-687) and run entirely on the GPU: top-k with TF's
+tie order, fused delta decode, bit-exact 3-D NMS and zero padding without a
+host round trip; fused multi-level trilinear ROI align in original order.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+class ProposalLayer:
+    def __init__(self, proposal_count, nms_threshold, pre_nms_limit, images_per_gpu,
+                 rpn_bbox_std_dev, image_depth, name="ROI", **kwargs):
+        self.proposal_count = int(proposal_count)
+        self.nms_threshold = float(nms_threshold)
+        self.pre_nms_limit = int(pre_nms_limit)
+        self.images_per_gpu = int(images_per_gpu)
+        self.rpn_bbox_std_dev = [float(v) for v in rpn_bbox_std_dev]
+        self.image_depth = int(image_depth)
+        self.name = name
+
+    def __call__(self, inputs, return_counts=False):
+        probs, deltas, anchors = inputs
+        B, A = probs.shape[:2]
+        k = min(self.pre_nms_limit, anchors.shape[1])
+        out = torch.empty((B, self.proposal_count, 6), device=probs.device, dtype=torch.float32)
+        counts = []
+        with torch.no_grad():
+            for b in range(B):
+                pb = probs[b].detach().float().contiguous()
+                db = deltas[b].detach().float().contiguous()
+                ab = anchors[b if anchors.shape[0] > 1 else 0].detach().float().contiguous()
+                order = ops.topk_order(pb, k)
+                boxes, scores = ops.proposal_decode(pb, db, ab, order, self.rpn_bbox_std_dev,
+                                                    self.image_depth)
+                keep, num = ops.non_max_suppression_3d_padded(boxes, scores, self.proposal_count,
+                                                              self.nms_threshold)
+                out[b] = ops.proposal_gather(boxes, keep, num, self.proposal_count)
+                counts.append(num)
+        if return_counts:
+            return out, torch.cat(counts)
+        return out
+
+    def compute_output_shape(self, input_shape):
+        return (None, self.proposal_count, 6)
+
+
+class PyramidROIAlign:
+    def __init__(self, pool_shape, name=None, **kwargs):
+        self.pool_shape = tuple(int(v) for v in pool_shape)
+        self.name = name
+
+    def __call__(self, inputs):
+        boxes, image_meta = inputs[0], inputs[1]
+        return ops.pyramid_roi_align(boxes, image_meta, list(inputs[2:6]), self.pool_shape)
+
+    def compute_output_shape(self, input_shape):
+        return tuple(input_shape[0][:2]) + self.pool_shape + (input_shape[2][-1],)

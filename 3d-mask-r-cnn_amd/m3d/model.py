@@ -1,0 +1,193 @@
+"""RPN training model (RPN.build / compile / one fit step) on the libm3d kernels.
+
+Mirrors core/models.py:3162-3387:
+  inputs [image, rpn_match, rpn_bbox] -> resnet_graph(stage5) -> FPN -> shared
+  RPN head on P2..P6 -> (rpn_class_logits, rpn_class, rpn_bbox) -> ProposalLayer
+  (POST_NMS_ROIS_TRAINING) -> rpn_class_loss (focal CE, 1589-1625) and
+  rpn_bbox_loss (XY/Z Huber, 1629-1673), weighted 1.0 / 1.5 (3366-3376), plus
+  the L2 term WEIGHT_DECAY*0.5*||w||^2/size(w) on every non-gamma/beta weight
+  (3378-3384), optimised by Keras SGD (momentum, clipnorm, decay).
+The two losses are tiny gathers over <= RPN_TRAIN_ANCHORS_PER_IMAGE anchors and
+run as torch ops on the GPU; all convolution / pooling / NMS work is libm3d.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .anchors import get_anchors
+from .backbone import FPN, ResNet3D, RPNHead
+from .layers import ProposalLayer
+from .params import ParamStore
+
+
+# ---------------------------------------------------------------------------
+# losses
+# ---------------------------------------------------------------------------
+class RPNTargets:
+    """Host-side prepared RPN targets: the tf.where index sets of the loss
+    graphs are fixed per batch, so they are built once on the host (where
+    rpn_match is produced) instead of a device nonzero() + sync."""
+
+    def __init__(self, rpn_match, rpn_bbox, device):
+        m = np.asarray(rpn_match).reshape(rpn_match.shape[0], -1)
+        B, A = m.shape
+        flat = m.reshape(-1)
+        cls_idx = np.nonzero(flat != 0)[0]                       # tf.where row-major order
+        pos_idx = np.nonzero(flat == 1)[0]
+        counts = (m == 1).sum(axis=1)
+        rb = np.asarray(rpn_bbox, np.float32)
+        gt = np.concatenate([rb[b, :counts[b]] for b in range(B)], axis=0) if B else rb[:0, 0]
+        self.cls_idx = torch.from_numpy(cls_idx.astype(np.int64)).to(device)
+        self.cls_labels = torch.from_numpy((flat[cls_idx] == 1).astype(np.int64)).to(device)
+        self.pos_idx = torch.from_numpy(pos_idx.astype(np.int64)).to(device)
+        self.gt_bbox = torch.from_numpy(gt.reshape(-1, 6).astype(np.float32)).to(device)
+        self.n_cls, self.n_pos = len(cls_idx), len(pos_idx)
+
+
+def rpn_class_loss(t: RPNTargets, rpn_class_logits, alpha=0.90, gamma=1.5):
+    """core/models.py:1589-1625."""
+    if t.n_cls == 0:
+        return rpn_class_logits.sum() * 0.0
+    logits = rpn_class_logits.reshape(-1, 2).index_select(0, t.cls_idx)
+    ce = torch.nn.functional.cross_entropy(logits, t.cls_labels, reduction="none")
+    probs = torch.softmax(logits, dim=-1)
+    p_t = probs.gather(1, t.cls_labels[:, None])[:, 0]
+    ce = torch.pow(1.0 - p_t, gamma) * ce
+    alpha_t = torch.where(t.cls_labels == 1, torch.full_like(ce, alpha), torch.full_like(ce, 1.0 - alpha))
+    return (alpha_t * ce).mean()
+
+
+def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
+    """core/models.py:1629-1673."""
+    if t.n_pos == 0:
+        return rpn_bbox.sum() * 0.0
+    pred = rpn_bbox.reshape(-1, 6).index_select(0, t.pos_idx).clamp(-5.0, 5.0)
+    diff = (t.gt_bbox - pred).clamp(-2.0, 2.0)
+    ad = diff.abs()
+    xy = torch.tensor([1., 1., 0., 1., 1., 0.], device=diff.device)
+    zm = torch.tensor([0., 0., 1., 0., 0., 1.], device=diff.device)
+    h_xy = torch.where(ad < 1.0, 0.5 * diff * diff, ad - 0.5) * xy
+    h_z = torch.where(ad < 0.5, 0.5 * diff * diff, 0.5 * ad - 0.25) * zm
+    return (h_xy + h_z).mean()
+
+
+# ---------------------------------------------------------------------------
+# model
+# ---------------------------------------------------------------------------
+class RPN:
+    """The RPN of the reference in training mode, built on a flat ParamStore."""
+
+    LOSS_WEIGHTS = {"rpn_class_loss": 1.0, "rpn_bbox_loss": 1.5}   # core/models.py:3366-3369
+
+    def __init__(self, config, device="cuda", seed=1):
+        h, w = int(config.IMAGE_SHAPE[0]), int(config.IMAGE_SHAPE[1])
+        if h % 64 or w % 64:
+            raise ValueError("IMAGE_SHAPE height & width must be multiples of 64")
+        _lib.load()
+        self.config = config
+        self.device = torch.device(device)
+        self.store = ParamStore()
+        self.backbone = ResNet3D(self.store, config.BACKBONE, stage5=True, train_bn=config.TRAIN_BN)
+        self.fpn = FPN(self.store, config.TOP_DOWN_PYRAMID_SIZE)
+        self.rpn = RPNHead(self.store, config.RPN_ANCHOR_STRIDE, len(config.RPN_ANCHOR_RATIOS),
+                           config.TOP_DOWN_PYRAMID_SIZE)
+        self.store.finalize(self.device, seed=seed, weight_decay=float(config.WEIGHT_DECAY))
+        self.anchors = torch.from_numpy(get_anchors(config)).to(self.device)[None]
+        self.proposal_layer = ProposalLayer(
+            proposal_count=config.POST_NMS_ROIS_TRAINING, nms_threshold=config.RPN_NMS_THRESHOLD,
+            pre_nms_limit=config.PRE_NMS_LIMIT, images_per_gpu=config.IMAGES_PER_GPU,
+            rpn_bbox_std_dev=config.RPN_BBOX_STD_DEV, image_depth=config.IMAGE_DEPTH, name="ROI")
+        opt = dict(config.OPTIMIZER.get("parameters", {}))
+        self.lr = float(opt.get("learning_rate", opt.get("lr", 0.01)))
+        self.momentum = float(opt.get("momentum", 0.0))
+        self.clipnorm = float(opt.get("clipnorm", 0.0))
+        self.decay = float(opt.get("decay", 0.0))
+        self.iterations = 0
+        name = str(config.OPTIMIZER.get("name", "SGD")).upper()
+        if name != "SGD":
+            raise NotImplementedError(f"optimizer {name}: only the SGD path is implemented")
+
+    # -- forward ----------------------------------------------------------
+    def features(self, image):
+        _, C2, C3, C4, C5 = self.backbone(image)
+        return self.fpn(C2, C3, C4, C5)
+
+    def forward(self, image, proposals=True):
+        fmaps = self.features(image)
+        logits, probs, bbox = self.rpn(fmaps)
+        rois = None
+        if proposals:
+            rois = self.proposal_layer([probs, bbox, self.anchors])
+        return {"rpn_class_logits": logits, "rpn_class": probs, "rpn_bbox": bbox,
+                "rpn_rois": rois, "feature_maps": fmaps}
+
+    def losses(self, out, targets: RPNTargets):
+        lc = rpn_class_loss(targets, out["rpn_class_logits"])
+        lb = rpn_bbox_loss(targets, out["rpn_bbox"])
+        return lc, lb
+
+    # -- one fit step -----------------------------------------------------
+    def current_lr(self):
+        return self.lr * (1.0 / (1.0 + self.decay * self.iterations))
+
+    def train_step(self, image, targets: RPNTargets, proposals=True):
+        self.store.zero_grad()
+        out = self.forward(image, proposals=proposals)
+        lc, lb = self.losses(out, targets)
+        total = lc * self.LOSS_WEIGHTS["rpn_class_loss"] + lb * self.LOSS_WEIGHTS["rpn_bbox_loss"]
+        total.backward()
+        self.rpn.finish_backward()
+        self.sgd_step()
+        return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
+                "rpn_rois": out["rpn_rois"]}
+
+    def sgd_step(self):
+        s = self.store
+        L = _lib.load()
+        _lib.check(L.m3d_sgd_keras(s.flat.data_ptr(), s.grad_flat.data_ptr(), s.moments.data_ptr(),
+                                   s.n_chunks, s.seg_of_chunk.data_ptr(), s.l2_coef.data_ptr(),
+                                   len(s.params), float(self.current_lr()), self.momentum,
+                                   self.clipnorm, s.norms.data_ptr(), _lib.stream()), "sgd")
+        self.iterations += 1
+
+    def l2_loss(self):
+        with torch.no_grad():
+            tot = torch.zeros((), device=self.device)
+            for p in self.store.params:
+                if p.l2:
+                    tot = tot + (self.config.WEIGHT_DECAY * 0.5) * (p.data * p.data).sum() / p.numel
+            return tot
+
+
+# ---------------------------------------------------------------------------
+# synthetic inputs
+# ---------------------------------------------------------------------------
+def synthetic_volume(size, depth=None, batch=1, seed=0):
+    """x = tanh(0.5 * N(0,1)), [B,S,S,D,1] float32 (range of core/data_generators.py:1612-1628)."""
+    g = torch.Generator().manual_seed(seed)
+    d = size if depth is None else depth
+    return torch.tanh(0.5 * torch.randn((batch, size, size, d, 1), generator=g))
+
+
+def synthetic_rpn_targets(n_anchors, n_train=1536, pos_frac=0.5, batch=1, seed=2):
+    """Seeded rpn_match [B,A,1] (+1/-1/0) with <= n_train non-zero entries and
+    rpn_bbox [B,n_train,6] delta targets (std-normalised scale).  Stands in for
+    the host target builder (core/data_generators.py:2031-2178, out of scope)."""
+    rng = np.random.default_rng(seed)
+    match = np.zeros((batch, n_anchors, 1), np.int32)
+    bbox = np.zeros((batch, n_train, 6), np.float32)
+    for b in range(batch):
+        sel = rng.choice(n_anchors, size=min(n_train, n_anchors), replace=False)
+        npos = int(len(sel) * pos_frac)
+        match[b, sel[:npos], 0] = 1
+        match[b, sel[npos:], 0] = -1
+        bbox[b, :npos] = rng.normal(0.0, 1.0, size=(npos, 6)).astype(np.float32)
+    return match, bbox
+
+
+def compose_image_meta(image_id, original_shape, image_shape, window, scale, active_class_ids):
+    """core/models.py compose_image_meta layout: [id, orig(4), shape(4), window(6), scale, classes]."""
+    return np.array([image_id] + list(original_shape) + list(image_shape) + list(window) + [scale] +
+                    list(active_class_ids), dtype=np.float32)

@@ -1,0 +1,288 @@
+"""Autograd functions of the backbone / FPN / RPN graph over libm3d.so.
+
+Parameters live in a flat ``ParamStore`` (see params.py); every function here
+accumulates its weight / bias / BN gradients straight into the parameter's
+gradient view with the kernels' atomics, so autograd only carries activation
+gradients.  Layout is channels-last [B,H,W,D,C] throughout, as the reference.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream
+
+
+def _L():
+    return _lib.load()
+
+
+def same_out_pad(n, k, s):
+    """TF 'SAME': out = ceil(n/s), pad_before = floor(max((out-1)s+k-n, 0)/2)."""
+    out = -(-n // s)
+    total = max((out - 1) * s + k - n, 0)
+    return out, total // 2
+
+
+def valid_out(n, k, s):
+    return (n - k) // s + 1
+
+
+@dataclass
+class ConvGeom:
+    k: tuple
+    stride: tuple
+    pad: tuple        # pad-before per axis
+    out: tuple        # output spatial (OH, OW, OD)
+
+
+def conv_geom(in_sp, k, stride, padding):
+    """padding: 'same' | 'valid' | int (explicit symmetric zero padding, ZeroPadding3D)."""
+    k = tuple(k)
+    stride = tuple(stride)
+    if padding == "same":
+        op = [same_out_pad(n, kk, s) for n, kk, s in zip(in_sp, k, stride)]
+        return ConvGeom(k, stride, tuple(p for _, p in op), tuple(o for o, _ in op))
+    if padding == "valid":
+        return ConvGeom(k, stride, (0, 0, 0), tuple(valid_out(n, kk, s) for n, kk, s in zip(in_sp, k, stride)))
+    p = int(padding)
+    return ConvGeom(k, stride, (p, p, p),
+                    tuple(valid_out(n + 2 * p, kk, s) for n, kk, s in zip(in_sp, k, stride)))
+
+
+class _ConvBNAct(torch.autograd.Function):
+    """y = act(BN_frozen(conv(x, w) + b) [+ residual]).
+
+    res_mode 1: residual has y's shape; 2: residual is the (2,2,1)-nearest
+    source of y (FPN top-down add, core/models.py:3193-3204)."""
+
+    @staticmethod
+    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx):
+        B, H, W, D, Cin = x.shape
+        kh, kw, kd = geo.k
+        Cout = w.shape[-1]
+        OH, OW, OD = geo.out
+        y = torch.empty((B, OH, OW, OD, Cout), device=x.device, dtype=torch.float32)
+        z = None
+        scale = shift = None
+        if bn is not None:
+            gamma, beta, mean, var, eps = bn
+            rstd = torch.rsqrt(var + eps)
+            scale = gamma * rstd
+            shift = beta - mean * scale
+            if grads is not None and grads.get("gamma") is not None:
+                z = torch.empty_like(y)
+            ctx.bn = (mean, rstd, scale)
+        else:
+            ctx.bn = None
+        check(_L().m3d_conv3d_fwd(ptr(x), B, H, W, D, Cin, ptr(w), kh, kw, kd, Cout, OH, OW, OD,
+                                  *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
+                                  ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
+                                  None, 0, 0, stream()), "conv3d_fwd")
+        ctx.save_for_backward(x, w, y, z)
+        ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
+        ctx.res_shape = None if residual is None else tuple(residual.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y, z = ctx.saved_tensors
+        dy = dy.contiguous()
+        geo, grads = ctx.geo, ctx.grads or {}
+        B, H, W, D, Cin = x.shape
+        kh, kw, kd = geo.k
+        Cout = w.shape[-1]
+        OH, OW, OD = geo.out
+        M = B * OH * OW * OD
+        L = _L()
+        need_res = ctx.res_mode != 0
+        trivial = ctx.bn is None and not ctx.relu
+        if trivial:
+            dz = dy
+            dres = dy if need_res else None
+            if grads.get("bias") is not None:
+                check(L.m3d_bn_act_bwd(ptr(dy), None, None, M, Cout, 0, None, None, None, None,
+                                       None, 0, None, None, ptr(grads["bias"]), stream()), "bn_act_bwd")
+        else:
+            dz = torch.empty_like(dy)
+            dres = torch.empty_like(dy) if need_res else None
+            mean = rstd = scale = None
+            if ctx.bn is not None:
+                mean, rstd, scale = ctx.bn
+            check(L.m3d_bn_act_bwd(ptr(dy), ptr(y), ptr(z), M, Cout, 1 if ctx.relu else 0,
+                                   ptr(scale), ptr(mean), ptr(rstd), ptr(dz), ptr(dres), 0,
+                                   ptr(grads.get("beta")), ptr(grads.get("gamma")) if z is not None else None,
+                                   ptr(grads.get("bias")), stream()), "bn_act_bwd")
+        if grads.get("kernel") is not None:
+            check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
+                                          OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
+                                          stream()), "conv3d_bwd_weight")
+        dx = None
+        if ctx.need_dx:
+            strided = any(s != 1 for s in geo.stride)
+            dx = (torch.zeros if strided else torch.empty)(x.shape, device=x.device, dtype=torch.float32)
+            wd, dzd, cpad = w, dz, Cout
+            if Cout % 32:   # bwd-data stages 32-channel slices of dz: zero-pad the channel dim
+                cpad = -(-Cout // 32) * 32
+                wd = torch.zeros((kh, kw, kd, Cin, cpad), device=w.device, dtype=torch.float32)
+                wd[..., :Cout] = w
+                dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
+                dzd[..., :Cout] = dz
+            check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
+                                        OD, *geo.stride, *geo.pad, ptr(dx), 0, stream()),
+                  "conv3d_bwd_data")
+        dr = None
+        if need_res:
+            if ctx.res_mode == 1:
+                dr = dres
+            else:
+                rb, rh, rw, rd, rc = ctx.res_shape
+                dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
+                check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
+                      "upsample221_bwd")
+        return dx, dr, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True):
+    """Functional entry: ``layer`` is a Conv3D parameter group from params.py."""
+    w = layer.kernel.data
+    b = layer.bias.data if layer.bias is not None else None
+    grads = layer.grad_dict(bn)
+    bnt = None
+    if bn is not None:
+        bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)
+    if residual is not None:
+        residual = residual.contiguous()
+    # the function must see at least one tensor requiring grad to be recorded
+    return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
+                            need_dx and x.requires_grad)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad, out):
+        B, H, W, D, C = x.shape
+        y = torch.empty((B, *out, C), device=x.device, dtype=torch.float32)
+        am = torch.empty((B, *out, C), device=x.device, dtype=torch.uint8)
+        check(_L().m3d_maxpool3d_fwd(ptr(x), B, H, W, D, C, *k, *stride, *pad, *out, ptr(y), ptr(am),
+                                     stream()), "maxpool3d_fwd")
+        ctx.save_for_backward(am)
+        ctx.cfg = (tuple(x.shape), k, stride, pad, out)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        shape, k, stride, pad, out = ctx.cfg
+        dx = torch.empty(shape, device=dy.device, dtype=torch.float32)
+        check(_L().m3d_maxpool3d_bwd(ptr(dy.contiguous()), ptr(am), *shape, *k, *stride, *pad, *out,
+                                     ptr(dx), stream()), "maxpool3d_bwd")
+        return dx, None, None, None, None
+
+
+def max_pool3d(x, k, stride, padding="same"):
+    """KL.MaxPooling3D(k, strides, padding) with TF SAME semantics."""
+    sp = x.shape[1:4]
+    if padding == "same":
+        op = [same_out_pad(n, kk, s) for n, kk, s in zip(sp, k, stride)]
+        out, pad = tuple(o for o, _ in op), tuple(p for _, p in op)
+    else:
+        out, pad = tuple(valid_out(n, kk, s) for n, kk, s in zip(sp, k, stride)), (0, 0, 0)
+    return _MaxPool.apply(x.contiguous(), tuple(k), tuple(stride), pad, out)
+
+
+class _Subsample221(torch.autograd.Function):
+    """P6 = MaxPooling3D(pool_size=(1,1,1), strides=(2,2,1)) (core/models.py:3211)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, H, W, D, C = x.shape
+        y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, D, C), device=x.device, dtype=torch.float32)
+        check(_L().m3d_subsample221_fwd(ptr(x), B, H, W, D, C, ptr(y), stream()), "subsample221")
+        ctx.shape = tuple(x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.zeros(ctx.shape, device=dy.device, dtype=torch.float32)
+        check(_L().m3d_subsample221_bwd(ptr(dy.contiguous()), *ctx.shape, ptr(dx), stream()),
+              "subsample221_bwd")
+        return dx
+
+
+def subsample221(x):
+    return _Subsample221.apply(x.contiguous())
+
+
+class _RPNOut(torch.autograd.Function):
+    """The RPN class/bbox 1x1x1 heads (rpn_class_raw, rpn_bbox_pred;
+    core/models.py:540-556) of all pyramid levels in one function.  Each level's
+    conv writes its rows straight into the level-concatenated outputs
+    rpn_class_logits [B,A,2] / rpn_bbox [B,A,6] (core/models.py:3250-3263)."""
+
+    @staticmethod
+    def forward(ctx, w24, b24, grads, apl, *shared):
+        dev = shared[0].device
+        B = shared[0].shape[0]
+        rows = [s.shape[1] * s.shape[2] * s.shape[3] for s in shared]
+        A = sum(rows) * apl
+        logits = torch.empty((B, A, 2), device=dev, dtype=torch.float32)
+        bbox = torch.empty((B, A, 6), device=dev, dtype=torch.float32)
+        Cin = shared[0].shape[-1]
+        L = _L()
+        for b in range(B):
+            off = 0
+            for s, r in zip(shared, rows):
+                xb = s[b:b + 1]
+                _, H, W, D, _ = xb.shape
+                check(L.m3d_conv3d_fwd(ptr(xb), 1, H, W, D, Cin, ptr(w24), 1, 1, 1, 8 * apl, H, W, D,
+                                       1, 1, 1, 0, 0, 0, ptr(b24), None, None, None, 0, 0, None,
+                                       logits[b].data_ptr() + off * apl * 2 * 4, 2 * apl,
+                                       bbox[b].data_ptr() + off * apl * 6 * 4, 6 * apl, 2 * apl,
+                                       stream()), "rpn_out_fwd")
+                off += r
+        ctx.save_for_backward(w24, *shared)
+        ctx.grads, ctx.rows, ctx.apl = grads, rows, apl
+        return logits, bbox
+
+    @staticmethod
+    def backward(ctx, dlogits, dbbox):
+        w24, *shared = ctx.saved_tensors
+        apl, rows, grads = ctx.apl, ctx.rows, ctx.grads
+        B = shared[0].shape[0]
+        Cin = shared[0].shape[-1]
+        n_out = 8 * apl
+        npad = -(-n_out // 32) * 32
+        dev = shared[0].device
+        if dlogits is None:
+            dlogits = torch.zeros((B, sum(rows) * apl, 2), device=dev)
+        if dbbox is None:
+            dbbox = torch.zeros((B, sum(rows) * apl, 6), device=dev)
+        w_pad = torch.zeros((Cin, npad), device=dev, dtype=torch.float32)
+        w_pad[:, :n_out] = w24.reshape(Cin, n_out)
+        dshared = [torch.empty_like(s) for s in shared]
+        L = _L()
+        for b in range(B):
+            off = 0
+            for li, (s, r) in enumerate(zip(shared, rows)):
+                xb = s[b:b + 1]
+                _, H, W, D, _ = xb.shape
+                dz = torch.zeros((r, npad), device=dev, dtype=torch.float32)
+                dz[:, :2 * apl] = dlogits[b, off * apl:(off + r) * apl].reshape(r, 2 * apl)
+                dz[:, 2 * apl:n_out] = dbbox[b, off * apl:(off + r) * apl].reshape(r, 6 * apl)
+                if grads.get("bias") is not None:
+                    check(L.m3d_bn_act_bwd(ptr(dz), None, None, r, npad, 0, None, None, None, None,
+                                           None, 0, None, None, ptr(grads["bias"]), stream()),
+                          "rpn_out_bias")
+                if grads.get("kernel") is not None:
+                    check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
+                                                  W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
+                                                  stream()), "rpn_out_wgrad")
+                check(L.m3d_conv3d_bwd_data(ptr(dz), ptr(w_pad), 1, H, W, D, Cin, 1, 1, 1, npad, H,
+                                            W, D, 1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(),
+                                            0, stream()), "rpn_out_dgrad")
+                off += r
+        return (None, None, None, None) + tuple(dshared)

@@ -1,0 +1,251 @@
+"""Benchmark: volumes/sec of the RPN training step (backbone + FPN + RPN head
+fwd/bwd + SGD + ProposalLayer with 3-D NMS) on synthetic 128^3 volumes
+(BASELINE.json configs[1]), one process per GPU (weak scaling, data parallel
+over RCCL), plus the 3-D PyramidROIAlign HBM roofline (configs[2] shapes).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 128]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-mask-r-cnn_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "volumes/sec fwd+bwd @128³ & 256³, 1/2/4/8 MI355X; 3D ROIAlign GB/s vs HBM peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFLOPS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------- dominant kernel
+def time_dominant_conv(model, fmaps, reps=5):
+    """The largest conv of the step: RPN head rpn_conv_shared1 (3x3x3, 256->512) on P2.
+    Timed with HIP events on the stream it is launched on (torch's current stream)."""
+    from m3d import _lib
+    from m3d.nn import conv_geom
+    L = _lib.load()
+    p2 = fmaps[0].detach().contiguous()
+    B, H, W, D, C = p2.shape
+    layer = model.rpn.shared1
+    geo = conv_geom((H, W, D), (3, 3, 3), (1, 1, 1), "same")
+    y = torch.empty((B, H, W, D, 512), device=p2.device)
+
+    def launch():
+        _lib.check(L.m3d_conv3d_fwd(p2.data_ptr(), B, H, W, D, C, layer.kernel.data.data_ptr(), 3, 3, 3,
+                                    512, H, W, D, 1, 1, 1, *geo.pad, layer.bias.data.data_ptr(), None,
+                                    None, None, 0, 1, None, y.data_ptr(), 512, None, 0, 0,
+                                    _lib.stream()), "conv")
+    launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps / 1e3
+    flops = 2.0 * B * H * W * D * 27 * C * 512
+    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "conv_gemm_kernel (fwd, rpn_conv_shared1 3x3x3 256->512 on P2)",
+            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
+
+
+# ---------------------------------------------------------------- ROIAlign roofline
+def roi_boxes(n, S, seed=3):
+    """128 ROIs with log-uniform cube-root pixel volume in [24,128]."""
+    rng = np.random.default_rng(seed)
+    side = np.exp(rng.uniform(np.log(24), np.log(128), n))
+    asp = np.exp(rng.uniform(-0.3, 0.3, (n, 3)))
+    ext = side[:, None] * asp / S
+    ext = np.minimum(ext, 0.95)
+    lo = rng.uniform(0, 1, (n, 3)) * (1 - ext)
+    return np.concatenate([lo, lo + ext], 1).astype(np.float32)[None]
+
+
+def unique_voxels(boxes, fshapes, pool, S):
+    """|U|: distinct input voxels touched by all 8-corner samples (host, exact float32 maths)."""
+    from oracle import ops_ref as R
+    bx, lvl = R.roi_prepare(boxes[0], (S, S, S))
+    total = 0
+    for li in range(4):
+        sel = np.nonzero(lvl == li + 2)[0]
+        if not len(sel):
+            continue
+        H, W, D = fshapes[li]
+        keys = set()
+        for b in bx[sel]:
+            coords = []
+            for ax, (n, Sz) in enumerate(zip(pool, (H, W, D))):
+                b1, b2 = np.float32(b[ax]), np.float32(b[ax + 3])
+                sc = np.float32((b2 - b1) * np.float32(Sz - 1)) / np.float32(n - 1)
+                c = np.float32(b1 * np.float32(Sz - 1)) + np.arange(n, dtype=np.float32) * sc
+                coords.append(np.unique(np.concatenate([np.floor(c), np.ceil(c)]).astype(np.int64)))
+            g = np.stack(np.meshgrid(*coords, indexing="ij"), -1).reshape(-1, 3)
+            keys.update(map(tuple, g))
+        total += len(keys)
+    return total
+
+
+def time_roi_align(fmaps, S, n_rois=128, reps=10):
+    from m3d import layers
+    maps = [f.detach().contiguous() for f in fmaps[:4]]
+    C = maps[0].shape[-1]
+    boxes = torch.from_numpy(roi_boxes(n_rois, S)).to(maps[0].device)
+    meta = torch.zeros((1, 18), device=maps[0].device)
+    meta[0, 5:8] = S
+    res = {}
+    fshapes = [tuple(m.shape[1:4]) for m in maps]
+    for p in (7, 14):
+        layer = layers.PyramidROIAlign((p, p, p))
+        layer([boxes, meta] + maps)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            layer([boxes, meta] + maps)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / reps / 1e3
+        u = unique_voxels(boxes.cpu().numpy(), fshapes, (p, p, p), S)
+        alg = 4.0 * n_rois * p ** 3 * C + 4.0 * C * u
+        res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "algorithmic_bytes": alg,
+                           "gather_bytes": 8 * 4.0 * n_rois * p ** 3 * C,
+                           "GBps": round(alg / t / 1e9, 1), "frac_hbm": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+    return res
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(model, S, depth_slab=8, threads=None):
+    """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
+    fwd+bwd of the same network on a depth slab of the volume (S x S x depth_slab),
+    scaled to whole volumes by the depth ratio (work is linear in depth)."""
+    from oracle import model_ref as MR
+    if threads:
+        torch.set_num_threads(threads)
+    params = model.store.state_dict()
+    ref = MR.RefRPN(params, dtype=torch.float32)
+    for k, v in ref.p.items():
+        if not k.endswith(("moving_mean:0", "moving_variance:0")):
+            v.requires_grad_(True)
+    x = torch.tanh(0.5 * torch.randn((1, S, S, depth_slab, 1), generator=torch.Generator().manual_seed(0)))
+    t0 = time.perf_counter()
+    o = ref.forward(x)
+    loss = o["rpn_class_logits"].square().mean() + o["rpn_bbox"].square().mean()
+    loss.backward()
+    t = time.perf_counter() - t0
+    vol_per_s = (depth_slab / S) / t
+    return {"value": vol_per_s, "unit": "volumes/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/model_ref.py torch-CPU fp32 fwd+bwd on a {S}x{S}x{depth_slab} depth slab "
+                      f"({t:.1f} s), scaled x{S // depth_slab} to one {S}^3 volume"}
+
+
+# ---------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=128)
+    ap.add_argument("--no-proposals", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip roofline / ROIAlign / CPU legs")
+    ap.add_argument("--cpu-slab", type=int, default=8)
+    args = ap.parse_args()
+
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
+    from m3d.parallel import data_parallel_train_step, init_from_env
+
+    rank, world = init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    S = args.size
+    cfg = synthetic_rpn_config(S)
+    model = RPN(cfg, device=dev, seed=1)          # same init on every rank
+    image = synthetic_volume(S, seed=100 + rank).to(dev)
+    match, bbox = synthetic_rpn_targets(model.anchors.shape[1], cfg.RPN_TRAIN_ANCHORS_PER_IMAGE,
+                                        seed=200 + rank)
+    targets = RPNTargets(match, bbox, dev)
+    props = not args.no_proposals
+
+    def step():
+        return data_parallel_train_step(model, image, targets, world, proposals=props)
+
+    log(f"[bench] rank {rank}/{world} size {S}^3, warmup {args.warmup}")
+    for _ in range(args.warmup):
+        r = step()
+    torch.cuda.synchronize()
+    log(f"[bench] warmup done, loss {float(r['loss']):.4f}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / args.steps * 1e3
+    value = world * args.steps / el
+    log(f"[bench] {ms:.1f} ms/step, {value:.3f} volumes/s, loss {float(r['loss']):.4f}")
+
+    out = {"metric": METRIC, "value": round(value, 4), "unit": "volumes/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (tanh(0.5*N(0,1)) volumes, seeded RPN targets; random-init weights)",
+           "config": {"workload": f"configs[1]: RPN training step, ResNet50-3D+FPN+RPN fwd+bwd+SGD"
+                                  f"{' + ProposalLayer(3D NMS 15000->6000)' if props else ''}, "
+                                  f"{S}^3 x1 volume per GPU",
+                      "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
+                      "anchors": int(model.anchors.shape[1])}}
+    if rank == 0 and not args.no_extras:
+        with torch.no_grad():
+            fmaps = model.features(image)
+        try:
+            out["roofline"] = time_dominant_conv(model, fmaps)
+        except Exception as e:  # report, never hide
+            out["roofline"] = {"error": repr(e)}
+        try:
+            out["roi_align"] = time_roi_align(fmaps, S)
+        except Exception as e:
+            out["roi_align"] = {"error": repr(e)}
+        del fmaps
+        torch.cuda.empty_cache()
+        if world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(model, S, args.cpu_slab)
+            except Exception as e:
+                out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

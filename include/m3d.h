@@ -1,0 +1,203 @@
+/*
+ * m3d.h -- C-ABI of libm3d.so, the MI355X-native (gfx950) replacement for the
+ * native hot path of podtyazhki1337/3d-mask-r-cnn.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer owned by the caller; nothing is
+ *     allocated inside an entry point (workspaces are caller-provided);
+ *   - every call is enqueued on the caller's stream `s` and never synchronises,
+ *     so entry points are hipGraph-capturable;
+ *   - tensors are channels-last exactly as the reference: images / feature
+ *     maps [B,H,W,D,C] (depth = 3rd spatial dim, C innermost), boxes
+ *     (y1,x1,z1,y2,x2,z2) normalised to [0,1], conv kernels Keras-ordered
+ *     [kh,kw,kd,Cin,Cout];
+ *   - return 0 (M3D_OK) on success, M3D_EINVAL for an argument the reference
+ *     op would reject (m3d_last_error() then holds the reference's
+ *     InvalidArgument text), M3D_EHIP for a HIP launch error.
+ *   - no global mutable state apart from the thread-local error string.
+ */
+#ifndef M3D_H
+#define M3D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* m3d_stream_t; /* == hipStream_t */
+
+#define M3D_OK 0
+#define M3D_EINVAL (-1)
+#define M3D_EHIP (-2)
+
+const char* m3d_last_error(void);
+int m3d_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * CropAndResize3D family.  Replaces the TF custom ops of the vendored wheel
+ * tensorflow_nms_car_3d==0.1.0 imported at core/custom_op/custom_op.py:22-24:
+ *   crop_and_resize_3d(image, boxes, box_ind, crop_size,
+ *                      method_name='trilinear', extrapolation_value=0)
+ *   crop_and_resize_3d_grad_image(grads, boxes, box_ind, image_size, T, method_name)
+ *   crop_and_resize_3d_grad_boxes(grads, image, boxes, box_ind, method_name)
+ * called from core/models.py:663 (PyramidROIAlign) and :992 (mask targets),
+ * gradient wiring core/custom_op/custom_op.py:28-65.
+ * method: 0 = trilinear, 1 = nearest.
+ * ------------------------------------------------------------------------- */
+int m3d_crop_and_resize3d_fwd(const float* image, int64_t B, int64_t H, int64_t W, int64_t D,
+                              int64_t C, const float* boxes, const int32_t* box_ind, int64_t N,
+                              int32_t ch, int32_t cw, int32_t cd, int32_t method,
+                              float extrapolation, float* crops /*[N,ch,cw,cd,C]*/,
+                              m3d_stream_t s);
+
+/* grad_image is zero-filled by the callee.  deterministic=0: fp32 atomics;
+ * deterministic=1: per-(image,channel) sequential replay in the reference's
+ * box->y->x->z order (bit-exact vs the reference summation order, slow). */
+int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* boxes,
+                                    const int32_t* box_ind, int64_t N, int32_t ch, int32_t cw,
+                                    int32_t cd, int64_t B, int64_t H, int64_t W, int64_t D,
+                                    int64_t C, int32_t method, int32_t deterministic,
+                                    float* grad_image /*[B,H,W,D,C]*/, m3d_stream_t s);
+
+int m3d_crop_and_resize3d_bwd_boxes(const float* grads, const float* image, int64_t B, int64_t H,
+                                    int64_t W, int64_t D, int64_t C, const float* boxes,
+                                    const int32_t* box_ind, int64_t N, int32_t ch, int32_t cw,
+                                    int32_t cd, float* grad_boxes /*[N,6]*/, m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * PyramidROIAlign fused forward/backward (core/models.py:597-687): clip, min
+ * size, level = clamp(4+round_half_even(log2(cbrt(vol)/(224/cbrt(HWD)))),2,5),
+ * trilinear crop from P_level, output written in the original (b,n) order,
+ * non-finite values scrubbed to 0.  fmaps[l] is P(l+2) [B,H_l,W_l,D_l,C];
+ * fshape[l] = {H_l,W_l,D_l}.  image_meta rows of meta_stride floats, image
+ * shape at meta[5:8] (core/models.py:7511-7532).
+ * boxes_adj [B,N,6] and levels [B,N] receive the clipped boxes / levels and
+ * are the inputs of the backward.
+ * ------------------------------------------------------------------------- */
+int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4], const int64_t fshape[4][3],
+                                int64_t C, const float* boxes, const float* image_meta,
+                                int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
+                                int32_t pw, int32_t pd, float* out /*[B,N,ph,pw,pd,C]*/,
+                                float* boxes_adj, int32_t* levels, m3d_stream_t s);
+
+/* gmaps[l] are zero-filled by the callee, then receive the image gradient. */
+int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
+                                const int32_t* levels, int64_t B, int64_t N, int32_t ph,
+                                int32_t pw, int32_t pd, float* const gmaps[4],
+                                const int64_t fshape[4][3], int64_t C, m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * NonMaxSuppression3D (core/custom_op/custom_op.py:25; called at
+ * core/models.py:453): greedy hard NMS, candidates ordered by (score desc,
+ * index asc), score > -FLT_MAX, suppress when IoU > iou_thr.  mode 0: 3-D
+ * boxes [N,6]; mode 1: 2-D boxes [N,4] (y1,x1,y2,x2) (TF 2.2 IOU).
+ * keep receives min(max_out, #kept) original indices in selection order;
+ * *num_keep (device int32) the count.  Bit-exact vs the reference.
+ * ------------------------------------------------------------------------- */
+size_t m3d_nms3d_workspace_bytes(int64_t N);
+int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int32_t max_out, float iou_thr,
+              int32_t mode, int32_t* keep, int32_t* num_keep, void* workspace, size_t ws_bytes,
+              m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * ProposalLayer pieces (core/models.py:369-503).
+ * m3d_score_keys: int64 keys whose descending order is tf.nn.top_k's order
+ *   (score desc, lower index first) for scores = probs[:, :, 1].
+ * m3d_proposal_decode: gather the top-k anchors/deltas, de-normalise by
+ *   rpn_bbox_std_dev, clip +-3, apply_box_deltas_graph, clip to [0,1], enforce
+ *   min sizes.  order[k] are int64 anchor indices.
+ * m3d_proposal_gather: proposals[P,6] = boxes[keep[i]] for i < *num_keep,
+ *   zero rows after (core/models.py:476-485).
+ * ------------------------------------------------------------------------- */
+int m3d_score_keys(const float* probs /*[A,2]*/, int64_t A, int64_t* keys, m3d_stream_t s);
+int m3d_proposal_decode(const float* probs, const float* deltas, const float* anchors,
+                        const int64_t* order, int64_t k, const float std_dev[6],
+                        float image_depth, float* boxes /*[k,6]*/, float* scores /*[k]*/,
+                        m3d_stream_t s);
+int m3d_proposal_gather(const float* boxes, const int32_t* keep, const int32_t* num_keep,
+                        int32_t P, float* proposals, m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * Conv3D (Keras Conv3D, core/models.py:157-273, 512-557, 3190-3214) as
+ * fp32 MFMA implicit GEMMs (v_mfma_f32_32x32x2_f32).
+ *
+ * m3d_conv3d_fwd: y = act(bn(conv(x, w) + bias) + residual)
+ *   x [B,H,W,D,Cin], w [kh,kw,kd,Cin,Cout], output grid [B,OH,OW,OD],
+ *   stride (sy,sx,sz), pad-before (py,px,pz) (zero padding, TF 'same'/'valid').
+ *   bias/bn_scale/bn_shift: [Cout] or NULL.  z_out (optional) receives
+ *   conv+bias before the BN affine.  residual: NULL, or a tensor added before
+ *   the activation; res_mode 1 = same shape as y, 2 = (2,2,1)-nearest
+ *   upsampled source [B,OH/2,OW/2,OD,Cout] (FPN top-down add).  relu 0/1.
+ *   y has row stride ldy >= Cout; if split_n > 0, channels >= split_n go to
+ *   y2 (row stride ldy2) at channel n - split_n (RPN class/bbox heads).
+ * m3d_conv3d_bwd_data: dx (+)= conv_transpose(dz, w), for stride-1 convs of
+ *   any kernel, and 1x1x1 convs of any stride (dx zeroed by the caller for
+ *   strided ones).  accumulate: 0 overwrite, 1 add to dx.
+ * m3d_conv3d_bwd_weight: dw [kh,kw,kd,Cin,Cout] += sum_m im2col(x)^T dz.
+ *   dw must be zeroed by the caller before the first accumulation.
+ * ------------------------------------------------------------------------- */
+int m3d_conv3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                   const float* w, int32_t kh, int32_t kw, int32_t kd, int64_t Cout,
+                   int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
+                   int32_t py, int32_t px, int32_t pz, const float* bias, const float* bn_scale,
+                   const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,
+                   float* z_out, float* y, int64_t ldy, float* y2, int64_t ldy2, int64_t split_n,
+                   m3d_stream_t s);
+int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                        int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd, int64_t Cout,
+                        int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
+                        int32_t py, int32_t px, int32_t pz, float* dx, int32_t accumulate,
+                        m3d_stream_t s);
+int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
+                          int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd,
+                          int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
+                          int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dw,
+                          m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
+ * ------------------------------------------------------------------------- */
+/* KL.MaxPooling3D(k, strides, padding='same'|'valid') (core/models.py:245,3211);
+ * argmax [B,OH,OW,OD,C] uint8 window index for the backward (may be NULL). */
+int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
+                      int32_t kh, int32_t kw, int32_t kd, int32_t sy, int32_t sx, int32_t sz,
+                      int32_t py, int32_t px, int32_t pz, int64_t OH, int64_t OW, int64_t OD,
+                      float* y, uint8_t* argmax, m3d_stream_t s);
+int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t B, int64_t H, int64_t W,
+                      int64_t D, int64_t C, int32_t kh, int32_t kw, int32_t kd, int32_t sy,
+                      int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, int64_t OH,
+                      int64_t OW, int64_t OD, float* dx, m3d_stream_t s);
+/* d_src[b,y,x,z,c] (+)= sum_{i,j in {0,1}} d_up[b,2y+i,2x+j,z,c]  (UpSampling3D((2,2,1)) bwd) */
+int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
+                        float* d_src, int32_t accumulate, m3d_stream_t s);
+/* y = x[:, ::2, ::2, :, :] (P6, core/models.py:3211) and its adjoint (accumulate into dx). */
+int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
+                         float* y, m3d_stream_t s);
+int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
+                         float* dx, m3d_stream_t s);
+/* Backward of y = act(z*scale + shift [+ residual]) for frozen-statistics BN
+ * (TRAIN_BN=False).  dpre = dy * (y > 0 if relu); dz = dpre*scale (or dpre);
+ * dres = dpre (may be NULL; accumulate_res adds into it);
+ * sums (atomically accumulated, caller-zeroed, may be NULL):
+ *   sum_dpre[c] += sum dpre, sum_dpre_xhat[c] += sum dpre*(z-mean)*rstd,
+ *   sum_dz[c] += sum dz. */
+int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, int64_t C,
+                   int32_t relu, const float* scale, const float* mean, const float* rstd,
+                   float* dz, float* dres, int32_t accumulate_res, float* sum_dpre,
+                   float* sum_dpre_xhat, float* sum_dz, m3d_stream_t s);
+/* Keras 2.3.1 SGD (momentum, per-tensor tf.clip_by_norm, decayed lr computed
+ * by the caller) plus the RPN L2 term wd*0.5*||w||^2/size(w) whose gradient
+ * l2_coef[seg]*w is added first (core/models.py:3340-3387).  params / grads /
+ * moments are one flat buffer of n_chunks*1024 floats; every tensor is a
+ * segment padded to whole 1024-float chunks; seg_of_chunk[n_chunks] maps a
+ * chunk to its segment; norms is [n_segments] device scratch. */
+int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
+                  const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
+                  float lr, float momentum, float clipnorm, float* norms, m3d_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* M3D_H */

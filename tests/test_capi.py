@@ -1,0 +1,53 @@
+"""libm3d.so loads on the host and exports every entry point of include/m3d.h
+(no compute calls: there is no GPU in the CPU suite)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "m3d.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(m3d_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import m3d._lib as lib
+    L = lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    # and the Python binding declares a signature for each of them
+    assert sorted(lib.EXPORTED) == syms
+
+
+def test_error_string_and_version():
+    import m3d._lib as lib
+    L = lib.load()
+    assert L.m3d_abi_version() == 1
+    assert isinstance(L.m3d_last_error(), bytes)
+
+
+def test_invalid_arguments_are_rejected_without_touching_the_gpu():
+    import m3d._lib as lib
+    L = lib.load()
+    rc = L.m3d_nms3d(None, None, 10, 5, 1.5, 0, None, None, None, 0, None)
+    assert rc == -1 and b"iou_threshold" in L.m3d_last_error()
+    rc = L.m3d_crop_and_resize3d_fwd(None, 1, 4, 4, 4, 1, None, None, 1, 0, 2, 2, 0, 0.0, None, None)
+    assert rc == -1 and b"crop dimensions must be positive" in L.m3d_last_error()
+    rc = L.m3d_crop_and_resize3d_fwd(None, 1, 4, 4, 4, 1, None, None, 1, 2, 2, 2, 7, 0.0, None, None)
+    assert rc == -1 and b"method" in L.m3d_last_error()
+
+
+def test_ops_refuse_cpu_tensors():
+    import pytest
+    import torch
+    from m3d import ops
+    with pytest.raises(ValueError, match="GPU"):
+        ops.crop_and_resize_3d(torch.zeros(1, 4, 4, 4, 1), torch.zeros(1, 6),
+                               torch.zeros(1, dtype=torch.int32), (2, 2, 2))
+    with pytest.raises(ValueError, match="GPU"):
+        ops.non_max_suppression_3d(torch.zeros(3, 6), torch.zeros(3), 2, 0.5)

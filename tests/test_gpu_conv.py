@@ -1,0 +1,171 @@
+"""GPU parity of the conv / pooling / optimizer kernels against the float64
+PyTorch-CPU restatement of the Keras graph (oracle/model_ref.py).
+Tolerance (north_star): fp32 results within 1e-4 relative to the output scale."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as MR
+
+pytestmark = pytest.mark.gpu
+
+
+def close(got, ref, rtol=1e-4):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    scale = float(ref.abs().max()) + 1e-12
+    err = float((got - ref).abs().max())
+    assert err <= rtol * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+class _Layer:
+    """Minimal stand-in of params.ConvLayer over explicit tensors."""
+
+    class P:
+        def __init__(self, data, grad):
+            self.data, self.grad = data, grad
+
+    def __init__(self, w, b):
+        self.kernel = self.P(w, torch.zeros_like(w))
+        self.bias = self.P(b, torch.zeros_like(b)) if b is not None else None
+        self.k = tuple(w.shape[:3])
+
+    def grad_dict(self, bn=None):
+        g = {"kernel": self.kernel.grad, "bias": self.bias.grad if self.bias else None}
+        if bn is not None:
+            g["gamma"], g["beta"] = bn.gamma.grad, bn.beta.grad
+        return g
+
+
+class _BN:
+    def __init__(self, c, dev, rng):
+        self.gamma = _Layer.P(torch.tensor(rng.uniform(0.5, 1.5, c), dtype=torch.float32, device=dev),
+                              torch.zeros(c, device=dev))
+        self.beta = _Layer.P(torch.tensor(rng.normal(0, 0.1, c), dtype=torch.float32, device=dev),
+                             torch.zeros(c, device=dev))
+        self.moving_mean = torch.tensor(rng.normal(0, 0.2, c), dtype=torch.float32, device=dev)
+        self.moving_variance = torch.tensor(rng.uniform(0.5, 2.0, c), dtype=torch.float32, device=dev)
+        self.eps = 1e-3
+
+
+CASES = [
+    # (in spatial, Cin, Cout, k, stride, padding, bn, relu, residual)
+    ((8, 8, 6), 64, 256, (1, 1, 1), (1, 1, 1), "valid", True, True, False),
+    ((8, 8, 6), 256, 128, (1, 1, 1), (2, 2, 1), "valid", True, True, False),
+    ((6, 6, 5), 64, 64, (3, 3, 3), (1, 1, 1), "same", True, True, False),
+    ((4, 4, 7), 128, 96, (3, 3, 3), (1, 1, 1), "same", False, True, False),
+    ((5, 5, 4), 256, 24, (1, 1, 1), (1, 1, 1), "valid", False, False, False),
+    ((6, 6, 4), 64, 256, (1, 1, 1), (1, 1, 1), "valid", True, True, True),
+    ((16, 16, 6), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),
+    ((3, 5, 9), 32, 160, (3, 3, 3), (1, 1, 1), "same", True, False, True),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_conv_block_fwd_bwd(cuda, case):
+    from m3d.nn import conv_bn_act, conv_geom
+    sp, cin, cout, k, stride, padding, use_bn, relu, use_res = case
+    rng = np.random.default_rng(abs(hash(str(case))) % 2**32)
+    x = torch.tensor(rng.normal(size=(2, *sp, cin)), dtype=torch.float32)
+    w = torch.tensor(rng.normal(0, 1.0 / np.sqrt(np.prod(k) * cin), (*k, cin, cout)), dtype=torch.float32)
+    b = torch.tensor(rng.normal(0, 0.1, cout), dtype=torch.float32)
+    geo = conv_geom(sp, k, stride, padding)
+    res = torch.tensor(rng.normal(size=(2, *geo.out, cout)), dtype=torch.float32) if use_res else None
+    layer = _Layer(w.to(cuda), b.to(cuda))
+    bn = _BN(cout, cuda, rng) if use_bn else None
+    xg = x.to(cuda).requires_grad_(cin != 1)
+    rg = res.to(cuda).requires_grad_(True) if use_res else None
+    # anchor tensor so the stem (input without grad) is still recorded
+    layer.kernel.data.requires_grad_(True)
+    y = conv_bn_act(xg, layer, geo, relu, residual=rg, res_mode=1 if use_res else 0, bn=bn,
+                    need_dx=cin != 1)
+    # float64 reference with autograd
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = MR.conv3d(xr, wr, br, stride, padding)
+    if use_bn:
+        gr = bn.gamma.data.cpu().double().requires_grad_(True)
+        ber = bn.beta.data.cpu().double().requires_grad_(True)
+        yr = MR.batchnorm(yr, gr, ber, bn.moving_mean.cpu().double(), bn.moving_variance.cpu().double())
+    rr = None
+    if use_res:
+        rr = res.double().requires_grad_(True)
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    close(y, yr)
+    g = torch.tensor(rng.normal(size=yr.shape), dtype=torch.float32)
+    y.backward(g.to(cuda))
+    yr.backward(g.double())
+    close(layer.kernel.grad, wr.grad)
+    close(layer.bias.grad, br.grad)
+    if cin != 1:
+        close(xg.grad, xr.grad)
+    if use_bn:
+        close(bn.gamma.grad, gr.grad)
+        close(bn.beta.grad, ber.grad)
+    if use_res:
+        close(rg.grad, rr.grad)
+
+
+def test_fpn_upsample_residual(cuda):
+    from m3d.nn import conv_bn_act, conv_geom
+    rng = np.random.default_rng(11)
+    c4 = torch.tensor(rng.normal(size=(1, 8, 8, 5, 64)), dtype=torch.float32)
+    p5 = torch.tensor(rng.normal(size=(1, 4, 4, 5, 32)), dtype=torch.float32)
+    w = torch.tensor(rng.normal(0, 0.1, (1, 1, 1, 64, 32)), dtype=torch.float32)
+    b = torch.tensor(rng.normal(0, 0.1, 32), dtype=torch.float32)
+    layer = _Layer(w.to(cuda).requires_grad_(True), b.to(cuda))
+    x = c4.to(cuda).requires_grad_(True)
+    r = p5.to(cuda).requires_grad_(True)
+    y = conv_bn_act(x, layer, conv_geom((8, 8, 5), (1, 1, 1), (1, 1, 1), "valid"), False,
+                    residual=r, res_mode=2)
+    xr, rr = c4.double().requires_grad_(True), p5.double().requires_grad_(True)
+    yr = MR.upsample221(rr) + MR.conv3d(xr, w.double(), b.double(), (1, 1, 1), "valid")
+    close(y, yr)
+    g = torch.randn(yr.shape)
+    y.backward(g.to(cuda))
+    yr.backward(g.double())
+    close(r.grad, rr.grad)
+    close(x.grad, xr.grad)
+
+
+def test_maxpool_same_and_subsample(cuda):
+    from m3d.nn import max_pool3d, subsample221
+    rng = np.random.default_rng(12)
+    x = torch.tensor(rng.normal(size=(2, 10, 12, 7, 8)), dtype=torch.float32)
+    xg = x.to(cuda).requires_grad_(True)
+    y = max_pool3d(xg, (3, 3, 3), (2, 2, 1), "same")
+    xr = x.double().requires_grad_(True)
+    yr = MR.maxpool3d_same(xr)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), yr.detach().float().numpy())
+    g = torch.randn(yr.shape)
+    y.backward(g.to(cuda))
+    yr.backward(g.double())
+    close(xg.grad, xr.grad, rtol=1e-6)
+    s = subsample221(xg)
+    np.testing.assert_array_equal(s.detach().cpu().numpy(), x[:, ::2, ::2].numpy())
+
+
+def test_sgd_keras_matches_formula(cuda):
+    from m3d import _lib
+    from m3d.params import ParamStore
+    st = ParamStore()
+    a = st.add("a/kernel:0", (3, 700), "glorot_uniform", True)
+    bb = st.add("b/gamma:0", (5,), "ones", False)
+    st.finalize(cuda, seed=3, weight_decay=0.01)
+    w0 = st.flat.detach().clone()
+    g = torch.randn(st.total, device=cuda) * 3
+    st.grad_flat.copy_(g)
+    lr, mom, clip = 0.1, 0.9, 5.0
+    L = _lib.load()
+    _lib.check(L.m3d_sgd_keras(st.flat.data_ptr(), st.grad_flat.data_ptr(), st.moments.data_ptr(),
+                               st.n_chunks, st.seg_of_chunk.data_ptr(), st.l2_coef.data_ptr(),
+                               len(st.params), lr, mom, clip, st.norms.data_ptr(), _lib.stream()))
+    for p, l2c in ((a, 0.01 / a.numel), (bb, 0.0)):
+        sl = slice(p.offset, p.offset + p.numel)
+        gt = g[sl] + l2c * w0[sl]
+        gt = gt * clip / max(float(gt.norm()), clip)
+        want = w0[sl] - lr * gt
+        close(st.flat.detach()[sl], want, rtol=1e-6)

@@ -1,0 +1,147 @@
+"""GPU parity: CropAndResize3D family, PyramidROIAlign, NMS3D, ProposalLayer
+against the committed golden fixtures and the CPU oracle (tests/golden/)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops_ref as R
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(G, name))
+
+
+def T(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+def test_crop_forward_bit_exact(cuda):
+    from m3d import ops
+    f = load("crop.npz")
+    img, boxes, bi = T(f["image"], cuda), T(f["boxes"], cuda), T(f["box_ind"], cuda)
+    tri = ops.crop_and_resize_3d(img, boxes, bi, (5, 4, 3), "trilinear", -1.5)
+    near = ops.crop_and_resize_3d(img, boxes, bi, (5, 4, 3), "nearest", -1.5)
+    one = ops.crop_and_resize_3d(img, boxes, bi, (1, 3, 1))
+    np.testing.assert_array_equal(tri.cpu().numpy(), f["crops_trilinear"])
+    np.testing.assert_array_equal(near.cpu().numpy(), f["crops_nearest"])
+    np.testing.assert_array_equal(one.cpu().numpy(), f["crops_one"])
+
+
+def test_crop_grad_image(cuda):
+    from m3d import ops
+    f = load("crop.npz")
+    g, boxes, bi = T(f["grads"], cuda), T(f["boxes"], cuda), T(f["box_ind"], cuda)
+    shape = f["image"].shape
+    det = ops.crop_and_resize_3d_grad_image(g, boxes, bi, shape, deterministic=True)
+    np.testing.assert_array_equal(det.cpu().numpy(), f["grad_image_trilinear"])   # same order
+    fast = ops.crop_and_resize_3d_grad_image(g, boxes, bi, shape)
+    np.testing.assert_allclose(fast.cpu().numpy(), f["grad_image_trilinear"], rtol=1e-5, atol=1e-5)
+    near = ops.crop_and_resize_3d_grad_image(g, boxes, bi, shape, method_name="nearest",
+                                             deterministic=True)
+    np.testing.assert_array_equal(near.cpu().numpy(), f["grad_image_nearest"])
+
+
+def test_crop_grad_boxes_and_autograd(cuda):
+    from m3d import ops
+    f = load("crop.npz")
+    img = T(f["image"], cuda).requires_grad_(True)
+    boxes = T(f["boxes"], cuda).requires_grad_(True)
+    out = ops.crop_and_resize_3d(img, boxes, T(f["box_ind"], cuda), (5, 4, 3), "trilinear", -1.5)
+    out.backward(T(f["grads"], cuda))
+    np.testing.assert_allclose(img.grad.cpu().numpy(), f["grad_image_trilinear"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(boxes.grad.cpu().numpy(), f["grad_boxes"], rtol=1e-4, atol=1e-3)
+
+
+def test_crop_validation_messages(cuda):
+    from m3d import ops
+    img = torch.zeros((1, 4, 4, 4, 2), device=cuda)
+    with pytest.raises(ValueError, match="boxes must have 6 columns"):
+        ops.crop_and_resize_3d(img, torch.zeros((2, 4), device=cuda),
+                               torch.zeros(2, dtype=torch.int32, device=cuda), (2, 2, 2))
+    with pytest.raises(ValueError, match="box_index has values outside"):
+        ops.crop_and_resize_3d(img, torch.zeros((1, 6), device=cuda),
+                               torch.ones(1, dtype=torch.int32, device=cuda), (2, 2, 2))
+    with pytest.raises(ValueError, match="crop_size must have three elements"):
+        ops.crop_and_resize_3d(img, torch.zeros((1, 6), device=cuda),
+                               torch.zeros(1, dtype=torch.int32, device=cuda), (2, 2))
+
+
+def test_pyramid_roi_align_bit_exact_and_grad(cuda):
+    from m3d import layers
+    f = load("pyramid.npz")
+    maps = [T(f[k], cuda).requires_grad_(True) for k in ("p2", "p3", "p4", "p5")]
+    boxes, meta = T(f["boxes"], cuda), T(f["meta"], cuda)
+    out7 = layers.PyramidROIAlign((7, 7, 7), name="roi_align_classifier")([boxes, meta] + maps)
+    out3 = layers.PyramidROIAlign((3, 3, 3))([boxes, meta] + maps)
+    np.testing.assert_array_equal(out7.detach().cpu().numpy(), f["out7"])
+    np.testing.assert_array_equal(out3.detach().cpu().numpy(), f["out3"])
+    # gradient = adjoint: <out, g> == sum_l <P_l, dP_l>
+    g = torch.randn_like(out7)
+    out7.backward(g)
+    lhs = float((out7.double() * g.double()).sum())
+    rhs = sum(float((m.double() * m.grad.double()).sum()) for m in maps)
+    assert abs(lhs - rhs) <= 1e-4 * (abs(lhs) + 1)
+
+
+def test_nms_bit_exact(cuda):
+    from m3d import ops
+    f = load("nms.npz")
+    keep = ops.non_max_suppression_3d(T(f["boxes"], cuda), T(f["scores"], cuda), int(f["max_out"]),
+                                      float(f["thr"]))
+    assert keep.dtype == torch.int32
+    np.testing.assert_array_equal(keep.cpu().numpy(), f["keep"])
+    tk = ops.non_max_suppression_3d(T(f["tie_boxes"], cuda), T(f["tie_scores"], cuda), 200, 0.5)
+    np.testing.assert_array_equal(tk.cpu().numpy(), f["tie_keep"])
+    k2, n2 = ops.non_max_suppression_3d_padded(T(f["boxes2d"], cuda), T(f["scores"], cuda), 800, 0.45,
+                                               mode="2d")
+    np.testing.assert_array_equal(k2[: int(n2.item())].cpu().numpy(), f["keep2d"])
+
+
+@pytest.mark.parametrize("n,thr,max_out", [(0, 0.5, 10), (1, 0.5, 10), (64, 0.5, 64), (65, 0.1, 3),
+                                           (15000, 0.7, 6000), (20000, 0.5, 20000)])
+def test_nms_sizes_vs_oracle(cuda, n, thr, max_out):
+    from m3d import ops
+    rng = np.random.default_rng(n)
+    lo = rng.uniform(0, 0.9, (n, 3)).astype(np.float32)
+    sz = rng.uniform(0.005, 0.2, (n, 3)).astype(np.float32)
+    boxes = np.concatenate([lo, lo + sz], 1).astype(np.float32)
+    scores = np.round(rng.uniform(size=n), 3).astype(np.float32)
+    want = R.non_max_suppression_3d(boxes, scores, max_out, thr)
+    got = ops.non_max_suppression_3d(T(boxes, cuda), T(scores, cuda), max_out, thr)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
+def test_nms_repeatable(cuda):
+    from m3d import ops
+    f = load("nms.npz")
+    b, s = T(f["boxes"], cuda), T(f["scores"], cuda)
+    runs = [ops.non_max_suppression_3d(b, s, 1500, 0.3).cpu().numpy() for _ in range(5)]
+    for r in runs[1:]:
+        np.testing.assert_array_equal(r, runs[0])
+
+
+def test_proposal_layer(cuda):
+    from m3d import layers, ops
+    f = load("proposal.npz")
+    probs, deltas, anchors = T(f["probs"], cuda), T(f["deltas"], cuda), T(f["anchors"], cuda)
+    # stage 1: top-k order identical to tf.nn.top_k (ties -> lower index)
+    order = ops.topk_order(probs, 1500)
+    np.testing.assert_array_equal(order.cpu().numpy(), f["order"])
+    # stage 2: decode within fp32 rounding of expf
+    boxes, scores = ops.proposal_decode(probs, deltas, anchors, order, f["std"], 32)
+    np.testing.assert_allclose(boxes.cpu().numpy(), f["boxes"], rtol=0, atol=2e-6)
+    np.testing.assert_array_equal(scores.cpu().numpy(), f["scores"])
+    # stage 3: NMS on the GPU-decoded boxes is bit-exact vs the oracle on the same boxes
+    want = R.non_max_suppression_3d(boxes.cpu().numpy(), scores.cpu().numpy(), 300, 0.7)
+    got = ops.non_max_suppression_3d(boxes, scores, 300, 0.7)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    # whole layer
+    layer = layers.ProposalLayer(300, 0.7, 1500, 1, f["std"], 32, name="ROI")
+    props = layer([probs[None], deltas[None], anchors[None]])
+    np.testing.assert_allclose(props[0].cpu().numpy(), f["proposals"], rtol=0, atol=2e-6)

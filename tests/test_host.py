@@ -1,0 +1,63 @@
+"""Host-side logic: config surface, anchors, TF padding arithmetic."""
+import json
+
+import numpy as np
+import pytest
+
+from m3d import anchors as A
+from m3d import config as C
+from m3d.nn import conv_geom, same_out_pad
+
+RATS_RPN = {  # values of configs/rpn/scp_rpn_rats.json (reference preset)
+    "NUM_CLASSES": 2, "CLASS_NAMES": ["neuron"], "IMAGE_SIZE": 256, "IMAGE_DEPTH": 12,
+    "IMAGE_CHANNEL_COUNT": 1, "MAX_GT_INSTANCES": 6, "USE_MINI_MASK": False,
+    "RPN_ANCHOR_SCALES": [25, 57, 84, 109, 135], "RPN_ANCHOR_RATIOS": [0.05, 0.06, 0.15],
+    "RPN_ANCHOR_STRIDE": 1, "RPN_BBOX_STD_DEV": [0.1, 0.1, 0.1, 0.213, 0.21, 0.15],
+    "RPN_NMS_THRESHOLD": 0.7, "MODE": "training",
+    "BACKBONE_STRIDES": [[4, 4, 1], [8, 8, 1], [16, 16, 1], [32, 32, 1], [64, 64, 1]],
+    "BACKBONE": "resnet50", "TOP_DOWN_PYRAMID_SIZE": 256, "RPN_TRAIN_ANCHORS_PER_IMAGE": 1536,
+    "PRE_NMS_LIMIT": 15000, "POST_NMS_ROIS_TRAINING": 6000, "POST_NMS_ROIS_INFERENCE": 8000,
+    "IMAGES_PER_GPU": 2, "GPU_COUNT": 1, "LOSS_WEIGHTS": {"rpn_class_loss": 3, "rpn_bbox_loss": 2},
+    "OPTIMIZER": {"name": "SGD", "parameters": {"learning_rate": 0.0002, "momentum": 0.9,
+                                                "clipnorm": 5.0, "decay": 1e-4}},
+    "WEIGHT_DECAY": 0.0005, "EPOCHS": 60,
+}
+
+
+def test_config_accepts_reference_keys_and_derives_fields(tmp_path):
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(RATS_RPN))
+    cfg = C.load_config(str(p))
+    assert list(cfg.IMAGE_SHAPE) == [256, 256, 12, 1]
+    assert cfg.BATCH_SIZE == 2 and cfg.IMAGE_META_SIZE == 18
+    assert cfg.ANCHOR_NB == 256 * 256 * 12 // 16 + 256 * 256 * 12 // 64 + 256 * 256 * 12 // 256 + \
+        256 * 256 * 12 // 1024 + 256 * 256 * 12 // 4096
+
+
+def test_config_rejects_unknown_keys():
+    with pytest.raises(TypeError):
+        C.Config(NOT_A_KEY=1)
+
+
+def test_anchor_count_matches_survey():
+    for S, A_expected in ((128, 523776), (256, 4190208)):
+        cfg = C.synthetic_rpn_config(S)
+        a = A.get_anchors(cfg)
+        assert a.shape == (A_expected, 6) and a.dtype == np.float32
+        assert a.min() >= 0 and a.max() <= 1
+
+
+def test_anchor_order_is_y_x_z_anchor():
+    cfg = C.synthetic_rpn_config(128)
+    a = A.get_anchors(cfg)
+    # first level P2 stride 4: anchors of cell (y=0,x=0,z=1) follow the 3 of cell (0,0,0)
+    cz = (a[3:6, 2] + a[3:6, 5]) / 2 * 128
+    assert np.all(cz > (a[0:3, 2] + a[0:3, 5]) / 2 * 128)
+    assert np.allclose(a[0:3, 3] - a[0:3, 0], a[0, 3] - a[0, 0])
+
+
+def test_tf_same_padding_is_asymmetric():
+    assert same_out_pad(64, 3, 2) == (32, 0)      # total pad 1 -> all after
+    assert same_out_pad(128, 3, 1) == (128, 1)
+    g = conv_geom((128, 128, 128), (7, 7, 7), (2, 2, 1), 3)  # ZeroPadding3D(3) + valid
+    assert g.out == (64, 64, 128) and g.pad == (3, 3, 3)
