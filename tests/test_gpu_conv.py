@@ -156,7 +156,9 @@ def test_sgd_keras_matches_formula(cuda):
     bb = st.add("b/gamma:0", (5,), "ones", False)
     st.finalize(cuda, seed=3, weight_decay=0.01)
     w0 = st.flat.detach().clone()
-    g = torch.randn(st.total, device=cuda) * 3
+    g = torch.zeros(st.total, device=cuda)      # padding of each segment stays zero
+    for p in (a, bb):
+        g[p.offset:p.offset + p.numel] = torch.randn(p.numel, device=cuda) * 3
     st.grad_flat.copy_(g)
     lr, mom, clip = 0.1, 0.9, 5.0
     L = _lib.load()

