@@ -63,6 +63,10 @@ struct Epi {
     int simple;       // y row == m (same grid, unit store stride)
 };
 
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
 // m < 2^31 is guaranteed by the host checks: 32-bit unsigned division only.
 __device__ __forceinline__ void decompose(int64_t m64, int OH, int OW, int OD, int& b, int& oy,
                                           int& ox, int& oz) {
@@ -110,8 +114,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     static_assert(WM * WN == 4, "4 waves");
     static_assert(TM >= 1 && TN >= 1, "tile");
-    constexpr int LDA = BK + 1;
-    constexpr int LDB = BT ? (BK + 1) : BN;
+    // [rows][k] tiles: row stride 36 floats keeps float4 alignment and makes the
+    // per-lane 16-float fragment reads (4 x ds_read_b128, rows = lanes) bank-
+    // conflict-free (36*i mod 64 dwords spreads 16 rows over all 64 banks).
+    constexpr int LDA = BK + 4;
+    constexpr int LDB = BT ? (BK + 4) : BN;
     constexpr int A_SZ = BM * LDA;
     constexpr int B_SZ = BT ? BN * LDB : BK * LDB;
     constexpr int AQ = AVEC ? BM / 32 : BM / 8;      // A elements (float4 or float) per thread
@@ -221,10 +228,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         float* Bs = As + A_SZ;
         if (AVEC) {
 #pragma unroll
-            for (int q = 0; q < AQ; ++q) {
-                float* d = As + ((tid >> 3) + 32 * q) * LDA + a_col4 * 4;
-                d[0] = ra[q].x; d[1] = ra[q].y; d[2] = ra[q].z; d[3] = ra[q].w;
-            }
+            for (int q = 0; q < AQ; ++q)
+                *reinterpret_cast<float4*>(As + ((tid >> 3) + 32 * q) * LDA + a_col4 * 4) = ra[q];
         } else {
 #pragma unroll
             for (int q = 0; q < AQ; ++q) As[((tid >> 5) + 8 * q) * LDA + (tid & 31)] = rs[q];
@@ -238,10 +243,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < BQ; ++q) {
-                float* d = Bs + ((tid >> 3) + 32 * q) * LDB + a_col4 * 4;
-                d[0] = rb[q].x; d[1] = rb[q].y; d[2] = rb[q].z; d[3] = rb[q].w;
-            }
+            for (int q = 0; q < BQ; ++q)
+                *reinterpret_cast<float4*>(Bs + ((tid >> 3) + 32 * q) * LDB + a_col4 * 4) = rb[q];
         }
     };
 
@@ -263,21 +266,38 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         if (kt + 1 < nk) load_tile(kt + 1);
         const float* As = smem + buf * (A_SZ + B_SZ);
         const float* Bs = As + A_SZ;
+        // fragments: lane (l32, h) owns row l32 of each 32-row tile and the 16
+        // k values 16h..16h+15 of this k-tile (MFMA step s consumes k = 16h+s)
+        float4 af[TM][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                af[i][q] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + i * 32 + l32) * LDA +
+                                                            h * 16 + 4 * q);
+        float4 bf[BT ? TN : 1][4];
+        if (BT) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    bf[j][q] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + j * 32 + l32) * LDB +
+                                                                h * 16 + 4 * q);
+        }
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int kk = h * 16 + s;
-            float a[TM], b[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = As[(wm * TM * 32 + i * 32 + l32) * LDA + kk];
+            float b[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                b[j] = BT ? Bs[(wn * TN * 32 + j * 32 + l32) * LDB + kk]
+                b[j] = BT ? f4get(bf[BT ? j : 0][s >> 2], s & 3)
                           : Bs[kk * LDB + wn * TN * 32 + j * 32 + l32];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i][s >> 2], s & 3), b[j],
+                                                                      acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) store_tile(buf ^ 1);
         __syncthreads();
@@ -345,15 +365,30 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
     float rx1[AVEC ? 1 : XQ];
     float4 rg[GQ];
 
+    // output coordinates of row (mb + xrow0), advanced incrementally (no
+    // per-row integer division in the m loop)
+    int cb_ = 0, cy_ = 0, cx_ = 0, cz_ = 0;
+    decompose(ms + xrow0 < me ? ms + xrow0 : ms, p.OH, p.OW, p.OD, cb_, cy_, cx_, cz_);
+    auto advance = [&](int& b, int& y, int& x, int& z, int delta) {
+        z += delta;
+        while (z >= p.OD) {
+            z -= p.OD;
+            if (++x == p.OW) {
+                x = 0;
+                if (++y == p.OH) { y = 0; ++b; }
+            }
+        }
+    };
     auto load_tile = [&](int64_t mb) {
+        int rb = cb_, ry = cy_, rx = cx_, rz = cz_;
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
             const int64_t m = mb + xrow0 + XRSTEP * q;
+            if (q > 0) advance(rb, ry, rx, rz, XRSTEP);
             bool ok = kok && m < me;
             int64_t off = 0;
             if (ok) {
-                int b, oy, ox, oz;
-                decompose(m, p.OH, p.OW, p.OD, b, oy, ox, oz);
+                const int b = rb, oy = ry, ox = rx, oz = rz;
                 const int iy = oy * p.sy - p.py + ky, ix = ox * p.sx - p.px + kx,
                           iz = oz * p.sz - p.pz + kz;
                 ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && iz >= 0 && iz < p.D;
@@ -362,6 +397,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
             if (AVEC) rx4[q] = ok ? *reinterpret_cast<const float4*>(p.a + off) : make_float4(0.f, 0.f, 0.f, 0.f);
             else rx1[q] = ok ? p.a[off] : 0.0f;
         }
+        advance(cb_, cy_, cx_, cz_, BKM);
 #pragma unroll
         for (int q = 0; q < GQ; ++q) {
             const int64_t m = mb + grow0 + GRSTEP * q;

@@ -129,13 +129,14 @@ __global__ void subsample221_kernel(const float4* __restrict__ src, int B, int H
 }
 
 // Thread layout: T threads per row cover T channel quads; R = 256/T rows per
-// block pass; gridDim.y channel groups of 4*T channels.
+// block pass; gridDim.y channel groups of 4*T channels.  Each block writes its
+// per-channel partial sums to part[3][gridDim.x][C] (no contended atomics);
+// bn_sums_reduce_kernel then folds them in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ z,
     int64_t M, int C, int T, int relu, const float* __restrict__ scale,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dz,
-    float* __restrict__ dres, int accumulate_res, float* __restrict__ sum_dpre,
-    float* __restrict__ sum_xhat, float* __restrict__ sum_dz) {
+    float* __restrict__ dres, int accumulate_res, int want_xhat, float* __restrict__ part) {
     const int R = 256 / T;
     const int tx = threadIdx.x % T, ty = threadIdx.x / T;
     const int c = (blockIdx.y * T + tx) * 4;
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
                 if (!(y4.w > 0.f)) g[3] = 0.f;
             }
             float zz[4] = {0, 0, 0, 0};
-            if (z && sum_xhat) { const float4 v = *(const float4*)(z + off); zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w; }
+            if (want_xhat) { const float4 v = *(const float4*)(z + off); zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w; }
             float d[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -177,7 +178,6 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
             }
         }
     }
-    // block reduction over the R rows sharing a channel quad
     __shared__ float red[3][256][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -199,13 +199,40 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
         __syncthreads();
     }
     if (ty == 0 && c < C) {
+        const int64_t gx = gridDim.x;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (sum_dpre) unsafeAtomicAdd(sum_dpre + c + q, red[0][tx][q]);
-            if (sum_xhat) unsafeAtomicAdd(sum_xhat + c + q, red[1][tx][q]);
-            if (sum_dz) unsafeAtomicAdd(sum_dz + c + q, red[2][tx][q]);
-        }
+        for (int a = 0; a < 3; ++a)
+            *(float4*)(part + ((int64_t)a * gx + blockIdx.x) * C + c) =
+                make_float4(red[a][tx][0], red[a][tx][1], red[a][tx][2], red[a][tx][3]);
     }
+}
+
+// out_a[c] += sum_b part[a][b][c].  grid (ceil(C/64), 3); 256 threads =
+// 64 channels x 4 row groups, each with 4 independent accumulators; the
+// partials are folded in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __restrict__ part, int gx,
+                                                             int C, float* __restrict__ s0,
+                                                             float* __restrict__ s1,
+                                                             float* __restrict__ s2) {
+    const int a = blockIdx.y;
+    float* dst = a == 0 ? s0 : (a == 1 ? s1 : s2);
+    if (!dst) return;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + tx;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
+        const float* p = part + (int64_t)a * gx * C + c;
+        int b = ty;
+        for (; b + 12 < gx; b += 16) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += p[(int64_t)(b + 4 * u) * C];
+        }
+        for (; b < gx; b += 4) acc[0] += p[(int64_t)b * C];
+    }
+    __shared__ float red[4][64];
+    red[ty][tx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (ty == 0 && c < C) dst[c] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
 // ---- Keras SGD over a flat parameter buffer split into segments padded to
@@ -322,27 +349,48 @@ extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64
     return check_launch("subsample221_kernel(bwd)");
 }
 
+static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {
+    const int quads = (int)(C / 4);
+    T = 1;
+    while (T < quads && T < 256) T <<= 1;
+    groups = (quads + T - 1) / T;
+    const int R = 256 / T;
+    gx = (M + R - 1) / R;
+    const int64_t cap = 512 / groups > 0 ? 512 / groups : 1;
+    if (gx > cap) gx = cap;
+    if (gx < 1) gx = 1;
+}
+
+extern "C" size_t m3d_bn_act_bwd_workspace_bytes(int64_t M, int64_t C) {
+    int T, groups;
+    int64_t gx;
+    bn_grid(M, C, T, groups, gx);
+    return sizeof(float) * 3 * (size_t)gx * (size_t)C;
+}
+
 extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M,
                               int64_t C, int32_t relu, const float* scale, const float* mean,
                               const float* rstd, float* dz, float* dres, int32_t accumulate_res,
                               float* sum_dpre, float* sum_dpre_xhat, float* sum_dz,
-                              m3d_stream_t s) {
+                              void* workspace, size_t ws_bytes, m3d_stream_t s) {
     if (C % 4) return einval("bn_act_bwd: C must be a multiple of 4");
     if (relu && !y) return einval("bn_act_bwd: relu needs y");
     if (sum_dpre_xhat && !z) return einval("bn_act_bwd: xhat sums need z");
     if (M == 0) return M3D_OK;
-    const int quads = (int)(C / 4);
-    int T = 1;
-    while (T < quads && T < 256) T <<= 1;
-    const int groups = (quads + T - 1) / T;
-    const int R = 256 / T;
-    int64_t gx = (M + R - 1) / R;
-    const int64_t cap = 2048 / groups + 1;
-    if (gx > cap) gx = cap;
+    int T, groups;
+    int64_t gx;
+    bn_grid(M, C, T, groups, gx);
+    const bool sums = sum_dpre || sum_dpre_xhat || sum_dz;
+    if (sums && ws_bytes < sizeof(float) * 3 * (size_t)gx * (size_t)C)
+        return einval("bn_act_bwd: workspace too small");
     hipLaunchKernelGGL(bn_act_bwd_kernel, dim3((unsigned)gx, (unsigned)groups), dim3(256), 0, st(s),
                        dy, y, z, M, (int)C, T, relu, scale, mean, rstd, dz, dres, accumulate_res,
-                       sum_dpre, sum_dpre_xhat, sum_dz);
-    return check_launch("bn_act_bwd_kernel");
+                       sum_dpre_xhat ? 1 : 0, (float*)workspace);
+    int rc = check_launch("bn_act_bwd_kernel");
+    if (rc || !sums) return rc;
+    hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 63) / 64), 3), dim3(256), 0, st(s),
+                       (const float*)workspace, (int)gx, (int)C, sum_dpre, sum_dpre_xhat, sum_dz);
+    return check_launch("bn_sums_reduce_kernel");
 }
 
 extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,

@@ -153,28 +153,46 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ 
 }
 
 // Greedy reduction.  removed[] lives in LDS (cb words, cb <= 16384).
+// Per 64-row block: wave 0 resolves the block serially in registers
+// (readlane over the diagonal mask words), then ALL threads OR the kept rows'
+// mask words into removed[] -- one independent global load per (kept row,
+// word) pair, folded with LDS 64-bit atomic ORs, so the global latency is paid
+// once per block instead of once per kept row.
 __global__ __launch_bounds__(1024) void nms_reduce_kernel(const uint64_t* __restrict__ mask,
                                                           const uint64_t* __restrict__ keys,
                                                           int64_t N, int64_t cb, int max_out,
                                                           int32_t* __restrict__ keep,
                                                           int32_t* __restrict__ num_keep) {
     extern __shared__ __attribute__((aligned(16))) uint64_t removed[];
-    __shared__ uint64_t kept_sh;
-    __shared__ int nkeep_sh, stop_sh;
+    __shared__ int kept_rows[64];
+    __shared__ int nkept_sh, nkeep_sh, stop_sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t w = tid; w < cb; w += blockDim.x) removed[w] = 0;
-    if (tid == 0) { nkeep_sh = 0; stop_sh = 0; }
+    if (tid == 0) { nkeep_sh = 0; stop_sh = 0; nkept_sh = 0; }
     __syncthreads();
+    // wave 0 keeps the next block's keys / diagonal words in flight across the
+    // OR phase (the mask is read-only), hiding one global round trip per block
+    uint64_t key_n = 0, diag_n = 0;
+    if (wave == 0) {
+        key_n = lane < N ? keys[lane] : ~0ull;
+        diag_n = lane < N ? mask[(int64_t)lane * cb] : 0ull;
+    }
     for (int64_t blk = 0; blk < cb; ++blk) {
         if (wave == 0) {
             const int64_t row = blk * 64 + lane;
-            uint64_t key = row < N ? keys[row] : ~0ull;
+            const uint64_t key = key_n;
             const bool valid = row < N && (key >> 32) != 0xFFFFFFFFull;
-            const uint64_t diag = valid ? mask[row * cb + blk] : 0ull;
+            const uint64_t diag = valid ? diag_n : 0ull;
+            if (blk + 1 < cb) {
+                const int64_t rn = row + 64;
+                key_n = rn < N ? keys[rn] : ~0ull;
+                diag_n = rn < N ? mask[rn * cb + blk + 1] : 0ull;
+            }
             const uint64_t vmask = __ballot(valid);
             uint64_t rem = removed[blk];
             uint64_t kept = 0;
-            int nk = nkeep_sh;
+            const int nk0 = nkeep_sh;
+            int nk = nk0;
             const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
             for (int r = 0; r < 64; ++r) {
                 if (!((vmask >> r) & 1ull)) break;            // sorted: rest invalid
@@ -188,29 +206,39 @@ __global__ __launch_bounds__(1024) void nms_reduce_kernel(const uint64_t* __rest
                 }
             }
             if ((kept >> lane) & 1ull) {
-                const int pos = nkeep_sh + __popcll(kept & ((1ull << lane) - 1ull));
-                keep[pos] = (int32_t)(uint32_t)key;
+                const int j = __popcll(kept & ((1ull << lane) - 1ull));
+                keep[nk0 + j] = (int32_t)(uint32_t)key;
+                kept_rows[j] = lane;
             }
             if (lane == 0) {
-                kept_sh = kept;
+                nkept_sh = nk - nk0;
                 nkeep_sh = nk;
                 if (nk >= max_out || vmask != ~0ull) stop_sh = 1;
             }
         }
         __syncthreads();
         if (stop_sh) break;
-        const uint64_t kept = kept_sh;
-        if (kept) {
-            for (int64_t w = blk + 1 + tid; w < cb; w += blockDim.x) {
-                uint64_t acc = removed[w];
-                uint64_t kk = kept;
-                while (kk) {
-                    const int r = __ffsll((long long)kk) - 1;
-                    kk &= kk - 1;
-                    acc |= mask[(blk * 64 + r) * cb + w];
+        const int nkb = nkept_sh;
+        const int64_t w0 = blk + 1, nw = cb - w0;
+        const int64_t total = (int64_t)nkb * nw;
+        const uint64_t* mrow = mask + (blk * 64) * cb;
+        for (int64_t p0 = tid; p0 < total; p0 += 4 * (int64_t)blockDim.x) {
+            uint64_t v[4];
+            int64_t wi[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t p = p0 + (int64_t)u * blockDim.x;
+                v[u] = 0;
+                wi[u] = -1;
+                if (p < total) {
+                    const int i = (int)(p / nw);
+                    wi[u] = w0 + p % nw;
+                    v[u] = mrow[(int64_t)kept_rows[i] * cb + wi[u]];
                 }
-                removed[w] = acc;
             }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (v[u]) atomicOr((unsigned long long*)&removed[wi[u]], (unsigned long long)v[u]);
         }
         __syncthreads();
     }

@@ -31,6 +31,17 @@ def valid_out(n, k, s):
     return (n - k) // s + 1
 
 
+def bn_act_bwd(dy, y, z, M, C, relu, scale, mean, rstd, dz, dres, sum_dpre, sum_xhat, sum_dz):
+    """m3d_bn_act_bwd with its deterministic-reduction workspace."""
+    L = _L()
+    need = sum_dpre is not None or sum_xhat is not None or sum_dz is not None
+    wsb = int(L.m3d_bn_act_bwd_workspace_bytes(M, C)) if need else 0
+    ws = torch.empty(max(wsb // 4, 1), device=dy.device, dtype=torch.float32) if need else None
+    check(L.m3d_bn_act_bwd(ptr(dy), ptr(y), ptr(z), M, C, 1 if relu else 0, ptr(scale), ptr(mean),
+                           ptr(rstd), ptr(dz), ptr(dres), 0, ptr(sum_dpre), ptr(sum_xhat),
+                           ptr(sum_dz), ptr(ws), wsb, stream()), "bn_act_bwd")
+
+
 @dataclass
 class ConvGeom:
     k: tuple
@@ -104,18 +115,16 @@ class _ConvBNAct(torch.autograd.Function):
             dz = dy
             dres = dy if need_res else None
             if grads.get("bias") is not None:
-                check(L.m3d_bn_act_bwd(ptr(dy), None, None, M, Cout, 0, None, None, None, None,
-                                       None, 0, None, None, ptr(grads["bias"]), stream()), "bn_act_bwd")
+                bn_act_bwd(dy, None, None, M, Cout, False, None, None, None, None, None, None, None,
+                           grads["bias"])
         else:
             dz = torch.empty_like(dy)
             dres = torch.empty_like(dy) if need_res else None
             mean = rstd = scale = None
             if ctx.bn is not None:
                 mean, rstd, scale = ctx.bn
-            check(L.m3d_bn_act_bwd(ptr(dy), ptr(y), ptr(z), M, Cout, 1 if ctx.relu else 0,
-                                   ptr(scale), ptr(mean), ptr(rstd), ptr(dz), ptr(dres), 0,
-                                   ptr(grads.get("beta")), ptr(grads.get("gamma")) if z is not None else None,
-                                   ptr(grads.get("bias")), stream()), "bn_act_bwd")
+            bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
+                       grads.get("gamma") if z is not None else None, grads.get("bias"))
         if grads.get("kernel") is not None:
             check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                           OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
@@ -274,9 +283,8 @@ class _RPNOut(torch.autograd.Function):
                 dz[:, :2 * apl] = dlogits[b, off * apl:(off + r) * apl].reshape(r, 2 * apl)
                 dz[:, 2 * apl:n_out] = dbbox[b, off * apl:(off + r) * apl].reshape(r, 6 * apl)
                 if grads.get("bias") is not None:
-                    check(L.m3d_bn_act_bwd(ptr(dz), None, None, r, npad, 0, None, None, None, None,
-                                           None, 0, None, None, ptr(grads["bias"]), stream()),
-                          "rpn_out_bias")
+                    bn_act_bwd(dz, None, None, r, npad, False, None, None, None, None, None, None,
+                               None, grads["bias"])
                 if grads.get("kernel") is not None:
                     check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
                                                   W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),

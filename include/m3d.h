@@ -178,15 +178,19 @@ int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_
 int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
                          float* dx, m3d_stream_t s);
 /* Backward of y = act(z*scale + shift [+ residual]) for frozen-statistics BN
- * (TRAIN_BN=False).  dpre = dy * (y > 0 if relu); dz = dpre*scale (or dpre);
- * dres = dpre (may be NULL; accumulate_res adds into it);
- * sums (atomically accumulated, caller-zeroed, may be NULL):
+ * (TRAIN_BN=False).  dpre = dy * (y > 0 if relu); dz = dpre*scale (or dpre;
+ * dz may be NULL when not needed); dres = dpre (may be NULL; accumulate_res
+ * adds into it).  Per-channel sums, each added (+=) into its destination when
+ * non-NULL, in a fixed order (deterministic, no float atomics):
  *   sum_dpre[c] += sum dpre, sum_dpre_xhat[c] += sum dpre*(z-mean)*rstd,
- *   sum_dz[c] += sum dz. */
+ *   sum_dz[c] += sum dz.
+ * workspace: m3d_bn_act_bwd_workspace_bytes(M, C) bytes of device scratch. */
+size_t m3d_bn_act_bwd_workspace_bytes(int64_t M, int64_t C);
 int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, int64_t C,
                    int32_t relu, const float* scale, const float* mean, const float* rstd,
                    float* dz, float* dres, int32_t accumulate_res, float* sum_dpre,
-                   float* sum_dpre_xhat, float* sum_dz, m3d_stream_t s);
+                   float* sum_dpre_xhat, float* sum_dz, void* workspace, size_t ws_bytes,
+                   m3d_stream_t s);
 /* Keras 2.3.1 SGD (momentum, per-tensor tf.clip_by_norm, decayed lr computed
  * by the caller) plus the RPN L2 term wd*0.5*||w||^2/size(w) whose gradient
  * l2_coef[seg]*w is added first (core/models.py:3340-3387).  params / grads /
