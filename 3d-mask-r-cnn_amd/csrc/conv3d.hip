@@ -127,8 +127,20 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-    const int64_t m0 = (int64_t)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order (speed only): the dispatcher deals consecutive
+    // workgroups round-robin to the 8 XCDs; remap so each XCD owns a contiguous
+    // run of tiles, N-tiles of one M-tile adjacent, so the im2col rows (and
+    // their 3x3x3 halo) are re-read from that XCD's L2, not from HBM.
+    int64_t m0;
+    int n0;
+    {
+        const int64_t nbx = gridDim.x, nby = gridDim.y, total = nbx * nby;
+        const int64_t L = (int64_t)blockIdx.x + nbx * blockIdx.y;
+        const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
+        const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+        m0 = (T / nby) * BM;
+        n0 = (int)(T % nby) * BN;
+    }
     const int taps_kd = p.kd, taps_kwkd = p.kw * p.kd;
     const int ntaps = p.kh * taps_kwkd;
 

@@ -383,6 +383,37 @@ __global__ __launch_bounds__(256) void pyramid_bwd_kernel(Pyr P, int C,
     scatter_sample(img, W, D, C, s, 0, gout + sidx * C, lane);
 }
 
+
+// DetectionTargetLayer GT-mask targets (core/models.py:972-996): for each
+// positive ROI p, crop channel assign[p] of the boolean instance masks
+// [H,W,D,G] (read in place -- the reference materialises a [P,H,W,D,1]
+// gather first) to (mh,mw,md) with trilinear CropAndResize3D semantics
+// (A.1), then tf.round (half to even).  One thread per output voxel.
+__global__ void mask_targets_kernel(const uint8_t* __restrict__ masks, int H, int W, int D, int G,
+                                    const float* __restrict__ boxes,
+                                    const int32_t* __restrict__ assign, int64_t total, int mh,
+                                    int mw, int md, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int64_t t = i;
+    const int z = (int)(t % md); t /= md;
+    const int x = (int)(t % mw); t /= mw;
+    const int y = (int)(t % mh);
+    const int64_t p = t / mh;
+    const Sample s = make_sample(boxes + p * 6, H, W, D, mh, mw, md, y, x, z);
+    float v = 0.0f;   // extrapolation_value 0
+    if (!s.oob) {
+        const int g = assign[p];
+        auto M = [&](int yy, int xx, int zz) {
+            return (float)masks[(((int64_t)yy * W + xx) * D + zz) * G + g];
+        };
+        v = tri(M(s.ty, s.lx, s.fz), M(s.ty, s.lx, s.kz), M(s.ty, s.rx, s.fz), M(s.ty, s.rx, s.kz),
+                M(s.by, s.lx, s.fz), M(s.by, s.lx, s.kz), M(s.by, s.rx, s.fz), M(s.by, s.rx, s.kz),
+                s.yl, s.xl, s.zl);
+    }
+    out[i] = rintf(v);
+}
+
 }  // namespace m3d
 
 using namespace m3d;
@@ -504,4 +535,17 @@ extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* b
     hipLaunchKernelGGL(pyramid_bwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
                        (int)C, boxes_adj, levels, N, total, ph, pw, pd, grad_out);
     return check_launch("pyramid_bwd_kernel");
+}
+
+extern "C" int m3d_mask_targets3d(const uint8_t* gt_masks, int64_t H, int64_t W, int64_t D,
+                                  int64_t G, const float* rois, const int32_t* assign, int64_t P,
+                                  int32_t mh, int32_t mw, int32_t md, float* out, m3d_stream_t s) {
+    if (H <= 0 || W <= 0 || D <= 0 || G < 0) return einval("gt_masks must be [H,W,D,G]");
+    if (mh <= 0 || mw <= 0 || md <= 0) return einval("crop dimensions must be positive");
+    const int64_t total = P * mh * mw * md;
+    if (total == 0) return M3D_OK;
+    if (G == 0) return einval("no GT masks to crop");
+    hipLaunchKernelGGL(mask_targets_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st(s), gt_masks,
+                       (int)H, (int)W, (int)D, (int)G, rois, assign, total, mh, mw, md, out);
+    return check_launch("mask_targets_kernel");
 }

@@ -37,6 +37,8 @@ _SIGS = {
                                     c_i32, c_p, c_p, c_p, c_p],
     "m3d_pyramid_roi_align3d_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p,
                                     c_i64, c_p],
+    "m3d_mask_targets3d": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_i32,
+                           c_p, c_p],
     "m3d_nms3d_workspace_bytes": [c_i64],
     "m3d_nms3d": [c_p, c_p, c_i64, c_i32, c_f, c_i32, c_p, c_p, c_p, c_sz, c_p],
     "m3d_score_keys": [c_p, c_i64, c_p, c_p],

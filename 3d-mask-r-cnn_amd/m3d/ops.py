@@ -133,6 +133,31 @@ def crop_and_resize_3d(image, boxes, box_ind, crop_size, method_name="trilinear"
                                   float(extrapolation_value))
 
 
+def detection_mask_targets(gt_masks, positive_rois, roi_gt_box_assignment, mask_shape,
+                           use_mini_mask=False, roi_gt_boxes=None):
+    """Mask targets of detection_targets_graph (core/models.py:972-996).
+
+    gt_masks [H,W,D,G] bool/uint8, positive_rois [P,6], roi_gt_box_assignment [P]
+    -> [P, mh, mw, md] float32 in {0,1} (tf.round of the trilinear crop)."""
+    _dev(gt_masks, positive_rois, roi_gt_box_assignment)
+    H, W, D, G = gt_masks.shape
+    boxes = _c(positive_rois.detach())
+    if use_mini_mask:
+        gb = roi_gt_boxes.detach().float()
+        gh, gw, gd = gb[:, 3] - gb[:, 0], gb[:, 4] - gb[:, 1], gb[:, 5] - gb[:, 2]
+        den = torch.stack([gh, gw, gd, gh, gw, gd], 1)
+        off = torch.cat([gb[:, :3], gb[:, :3]], 1)
+        boxes = ((boxes - off) / den).contiguous()
+    m = gt_masks.to(torch.uint8).contiguous()
+    assign = _c(roi_gt_box_assignment, torch.int32)
+    P = boxes.shape[0]
+    mh, mw, md = (int(v) for v in mask_shape)
+    out = torch.empty((P, mh, mw, md), device=boxes.device, dtype=torch.float32)
+    check(_L().m3d_mask_targets3d(ptr(m), H, W, D, G, ptr(boxes), ptr(assign), P, mh, mw, md,
+                                  ptr(out), stream()), "mask_targets3d")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # NonMaxSuppression3D (core/custom_op/custom_op.py:25)
 # ---------------------------------------------------------------------------

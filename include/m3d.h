@@ -88,6 +88,15 @@ int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
                                 int32_t pw, int32_t pd, float* const gmaps[4],
                                 const int64_t fshape[4][3], int64_t C, m3d_stream_t s);
 
+/* DetectionTargetLayer mask targets (core/models.py:972-996): out[p] =
+ * round_half_even(CropAndResize3D(float(gt_masks[..., assign[p]]), rois[p],
+ * (mh,mw,md), trilinear, extrapolation 0)), reading the boolean masks
+ * [H,W,D,G] (uint8) in place instead of materialising the [P,H,W,D,1] gather.
+ * rois are the (mini-mask-normalised when USE_MINI_MASK) positive boxes. */
+int m3d_mask_targets3d(const uint8_t* gt_masks, int64_t H, int64_t W, int64_t D, int64_t G,
+                       const float* rois, const int32_t* assign, int64_t P, int32_t mh,
+                       int32_t mw, int32_t md, float* out /*[P,mh,mw,md]*/, m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * NonMaxSuppression3D (core/custom_op/custom_op.py:25; called at
  * core/models.py:453): greedy hard NMS, candidates ordered by (score desc,

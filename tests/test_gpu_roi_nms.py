@@ -145,3 +145,24 @@ def test_proposal_layer(cuda):
     layer = layers.ProposalLayer(300, 0.7, 1500, 1, f["std"], 32, name="ROI")
     props = layer([probs[None], deltas[None], anchors[None]])
     np.testing.assert_allclose(props[0].cpu().numpy(), f["proposals"], rtol=0, atol=2e-6)
+
+
+def test_detection_mask_targets_bit_exact(cuda):
+    """a12: GT-mask crop of DetectionTargetLayer, read in place + tf.round."""
+    from m3d import ops
+    rng = np.random.default_rng(21)
+    H, W, D, G = 24, 20, 12, 5
+    masks = np.zeros((H, W, D, G), bool)
+    for g in range(G):
+        c = rng.uniform(4, [H - 4, W - 4, D - 4])
+        r = rng.uniform(2, 5, 3)
+        yy, xx, zz = np.meshgrid(np.arange(H), np.arange(W), np.arange(D), indexing="ij")
+        masks[..., g] = ((yy - c[0]) / r[0]) ** 2 + ((xx - c[1]) / r[1]) ** 2 + ((zz - c[2]) / r[2]) ** 2 < 1
+    P = 9
+    lo = rng.uniform(0, 0.6, (P, 3))
+    rois = np.concatenate([lo, lo + rng.uniform(0.1, 0.4, (P, 3))], 1).astype(np.float32)
+    assign = rng.integers(0, G, P).astype(np.int32)
+    got = ops.detection_mask_targets(T(masks, cuda), T(rois, cuda), T(assign, cuda), (28, 28, 28))
+    roi_masks = np.transpose(masks, (3, 0, 1, 2))[..., None][assign].astype(np.float32)
+    want = np.rint(R.crop_and_resize_3d(roi_masks, rois, np.arange(P), (28, 28, 28))[..., 0])
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
