@@ -42,6 +42,9 @@ struct ConvP {
     const float* w;
     int N;
     int flip;         // bwd-data: use tap (taps-1-t)
+    // batched GEMMs (Winograd points): blockIdx.z selects the batch; A, W and Y
+    // advance by these element strides (0 for ordinary convs)
+    int64_t bsa, bsw, bsy;
 };
 
 struct Epi {
@@ -140,6 +143,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
         m0 = (T / nby) * BM;
         n0 = (int)(T % nby) * BN;
+    }
+    if (blockIdx.z) {
+        p.a += blockIdx.z * p.bsa;
+        p.w += blockIdx.z * p.bsw;
+        e.y += blockIdx.z * p.bsy;
     }
     const int taps_kd = p.kd, taps_kwkd = p.kw * p.kd;
     const int ntaps = p.kh * taps_kwkd;
@@ -350,7 +358,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
     const int wi = wave / WJ, wj = wave % WJ;
     const int k0 = blockIdx.x * BI;
     const int n0 = blockIdx.y * BJ;
-    const int64_t ms = (int64_t)blockIdx.z * m_per_split;
+    const int64_t nsplit = (p.M + m_per_split - 1) / m_per_split;
+    const int64_t batch = blockIdx.z / nsplit;
+    if (batch) {
+        p.a += batch * p.bsa;
+        dz += batch * p.bsw;
+        dw += batch * p.bsy;
+    }
+    const int64_t ms = (int64_t)(blockIdx.z % nsplit) * m_per_split;
     int64_t me = ms + m_per_split;
     if (me > p.M) me = p.M;
     if (ms >= me) return;
@@ -483,27 +498,27 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 
 // ------------------------------------------------------------------ dispatch
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC>
-static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s) {
-    dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN));
+static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
+    dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC>), grid, dim3(256), 0, s, p, e);
 }
 
 template <bool BT, bool AVEC>
-static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s) {
+static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch = 1) {
     if (p.N <= 32) {
-        launch_gemm<128, 32, 4, 1, BT, AVEC>(p, e, s);
+        launch_gemm<128, 32, 4, 1, BT, AVEC>(p, e, s, nbatch);
     } else if (p.N <= 64) {
-        launch_gemm<128, 64, 4, 1, BT, AVEC>(p, e, s);
+        launch_gemm<128, 64, 4, 1, BT, AVEC>(p, e, s, nbatch);
     } else {
-        const int64_t blocks128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
-        if (blocks128 < 512) launch_gemm<64, 128, 2, 2, BT, AVEC>(p, e, s);
-        else launch_gemm<128, 128, 2, 2, BT, AVEC>(p, e, s);
+        const int64_t blocks128 = ((p.M + 127) / 128) * ((p.N + 127) / 128) * nbatch;
+        if (blocks128 < 512) launch_gemm<64, 128, 2, 2, BT, AVEC>(p, e, s, nbatch);
+        else launch_gemm<128, 128, 2, 2, BT, AVEC>(p, e, s, nbatch);
     }
 }
 
 template <int BI, int BJ, int WI, int WJ, bool AVEC>
-static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s) {
-    const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ);
+static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s, int nbatch = 1) {
+    const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;                   // aim >= 1024 blocks
     const int64_t max_splits = (p.M + 1023) / 1024;                 // >= 1024 m per block
     if (splits > max_splits) splits = max_splits;
@@ -511,9 +526,331 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
     int64_t mper = (p.M + splits - 1) / splits;
     mper = (mper + 31) / 32 * 32;
     splits = (p.M + mper - 1) / mper;
-    dim3 grid((unsigned)((p.K + BI - 1) / BI), (unsigned)((p.N + BJ - 1) / BJ), (unsigned)splits);
+    dim3 grid((unsigned)((p.K + BI - 1) / BI), (unsigned)((p.N + BJ - 1) / BJ),
+              (unsigned)(splits * nbatch));
     hipLaunchKernelGGL((conv_wgrad_kernel<BI, BJ, WI, WJ, AVEC>), grid, dim3(256), 0, s, p, dz, dw,
                        mper);
+}
+
+
+// =========================================================================
+// Winograd F(2x2x2, 3x3x3) for stride-1 'same' 3x3x3 convs.
+//   fwd:   Y   = A^T [ (G W G^T) . (B^T X B) ] A        (per 2^3 output tile)
+//   dgrad: dX  = same with W'[t][n][c] = W[flip t][c][n]
+//   wgrad: dW  = G^T [ sum_tiles (B^T X B) . (A dZ A^T) ] G
+// 1-D matrices (F(2,3), points 0, 1, -1, inf):
+//   B^T d = [d0-d2, d1+d2, d2-d1, d1-d3]      G g = [g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2]
+//   A^T m = [m0+m1+m2, m1-m2-m3]              A e = [e0, e0+e1, e0-e1, -e1]
+//   G^T v = [v0+(v1+v2)/2, (v1-v2)/2, (v1+v2)/2+v3]
+// The 64 point-wise products become 64 independent GEMMs (one per point xi)
+// run by the same MFMA kernels in batched mode: 3.375x fewer FLOPs than the
+// direct implicit GEMM.  Transformed operands live in a caller workspace,
+// xi-major: U[64][T][C], V[64][K][N], M[64][T][N].
+// =========================================================================
+struct WinoGeom {
+    int B, H, W, D, TY, TX, TZ;
+    int64_t T;
+};
+
+__device__ __forceinline__ void bt4(float& a0, float& a1, float& a2, float& a3) {
+    const float t0 = a0 - a2, t1 = a1 + a2, t2 = a2 - a1, t3 = a1 - a3;
+    a0 = t0; a1 = t1; a2 = t2; a3 = t3;
+}
+
+__device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b, int& ty, int& tx,
+                                            int& tz) {
+    tz = (int)(t % g.TZ);
+    int64_t r = t / g.TZ;
+    tx = (int)(r % g.TX);
+    r /= g.TX;
+    ty = (int)(r % g.TY);
+    b = (int)(r / g.TY);
+}
+
+// U[xi][t][c] = (B^T (x) B^T (x) B^T) d, d = the 4^3 input tile at (2ty-1, 2tx-1, 2tz-1).
+__global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
+                                                         int C, float* __restrict__ U) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.T * C) return;
+    const int c = (int)(i % C);
+    const int64_t t = i / C;
+    int b, ty, tx, tz;
+    tile_coords(t, g, b, ty, tx, tz);
+    float d[4][4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int y = 2 * ty - 1 + a;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const int xx = 2 * tx - 1 + bb;
+            const bool ok = y >= 0 && y < g.H && xx >= 0 && xx < g.W;
+            const float* row = x + ((((int64_t)b * g.H + y) * g.W + xx) * g.D) * C + c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int z = 2 * tz - 1 + k;
+                d[a][bb][k] = (ok && z >= 0 && z < g.D) ? row[(int64_t)z * C] : 0.0f;
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) bt4(d[a][bb][0], d[a][bb][1], d[a][bb][2], d[a][bb][3]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bt4(d[a][0][k], d[a][1][k], d[a][2][k], d[a][3][k]);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bt4(d[0][bb][k], d[1][bb][k], d[2][bb][k], d[3][bb][k]);
+    const int64_t stride = g.T * C;
+    float* o = U + t * C + c;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[(int64_t)((a * 4 + bb) * 4 + k) * stride] = d[a][bb][k];
+}
+
+__device__ __forceinline__ void g3(float g0, float g1, float g2, float* o) {
+    o[0] = g0;
+    o[1] = (g0 + g1 + g2) * 0.5f;
+    o[2] = (g0 - g1 + g2) * 0.5f;
+    o[3] = g2;
+}
+
+// V[xi][k'][n'] = (G (x) G (x) G) w.  fwd: k'=cin, n'=cout; bwd (transpose_flip):
+// k'=cout, n'=cin, w taken at the flipped tap.
+__global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restrict__ w, int Cin,
+                                                          int Cout, int transpose_flip,
+                                                          float* __restrict__ V) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t KN = (int64_t)Cin * Cout;
+    if (i >= KN) return;
+    int cin, cout, kp, np_, Np;
+    if (!transpose_flip) { cout = (int)(i % Cout); cin = (int)(i / Cout); kp = cin; np_ = cout; Np = Cout; }
+    else { cin = (int)(i % Cin); cout = (int)(i / Cin); kp = cout; np_ = cin; Np = Cin; }
+    float gw[3][3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int t = transpose_flip ? ((2 - a) * 3 + (2 - b)) * 3 + (2 - k) : (a * 3 + b) * 3 + k;
+                gw[a][b][k] = w[(int64_t)t * KN + (int64_t)cin * Cout + cout];
+            }
+    float t1[3][3][4];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) g3(gw[a][b][0], gw[a][b][1], gw[a][b][2], t1[a][b]);
+    float t2[3][4][4];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float o[4];
+            g3(t1[a][0][k], t1[a][1][k], t1[a][2][k], o);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) t2[a][b][k] = o[b];
+        }
+    float* out = V + (int64_t)kp * Np + np_;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float o[4];
+            g3(t2[0][b][k], t2[1][b][k], t2[2][b][k], o);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + b) * 4 + k) * KN] = o[a];
+        }
+}
+
+__device__ __forceinline__ void at4(float m0, float m1, float m2, float m3, float& o0, float& o1) {
+    o0 = m0 + m1 + m2;
+    o1 = m1 - m2 - m3;
+}
+
+// Y tile (2^3) = (A^T (x) A^T (x) A^T) M[.][t][n], then the conv epilogue.
+__global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, WinoGeom g,
+                                                          int N, Epi e) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.T * N) return;
+    const int n = (int)(i % N);
+    const int64_t t = i / N;
+    int b, ty, tx, tz;
+    tile_coords(t, g, b, ty, tx, tz);
+    const int64_t stride = g.T * N;
+    const float* src = Mt + t * N + n;
+    float m[4][4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[a][bb][k] = src[(int64_t)((a * 4 + bb) * 4 + k) * stride];
+    float r1[4][4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+            at4(m[a][bb][0], m[a][bb][1], m[a][bb][2], m[a][bb][3], r1[a][bb][0], r1[a][bb][1]);
+    float r2[4][2][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
+    float o[2][2][2];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
+    const float bias = e.bias ? e.bias[n] : 0.0f;
+    const float sc = e.scale ? e.scale[n] : 1.0f, sh = e.scale ? e.shift[n] : 0.0f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int y = 2 * ty + a;
+        if (y >= g.H) continue;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int xx = 2 * tx + bb;
+            if (xx >= g.W) continue;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int z = 2 * tz + k;
+                if (z >= g.D) continue;
+                const int64_t row = (((int64_t)b * g.H + y) * g.W + xx) * g.D + z;
+                float v = o[a][bb][k];
+                if (e.bias) v += bias;
+                if (e.z) e.z[row * N + n] = v;
+                if (e.scale) v = v * sc + sh;
+                if (e.res_mode == 1) v += e.res[row * e.ldy + n];
+                if (e.relu) v = v > 0.0f ? v : 0.0f;
+                float* dst = e.y + row * e.ldy + n;
+                if (e.accumulate) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
+// DY[xi][t][n] = (A (x) A (x) A) e, e = the 2^3 output-gradient tile (0 outside).
+__global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict__ dz, WinoGeom g,
+                                                        int N, float* __restrict__ DY) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.T * N) return;
+    const int n = (int)(i % N);
+    const int64_t t = i / N;
+    int b, ty, tx, tz;
+    tile_coords(t, g, b, ty, tx, tz);
+    float ev[2][2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int y = 2 * ty + a, xx = 2 * tx + bb, z = 2 * tz + k;
+                ev[a][bb][k] = (y < g.H && xx < g.W && z < g.D)
+                                   ? dz[((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * N + n]
+                                   : 0.0f;
+            }
+    auto A4 = [](float e0, float e1, float* o) { o[0] = e0; o[1] = e0 + e1; o[2] = e0 - e1; o[3] = -e1; };
+    float t1[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) A4(ev[a][bb][0], ev[a][bb][1], t1[a][bb]);
+    float t2[2][4][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float o[4];
+            A4(t1[a][0][k], t1[a][1][k], o);
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) t2[a][bb][k] = o[bb];
+        }
+    const int64_t stride = g.T * N;
+    float* out = DY + t * N + n;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float o[4];
+            A4(t2[0][bb][k], t2[1][bb][k], o);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + bb) * 4 + k) * stride] = o[a];
+        }
+}
+
+__device__ __forceinline__ void gt4(float v0, float v1, float v2, float v3, float* o) {
+    o[0] = v0 + (v1 + v2) * 0.5f;
+    o[1] = (v1 - v2) * 0.5f;
+    o[2] = (v1 + v2) * 0.5f + v3;
+}
+
+// dW[t][c][n] += (G^T (x) G^T (x) G^T) dWh[.][c][n]
+__global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ dWh, int C,
+                                                             int N, float* __restrict__ dw) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t CN = (int64_t)C * N;
+    if (i >= CN) return;
+    float v[4][4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[a][b][k] = dWh[(int64_t)((a * 4 + b) * 4 + k) * CN + i];
+    float t1[4][4][3];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) gt4(v[a][b][0], v[a][b][1], v[a][b][2], v[a][b][3], t1[a][b]);
+    float t2[4][3][3];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float o[3];
+            gt4(t1[a][0][k], t1[a][1][k], t1[a][2][k], t1[a][3][k], o);
+#pragma unroll
+            for (int b = 0; b < 3; ++b) t2[a][b][k] = o[b];
+        }
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float o[3];
+            gt4(t2[0][b][k], t2[1][b][k], t2[2][b][k], t2[3][b][k], o);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) dw[(int64_t)((a * 3 + b) * 3 + k) * CN + i] += o[a];
+        }
+}
+
+static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D) {
+    WinoGeom g;
+    g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D;
+    g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + 1) / 2);
+    g.T = B * g.TY * g.TX * g.TZ;
+    return g;
+}
+
+// batched GEMM view over the 64 Winograd points: rows = tiles
+static ConvP wino_gemm_p(const float* A, int64_t T, int K, const float* V, int N) {
+    ConvP p{};
+    p.a = A; p.B = 1; p.H = (int)T; p.W = 1; p.D = 1; p.C = K;
+    p.OH = (int)T; p.OW = 1; p.OD = 1;
+    p.kh = p.kw = p.kd = 1; p.sy = p.sx = p.sz = 1;
+    p.M = T; p.K = K; p.w = V; p.N = N;
+    p.bsa = T * K; p.bsw = (int64_t)K * N; p.bsy = T * N;
+    return p;
 }
 
 }  // namespace m3d
@@ -551,7 +888,7 @@ extern "C" int m3d_conv3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, i
     if (res_mode == 2 && ((OH & 1) || (OW & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
     if (split_n > 0 && y2 == nullptr) return einval("conv3d: split output needs y2");
     ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
-            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0};
+            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0, 0, 0, 0};
     Epi e{bias, bn_scale, bn_shift, residual, res_mode, relu, z_out, y, ldy > 0 ? ldy : Cout,
           y2, ldy2, (int)split_n, (int)OH, (int)OW, (int)OD, 1, 1, 1, 0, 1};
     if (Cin % 32 == 0) dispatch_gemm<false, true>(p, e, st(s));
@@ -571,7 +908,7 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
     const bool unit = kh == 1 && kw == 1 && kd == 1;
     if (!unit && (sy != 1 || sx != 1 || sz != 1))
         return einval("conv3d bwd-data: strided convs supported for 1x1x1 kernels only");
-    ConvP p;
+    ConvP p{};
     Epi e{};
     e.y = dx;
     e.ldy = Cin;
@@ -618,7 +955,7 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
     if (rc) return rc;
     ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
-            (int)Cout, 0};
+            (int)Cout, 0, 0, 0, 0};
     const bool vec = (Cin % 4) == 0;
     if (Cout <= 64) {
         if (vec) launch_wgrad<128, 64, 2, 2, true>(p, dz, dw, st(s));
@@ -628,4 +965,113 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
         else launch_wgrad<128, 128, 2, 2, false>(p, dz, dw, st(s));
     }
     return check_launch("conv_wgrad_kernel");
+}
+
+// ---- Winograd entry points -------------------------------------------------
+static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, int64_t Cout) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0 || Cin <= 0 || Cout <= 0)
+        return einval("conv3d winograd: tensor dimensions must be positive");
+    if (Cin % 32 || Cout % 32) return einval("conv3d winograd: Cin and Cout must be multiples of 32");
+    if (B * H * W * D > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
+    return M3D_OK;
+}
+
+extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
+                                                  int64_t Cin, int64_t Cout) {
+    const WinoGeom g = wino_geom(B, H, W, D);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + al(sizeof(float) * 64 * (size_t)g.T * Cin) +
+           al(sizeof(float) * 64 * (size_t)g.T * Cout);
+}
+
+struct WinoWs { float *V, *U, *M; };
+static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    char* p = (char*)ws;
+    WinoWs w;
+    w.V = (float*)p; p += al(sizeof(float) * 64 * (size_t)Cin * Cout);
+    w.U = (float*)p; p += al(sizeof(float) * 64 * (size_t)g.T * Cin);
+    w.M = (float*)p;
+    return w;
+}
+
+extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                   int64_t Cin, const float* w, int64_t Cout, const float* bias,
+                                   const float* bn_scale, const float* bn_shift,
+                                   const float* residual, int32_t relu, float* z_out, float* y,
+                                   void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, Cin, Cout);
+    if (rc) return rc;
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+        return einval("conv3d winograd: workspace too small");
+    const WinoGeom g = wino_geom(B, H, W, D);
+    WinoWs ws = wino_ws(workspace, g, Cin, Cout);
+    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+                       (int)Cin, (int)Cout, 0, ws.V);
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
+                       (int)Cin, ws.U);
+    ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
+    Epi e{};
+    e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = (int)g.T; e.YW = 1; e.YD = 1;
+    e.ysy = e.ysx = e.ysz = 1;
+    dispatch_gemm<false, true>(p, e, st(s), 64);
+    Epi o{};
+    o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
+    o.res_mode = residual ? 1 : 0; o.relu = relu; o.z = z_out; o.y = y; o.ldy = Cout;
+    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), ws.M,
+                       g, (int)Cout, o);
+    return check_launch("conv3d winograd fwd");
+}
+
+extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H,
+                                        int64_t W, int64_t D, int64_t Cin, int64_t Cout, float* dx,
+                                        int32_t accumulate, void* workspace, size_t ws_bytes,
+                                        m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, Cin, Cout);
+    if (rc) return rc;
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+        return einval("conv3d winograd: workspace too small");
+    const WinoGeom g = wino_geom(B, H, W, D);
+    // same layout with the roles of Cin/Cout swapped (V'[64][Cout][Cin], U'[64][T][Cout])
+    WinoWs ws = wino_ws(workspace, g, Cout, Cin);
+    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+                       (int)Cin, (int)Cout, 1, ws.V);
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+                       (int)Cout, ws.U);
+    ConvP p = wino_gemm_p(ws.U, g.T, (int)Cout, ws.V, (int)Cin);
+    Epi e{};
+    e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = (int)g.T; e.YW = 1; e.YD = 1;
+    e.ysy = e.ysx = e.ysz = 1;
+    dispatch_gemm<false, true>(p, e, st(s), 64);
+    Epi o{};
+    o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
+    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
+                       g, (int)Cin, o);
+    return check_launch("conv3d winograd bwd-data");
+}
+
+extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H,
+                                          int64_t W, int64_t D, int64_t Cin, int64_t Cout,
+                                          float* dw, void* workspace, size_t ws_bytes,
+                                          m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, Cin, Cout);
+    if (rc) return rc;
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+        return einval("conv3d winograd: workspace too small");
+    const WinoGeom g = wino_geom(B, H, W, D);
+    WinoWs ws = wino_ws(workspace, g, Cin, Cout);   // V <- dW_hat, U <- B^T x, M <- A dz
+    if (hipMemsetAsync(ws.V, 0, sizeof(float) * 64 * (size_t)Cin * Cout, st(s)) != hipSuccess)
+        return check_launch("memset dW_hat");
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
+                       (int)Cin, ws.U);
+    hipLaunchKernelGGL(wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+                       (int)Cout, ws.M);
+    ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, nullptr, (int)Cout);
+    p.bsw = g.T * Cout;                 // dz (DY) batch stride
+    p.bsy = (int64_t)Cin * Cout;        // dW_hat batch stride
+    if (Cout <= 64) launch_wgrad<128, 64, 2, 2, true>(p, ws.M, ws.V, st(s), 64);
+    else launch_wgrad<128, 128, 2, 2, true>(p, ws.M, ws.V, st(s), 64);
+    hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s),
+                       ws.V, (int)Cin, (int)Cout, dw);
+    return check_launch("conv3d winograd bwd-weight");
 }

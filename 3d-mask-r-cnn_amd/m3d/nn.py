@@ -7,7 +7,7 @@ gradients.  Layout is channels-last [B,H,W,D,C] throughout, as the reference.
 """
 from __future__ import annotations
 
-import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -18,6 +18,23 @@ from ._lib import check, ptr, stream
 
 def _L():
     return _lib.load()
+
+
+# Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
+WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
+WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "128"))
+
+
+def use_winograd(geo, cin, cout):
+    # below 128 channels the (bandwidth-bound) transforms cost more than the
+    # 3.375x MFMA saving (measured: res2*_branch2b 64->64 is no faster)
+    return (WINOGRAD and geo.k == (3, 3, 3) and geo.stride == (1, 1, 1) and geo.pad == (1, 1, 1)
+            and cin % 32 == 0 and cout % 32 == 0 and min(cin, cout) >= WINO_MIN_C)
+
+
+def _wino_ws(B, H, W, D, cin, cout, dev):
+    n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, cin, cout))
+    return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
 
 
 def same_out_pad(n, k, s):
@@ -89,10 +106,17 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.bn = (mean, rstd, scale)
         else:
             ctx.bn = None
-        check(_L().m3d_conv3d_fwd(ptr(x), B, H, W, D, Cin, ptr(w), kh, kw, kd, Cout, OH, OW, OD,
-                                  *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
-                                  ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
-                                  None, 0, 0, stream()), "conv3d_fwd")
+        ctx.wino = use_winograd(geo, Cin, Cout) and res_mode != 2
+        if ctx.wino:
+            ws, wsb = _wino_ws(B, H, W, D, Cin, Cout, x.device)
+            check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, ptr(b), ptr(scale),
+                                           ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
+                                           ptr(ws), wsb, stream()), "conv3d_fwd_wino")
+        else:
+            check(_L().m3d_conv3d_fwd(ptr(x), B, H, W, D, Cin, ptr(w), kh, kw, kd, Cout, OH, OW, OD,
+                                      *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
+                                      ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
+                                      None, 0, 0, stream()), "conv3d_fwd")
         ctx.save_for_backward(x, w, y, z)
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -125,6 +149,18 @@ class _ConvBNAct(torch.autograd.Function):
                 mean, rstd, scale = ctx.bn
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
+        if ctx.wino:
+            ws, wsb = _wino_ws(B, H, W, D, Cin, Cout, x.device)
+            if grads.get("kernel") is not None:
+                check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout,
+                                                   ptr(grads["kernel"]), ptr(ws), wsb, stream()),
+                      "conv3d_bwd_weight_wino")
+            dx = None
+            if ctx.need_dx:
+                dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+                check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, ptr(dx), 0,
+                                                 ptr(ws), wsb, stream()), "conv3d_bwd_data_wino")
+            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                           OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),

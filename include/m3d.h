@@ -165,6 +165,24 @@ int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,
                           int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dw,
                           m3d_stream_t s);
 
+/* Winograd F(2x2x2,3x3x3) versions of the three passes for stride-1 'same'
+ * 3x3x3 convs (every 3x3x3 conv of the graph: res*_branch2b, fpn_p*,
+ * rpn_conv_shared1): 3.375x fewer multiplies, the 64 point-wise products run
+ * as batched fp32-MFMA GEMMs.  Cin, Cout multiples of 32.  Same epilogue as
+ * m3d_conv3d_fwd (res_mode 1 only).  workspace: m3d_conv3d_wino_workspace_bytes. */
+size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                                       int64_t Cout);
+int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                        const float* w, int64_t Cout, const float* bias, const float* bn_scale,
+                        const float* bn_shift, const float* residual, int32_t relu, float* z_out,
+                        float* y, void* workspace, size_t ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                             int64_t D, int64_t Cin, int64_t Cout, float* dx, int32_t accumulate,
+                             void* workspace, size_t ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
+                               int64_t D, int64_t Cin, int64_t Cout, float* dw, void* workspace,
+                               size_t ws_bytes, m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
  * ------------------------------------------------------------------------- */

@@ -61,9 +61,13 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("wino", [True, False], ids=["wino", "direct"])
 @pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
-def test_conv_block_fwd_bwd(cuda, case):
+def test_conv_block_fwd_bwd(cuda, case, wino, monkeypatch):
+    import m3d.nn as mnn
     from m3d.nn import conv_bn_act, conv_geom
+    monkeypatch.setattr(mnn, "WINOGRAD", wino)
+    monkeypatch.setattr(mnn, "WINO_MIN_C", 32)
     sp, cin, cout, k, stride, padding, use_bn, relu, use_res = case
     rng = np.random.default_rng(abs(hash(str(case))) % 2**32)
     x = torch.tensor(rng.normal(size=(2, *sp, cin)), dtype=torch.float32)
