@@ -398,11 +398,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
     decompose(ms + xrow0 < me ? ms + xrow0 : ms, p.OH, p.OW, p.OD, cb_, cy_, cx_, cz_);
     auto advance = [&](int& b, int& y, int& x, int& z, int delta) {
         z += delta;
-        while (z >= p.OD) {
-            z -= p.OD;
-            if (++x == p.OW) {
-                x = 0;
-                if (++y == p.OH) { y = 0; ++b; }
+        if (z >= p.OD) {                 // rare when OD >= 32: carry by division
+            x += z / p.OD;
+            z %= p.OD;
+            if (x >= p.OW) {
+                y += x / p.OW;
+                x %= p.OW;
+                if (y >= p.OH) {
+                    b += y / p.OH;
+                    y %= p.OH;
+                }
             }
         }
     };
@@ -845,8 +850,8 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D) {
 // batched GEMM view over the 64 Winograd points: rows = tiles
 static ConvP wino_gemm_p(const float* A, int64_t T, int K, const float* V, int N) {
     ConvP p{};
-    p.a = A; p.B = 1; p.H = (int)T; p.W = 1; p.D = 1; p.C = K;
-    p.OH = (int)T; p.OW = 1; p.OD = 1;
+    p.a = A; p.B = 1; p.H = 1; p.W = 1; p.D = (int)T; p.C = K;      // tiles along "z":
+    p.OH = 1; p.OW = 1; p.OD = (int)T;                                // no carries in m loops
     p.kh = p.kw = p.kd = 1; p.sy = p.sx = p.sz = 1;
     p.M = T; p.K = K; p.w = V; p.N = N;
     p.bsa = T * K; p.bsw = (int64_t)K * N; p.bsy = T * N;
@@ -1012,7 +1017,7 @@ extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t
                        (int)Cin, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
     Epi e{};
-    e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = (int)g.T; e.YW = 1; e.YD = 1;
+    e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
     dispatch_gemm<false, true>(p, e, st(s), 64);
     Epi o{};
@@ -1040,7 +1045,7 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
                        (int)Cout, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cout, ws.V, (int)Cin);
     Epi e{};
-    e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = (int)g.T; e.YW = 1; e.YD = 1;
+    e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
     dispatch_gemm<false, true>(p, e, st(s), 64);
     Epi o{};
