@@ -66,6 +66,20 @@ struct Epi {
     int simple;       // y row == m (same grid, unit store stride)
 };
 
+// Raw buffer loads: 32-bit byte offsets, and an out-of-range offset returns 0
+// -- used for the implicit zero padding of im2col so the loaders are
+// branch-free (no exec-mask divergence around every load).
+#define M3D_OOB 0xFFFFFFF0u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)(uint32_t)(bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : bytes),
+                                             0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return *reinterpret_cast<float4*>(&v);
+}
+
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
@@ -152,10 +166,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
     const int taps_kd = p.kd, taps_kwkd = p.kw * p.kd;
     const int ntaps = p.kh * taps_kwkd;
 
-    // per-thread A rows (vector path): base coordinates
-    int a_b[AVEC ? AQ : 1], a_y[AVEC ? AQ : 1], a_x[AVEC ? AQ : 1], a_z[AVEC ? AQ : 1];
+    // per-thread A rows (vector path): base coordinates and 32-bit element
+    // offsets (tensor bytes < 4 GiB is checked on the host)
+    int a_y[AVEC ? AQ : 1], a_x[AVEC ? AQ : 1], a_z[AVEC ? AQ : 1], a_off[AVEC ? AQ : 1];
     bool a_ok[AVEC ? AQ : 1];
     const int a_col4 = tid & 7;
+    const int rowW = p.D * p.C, rowH = p.W * rowW;
     if (AVEC) {
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
@@ -163,12 +179,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
             a_ok[q] = m < p.M;
             int b, oy, ox, oz;
             decompose(a_ok[q] ? m : 0, p.OH, p.OW, p.OD, b, oy, ox, oz);
-            a_b[q] = b;
             a_y[q] = oy * p.sy - p.py;
             a_x[q] = ox * p.sx - p.px;
             a_z[q] = oz * p.sz - p.pz;
+            a_off[q] = ((b * p.H + a_y[q]) * p.W + a_x[q]) * rowW + a_z[q] * p.C + a_col4 * 4;
         }
     }
+    const __amdgpu_buffer_rsrc_t rsA =
+        make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
+    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.w, (uint64_t)p.K * p.N * 4);
 
     float4 ra[AVEC ? AQ : 1];
     float rs[AVEC ? 1 : AQ];
@@ -180,18 +199,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
             const int tap = k0 / p.C;
             const int c0 = k0 - tap * p.C;
             const int ky = tap / taps_kwkd, kx = (tap / taps_kd) % p.kw, kz = tap % taps_kd;
+            const int toff = ky * rowH + kx * rowW + kz * p.C + c0;
 #pragma unroll
             for (int q = 0; q < AQ; ++q) {
-                const int iy = a_y[q] + ky, ix = a_x[q] + kx, iz = a_z[q] + kz;
-                const bool ok = a_ok[q] && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && iz >= 0 &&
-                                iz < p.D;
-                if (ok) {
-                    const int64_t off = ((((int64_t)a_b[q] * p.H + iy) * p.W + ix) * p.D + iz) * p.C +
-                                        c0 + a_col4 * 4;
-                    ra[q] = *reinterpret_cast<const float4*>(p.a + off);
-                } else {
-                    ra[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
+                const bool ok = a_ok[q] && (unsigned)(a_y[q] + ky) < (unsigned)p.H &&
+                                (unsigned)(a_x[q] + kx) < (unsigned)p.W &&
+                                (unsigned)(a_z[q] + kz) < (unsigned)p.D;
+                ra[q] = bload4(rsA, ok ? (uint32_t)(a_off[q] + toff) * 4u : M3D_OOB);
             }
         } else {
             const int col = tid & 31;
@@ -224,9 +238,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
                 const int idx = tid + 256 * q;
                 const int kr = idx / C4, c4 = idx % C4;
                 const int k = k0 + kr, n = n0 + c4 * 4;
-                rb[q] = (k < p.K && n < p.N)
-                            ? *reinterpret_cast<const float4*>(p.w + (int64_t)k * p.N + n)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                rb[q] = bload4(rsB, (k < p.K && n < p.N) ? (uint32_t)(k * p.N + n) * 4u : M3D_OOB);
             }
         } else {
             // B(k=(t,c'), n) = w[(t'*N + n)*C + c'], tile rows n, 32 contiguous c'
@@ -236,9 +248,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
 #pragma unroll
             for (int q = 0; q < BQ; ++q) {
                 const int n = n0 + (tid >> 3) + 32 * q;
-                rb[q] = n < p.N ? *reinterpret_cast<const float4*>(
-                                      p.w + ((int64_t)wt * p.N + n) * p.C + c0 + a_col4 * 4)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                rb[q] = bload4(rsB, n < p.N ? (uint32_t)((wt * p.N + n) * p.C + c0 + a_col4 * 4) * 4u
+                                            : M3D_OOB);
             }
         }
     };
@@ -411,31 +422,31 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
             }
         }
     };
+    const __amdgpu_buffer_rsrc_t rsX =
+        make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
+    const __amdgpu_buffer_rsrc_t rsG = make_rsrc(dz, (uint64_t)p.M * p.N * 4);
+    const int rowWx = p.D * p.C, rowHx = p.W * rowWx;
     auto load_tile = [&](int64_t mb) {
         int rb = cb_, ry = cy_, rx = cx_, rz = cz_;
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
             const int64_t m = mb + xrow0 + XRSTEP * q;
             if (q > 0) advance(rb, ry, rx, rz, XRSTEP);
-            bool ok = kok && m < me;
-            int64_t off = 0;
-            if (ok) {
-                const int b = rb, oy = ry, ox = rx, oz = rz;
-                const int iy = oy * p.sy - p.py + ky, ix = ox * p.sx - p.px + kx,
-                          iz = oz * p.sz - p.pz + kz;
-                ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && iz >= 0 && iz < p.D;
-                off = ((((int64_t)b * p.H + iy) * p.W + ix) * p.D + iz) * p.C + cc;
-            }
-            if (AVEC) rx4[q] = ok ? *reinterpret_cast<const float4*>(p.a + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-            else rx1[q] = ok ? p.a[off] : 0.0f;
+            const int iy = ry * p.sy - p.py + ky, ix = rx * p.sx - p.px + kx,
+                      iz = rz * p.sz - p.pz + kz;
+            const bool ok = kok && m < me && (unsigned)iy < (unsigned)p.H &&
+                            (unsigned)ix < (unsigned)p.W && (unsigned)iz < (unsigned)p.D;
+            const uint32_t off = ok ? (uint32_t)((rb * p.H + iy) * rowHx + ix * rowWx + iz * p.C + cc) * 4u
+                                    : M3D_OOB;
+            if (AVEC) rx4[q] = bload4(rsX, off);
+            else rx1[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, (int)off, 0, 0));
         }
         advance(cb_, cy_, cx_, cz_, BKM);
 #pragma unroll
         for (int q = 0; q < GQ; ++q) {
             const int64_t m = mb + grow0 + GRSTEP * q;
             const int n = n0 + gcol * 4;
-            rg[q] = (m < me && n < p.N) ? *reinterpret_cast<const float4*>(dz + m * p.N + n)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            rg[q] = bload4(rsG, (m < me && n < p.N) ? (uint32_t)(m * p.N + n) * 4u : M3D_OOB);
         }
     };
     auto store_tile = [&](int buf) {
@@ -874,6 +885,11 @@ static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, i
     if ((int64_t)kh * kw * kd * Cin > 0x7FFFFFFF) return einval("conv3d: K too large");
     if (B * H * W * D > 0x7FFFFFFF || B * OH * OW * OD > 0x7FFFFFFF)
         return einval("conv3d: more than 2^31 voxels per tensor");
+    // 32-bit buffer addressing: every operand below 4 GiB
+    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
+    if (B * H * W * D * Cin >= lim || B * OH * OW * OD * Cout >= lim ||
+        (int64_t)kh * kw * kd * Cin * Cout >= lim)
+        return einval("conv3d: operand larger than 4 GiB (32-bit buffer offsets)");
     return M3D_OK;
 }
 
