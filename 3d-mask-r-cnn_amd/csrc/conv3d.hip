@@ -873,6 +873,30 @@ static ConvP wino_gemm_p(const float* A, int64_t T, int K, const float* V, int N
 
 using namespace m3d;
 
+// Plain batched fp32 GEMM on the conv MFMA kernel: C[b] (+)= act(A[b] B[b] + bias).
+// A [M][K], B [K][N], C [M][N] row-major, batches contiguous.  Runs the same
+// conv_gemm_kernel instantiations as the Winograd point-wise GEMMs (a GEMM is
+// a 1x1x1 conv whose voxels lie along "z").
+extern "C" int m3d_gemm_f32(const float* A, const float* Bm, float* C, int64_t batch, int64_t M,
+                            int64_t K, int64_t N, const float* bias, int32_t relu,
+                            int32_t accumulate, m3d_stream_t s) {
+    if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm: dimensions must be positive");
+    if (N % 4) return einval("gemm: N must be a multiple of 4");
+    if (M > 0x7FFFFFFF || K > 0x7FFFFFFF || N > 0x7FFFFFFF)
+        return einval("gemm: dimension larger than 2^31");
+    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
+    if (M * K >= lim || K * N >= lim || M * N >= lim)
+        return einval("gemm: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p = wino_gemm_p(A, M, (int)K, Bm, (int)N);
+    Epi e{};
+    e.bias = bias; e.relu = relu; e.accumulate = accumulate;
+    e.y = C; e.ldy = N; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)M;
+    e.ysy = e.ysx = e.ysz = 1;
+    if (K % 32 == 0) dispatch_gemm<false, true>(p, e, st(s), (int)batch);
+    else dispatch_gemm<false, false>(p, e, st(s), (int)batch);
+    return check_launch("m3d_gemm_f32");
+}
+
 static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, int32_t kh,
                       int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
                       int32_t sy, int32_t sx, int32_t sz) {

@@ -37,9 +37,67 @@ def log(*a):
 
 
 # ---------------------------------------------------------------- dominant kernel
-def time_dominant_conv(model, fmaps, reps=5):
-    """The largest conv of the step: RPN head rpn_conv_shared1 (3x3x3, 256->512) on P2.
-    Timed with HIP events on the stream it is launched on (torch's current stream)."""
+def _event_time(fn, reps):
+    """Average seconds per call of fn(), HIP events on torch's current stream
+    (the stream every libm3d launch of fn() is enqueued on)."""
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps / 1e3
+
+
+def _pmc_traffic(kernel_key):
+    """HBM bytes per launch of the same launch, measured by rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (scripts/gpu_prof.sh, gfx950 FETCH x2
+    correction) and committed under profiles/; None if not measured."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        return json.load(open(path)).get(kernel_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def wino_gemm_shape(S):
+    """The step's largest launch of its dominant kernel (conv_gemm_kernel):
+    the 64 batched Winograd point-wise GEMMs of rpn_conv_shared1 (3x3x3,
+    256->512) on P2 [S/4, S/4, S]: M = T = 2x2x2 output tiles, K = 256, N = 512."""
+    q = S // 4
+    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + 1) // 2)
+    return 64, T, 256, 512
+
+
+def time_dominant_kernel(S, reps=5):
+    from m3d import _lib
+    L = _lib.load()
+    nb, T, K, N = wino_gemm_shape(S)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn((nb, T, K), device="cuda", generator=g)
+    Bm = torch.randn((nb, K, N), device="cuda", generator=g) * 0.05
+    C = torch.empty((nb, T, N), device="cuda")
+
+    def launch():
+        _lib.check(L.m3d_gemm_f32(A.data_ptr(), Bm.data_ptr(), C.data_ptr(), nb, T, K, N, None, 0, 0,
+                                  _lib.stream()), "gemm")
+    t = _event_time(launch, reps)
+    flops = 2.0 * nb * T * K * N
+    key = f"wino_gemm_rpn_shared1_S{S}"
+    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": _pmc_traffic(key),
+            "kernel": f"conv_gemm_kernel<128,128> (fp32 MFMA): 64 batched Winograd GEMMs of "
+                      f"rpn_conv_shared1 on P2, M={T} K={K} N={N}",
+            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
+            "algorithmic_bytes_per_launch": 4.0 * nb * (T * K + K * N + T * N),
+            "direct_conv_equivalent_tflops": round(2.0 * T * 8 * 27 * K * N / t / 1e12, 2)}
+
+
+def time_direct_conv(model, fmaps, reps=5):
+    """rpn_conv_shared1 (3x3x3, 256->512) on P2 as the direct implicit GEMM."""
     from m3d import _lib
     from m3d.nn import conv_geom
     L = _lib.load()
@@ -54,20 +112,11 @@ def time_dominant_conv(model, fmaps, reps=5):
                                     512, H, W, D, 1, 1, 1, *geo.pad, layer.bias.data.data_ptr(), None,
                                     None, None, 0, 1, None, y.data_ptr(), 512, None, 0, 0,
                                     _lib.stream()), "conv")
-    launch()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        launch()
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / reps / 1e3
+    t = _event_time(launch, reps)
     flops = 2.0 * B * H * W * D * 27 * C * 512
-    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "conv_gemm_kernel (fwd, rpn_conv_shared1 3x3x3 256->512 on P2)",
-            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
+    return {"achieved": round(flops / t / 1e12, 2), "unit": "TFLOP/s",
+            "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(t * 1e3, 4),
+            "traffic": _pmc_traffic(f"direct_conv_rpn_shared1_S{model.config.IMAGE_SHAPE[0]}")}
 
 
 # ---------------------------------------------------------------- ROIAlign roofline
@@ -106,7 +155,7 @@ def unique_voxels(boxes, fshapes, pool, S):
     return total
 
 
-def time_roi_align(fmaps, S, n_rois=128, reps=10):
+def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14)):
     from m3d import layers
     maps = [f.detach().contiguous() for f in fmaps[:4]]
     C = maps[0].shape[-1]
@@ -115,7 +164,7 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10):
     meta[0, 5:8] = S
     res = {}
     fshapes = [tuple(m.shape[1:4]) for m in maps]
-    for p in (7, 14):
+    for p in pools:
         layer = layers.PyramidROIAlign((p, p, p))
         layer([boxes, meta] + maps)
         torch.cuda.synchronize()
@@ -130,16 +179,18 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10):
         alg = 4.0 * n_rois * p ** 3 * C + 4.0 * C * u
         res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "algorithmic_bytes": alg,
                            "gather_bytes": 8 * 4.0 * n_rois * p ** 3 * C,
-                           "GBps": round(alg / t / 1e9, 1), "frac_hbm": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+                           "GBps": round(alg / t / 1e9, 1), "frac_hbm": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": _pmc_traffic(f"pyramid_fwd_pool{p}_S{S}")}
     return res
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(model, S, depth_slab=8, threads=None):
+def cpu_baseline(model, S, depth_slab=0, threads=None):
     """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
     fwd+bwd of the same network on a depth slab of the volume (S x S x depth_slab),
     scaled to whole volumes by the depth ratio (work is linear in depth)."""
     from oracle import model_ref as MR
+    depth_slab = depth_slab or S
     if threads:
         torch.set_num_threads(threads)
     params = model.store.state_dict()
@@ -156,7 +207,7 @@ def cpu_baseline(model, S, depth_slab=8, threads=None):
     vol_per_s = (depth_slab / S) / t
     return {"value": vol_per_s, "unit": "volumes/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/model_ref.py torch-CPU fp32 fwd+bwd on a {S}x{S}x{depth_slab} depth slab "
-                      f"({t:.1f} s), scaled x{S // depth_slab} to one {S}^3 volume"}
+                      f"({t:.1f} s)" + (f", scaled x{S // depth_slab} to one {S}^3 volume" if depth_slab != S else "")}
 
 
 # ---------------------------------------------------------------- main
@@ -168,7 +219,7 @@ def main():
     ap.add_argument("--size", type=int, default=128)
     ap.add_argument("--no-proposals", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / ROIAlign / CPU legs")
-    ap.add_argument("--cpu-slab", type=int, default=8)
+    ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
     args = ap.parse_args()
 
     from m3d.config import synthetic_rpn_config
@@ -227,7 +278,8 @@ def main():
         with torch.no_grad():
             fmaps = model.features(image)
         try:
-            out["roofline"] = time_dominant_conv(model, fmaps)
+            out["roofline"] = time_dominant_kernel(S)
+            out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
         except Exception as e:  # report, never hide
             out["roofline"] = {"error": repr(e)}
         try:

@@ -183,6 +183,14 @@ int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64
                                int64_t D, int64_t Cin, int64_t Cout, float* dw, void* workspace,
                                size_t ws_bytes, m3d_stream_t s);
 
+/* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
+ * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],
+ * C [M][N] row-major, batches contiguous; N multiple of 4.  The Winograd
+ * point-wise products above are exactly this call with batch = 64 (bench.py
+ * prices the RPN head's largest one). */
+int m3d_gemm_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
+                 int64_t N, const float* bias, int32_t relu, int32_t accumulate, m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
  * ------------------------------------------------------------------------- */

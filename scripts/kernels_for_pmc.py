@@ -1,17 +1,30 @@
-"""Runs the dominant conv kernel (rpn_conv_shared1 fwd on P2 @128^3) and the
-PyramidROIAlign 14^3 / 7^3 kernels a few times each, for rocprofv3 --pmc passes."""
-import os, sys
+"""Runs ONE priced launch of bench.py a few times for the rocprofv3 --pmc
+passes of scripts/gpu_prof.sh:  kernels_for_pmc.py LEG [S]
+  gemm    the dominant kernel's largest launch (batched Winograd GEMM of rpn_conv_shared1)
+  direct  rpn_conv_shared1 as a direct implicit-GEMM conv on P2
+  roi7 / roi14  PyramidROIAlign 7^3 / 14^3 at configs[2] shapes
+The priced kernel's dispatches are the LAST ones of its name in the trace."""
+import os
+import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "3d-mask-r-cnn_amd")]
-import torch
-import bench
-from m3d.config import synthetic_rpn_config
-from m3d.model import RPN, synthetic_volume
+import torch  # noqa: E402
 
-dev = torch.device("cuda")
-S = 128
-model = RPN(synthetic_rpn_config(S), device=dev, seed=1)
-with torch.no_grad():
-    fmaps = model.features(synthetic_volume(S).to(dev))
-print(bench.time_dominant_conv(model, fmaps, reps=3))
-print(bench.time_roi_align(fmaps, S, reps=3))
+import bench  # noqa: E402
+
+leg = sys.argv[1]
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+if leg == "gemm":
+    print(bench.time_dominant_kernel(S, reps=3))
+else:
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, synthetic_volume
+    model = RPN(synthetic_rpn_config(S), device=torch.device("cuda"), seed=1)
+    with torch.no_grad():
+        fmaps = model.features(synthetic_volume(S).to("cuda"))
+    torch.cuda.synchronize()
+    if leg == "direct":
+        print(bench.time_direct_conv(model, fmaps, reps=3))
+    else:
+        print(bench.time_roi_align(fmaps, S, reps=3, pools=(int(leg[3:]),)))

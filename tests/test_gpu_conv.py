@@ -175,3 +175,24 @@ def test_sgd_keras_matches_formula(cuda):
         gt = gt * clip / max(float(gt.norm()), clip)
         want = w0[sl] - lr * gt
         close(st.flat.detach()[sl], want, rtol=1e-6)
+
+
+@pytest.mark.parametrize("nb,M,K,N,relu", [(3, 200, 64, 96, 0), (2, 130, 40, 36, 1), (64, 96, 256, 512, 0)])
+def test_batched_gemm_f32(cuda, nb, M, K, N, relu):
+    """m3d_gemm_f32 (the Winograd point-wise GEMM launch bench.py prices)
+    against a float64 torch matmul, incl. ragged M/K/N tiles, bias, ReLU, accumulate."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn((nb, M, K), generator=g)
+    Bm = torch.randn((nb, K, N), generator=g)
+    bias = torch.randn((N,), generator=g)
+    C0 = torch.randn((nb, M, N), generator=g)
+    ref = torch.bmm(A.double(), Bm.double()) + bias.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    ref = ref + C0.double()
+    Ad, Bd, bd, Cd = (t.to(cuda).contiguous() for t in (A, Bm, bias, C0))
+    _lib.check(L.m3d_gemm_f32(Ad.data_ptr(), Bd.data_ptr(), Cd.data_ptr(), nb, M, K, N, bd.data_ptr(),
+                              relu, 1, _lib.stream()), "gemm")
+    close(Cd, ref)
