@@ -563,8 +563,11 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
 // direct implicit GEMM.  Transformed operands live in a caller workspace,
 // xi-major: U[64][T][C], V[64][K][N], M[64][T][N].
 // =========================================================================
+// Tile grid over the OUTPUT (depth D); the transformed input is read from a
+// tensor of depth Din at z = 2tz - pz + k ('same': Din = D, pz = 1; a depth
+// slab extended by z-halo planes: Din = D + halos, pz = 1 - lower halo).
 struct WinoGeom {
-    int B, H, W, D, TY, TX, TZ;
+    int B, H, W, D, Din, pz, TY, TX, TZ;
     int64_t T;
 };
 
@@ -600,11 +603,11 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
         for (int bb = 0; bb < 4; ++bb) {
             const int xx = 2 * tx - 1 + bb;
             const bool ok = y >= 0 && y < g.H && xx >= 0 && xx < g.W;
-            const float* row = x + ((((int64_t)b * g.H + y) * g.W + xx) * g.D) * C + c;
+            const float* row = x + ((((int64_t)b * g.H + y) * g.W + xx) * g.Din) * C + c;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int z = 2 * tz - 1 + k;
-                d[a][bb][k] = (ok && z >= 0 && z < g.D) ? row[(int64_t)z * C] : 0.0f;
+                const int z = 2 * tz - g.pz + k;
+                d[a][bb][k] = (ok && z >= 0 && z < g.Din) ? row[(int64_t)z * C] : 0.0f;
             }
         }
     }
@@ -850,9 +853,9 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
         }
 }
 
-static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D) {
+static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz) {
     WinoGeom g;
-    g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D;
+    g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
     g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + 1) / 2);
     g.T = B * g.TY * g.TX * g.TZ;
     return g;
@@ -1013,20 +1016,26 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
 }
 
 // ---- Winograd entry points -------------------------------------------------
-static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, int64_t Cout) {
-    if (B <= 0 || H <= 0 || W <= 0 || D <= 0 || Cin <= 0 || Cout <= 0)
+// x depth D, output depth OD, z pad-before pz: 'same' is OD == D, pz == 1; a
+// z-halo-extended depth slab has D = OD + halos and pz = 1 - (lower halo).
+static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, int32_t pz,
+                      int64_t Cin, int64_t Cout) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0 || OD <= 0 || Cin <= 0 || Cout <= 0)
         return einval("conv3d winograd: tensor dimensions must be positive");
     if (Cin % 32 || Cout % 32) return einval("conv3d winograd: Cin and Cout must be multiples of 32");
-    if (B * H * W * D > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
+    if (pz < 0 || pz > 1 || D - OD < 0 || D - OD > 2)
+        return einval("conv3d winograd: z geometry must be pz in {0,1} and 0 <= D - OD <= 2");
+    if (B * H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
     return M3D_OK;
 }
-
+// Workspace: V [64][Cin][Cout] + U [64][T][max C] + M [64][T][max C], T the
+// larger of the fwd (tiles over OD) and bwd-data (tiles over D) tile counts.
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
-                                                  int64_t Cin, int64_t Cout) {
-    const WinoGeom g = wino_geom(B, H, W, D);
+                                                  int64_t OD, int64_t Cin, int64_t Cout) {
+    const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1);
+    const size_t C = (size_t)(Cin > Cout ? Cin : Cout);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + al(sizeof(float) * 64 * (size_t)g.T * Cin) +
-           al(sizeof(float) * 64 * (size_t)g.T * Cout);
+    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + 2 * al(sizeof(float) * 64 * (size_t)g.T * C);
 }
 
 struct WinoWs { float *V, *U, *M; };
@@ -1041,15 +1050,16 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout) {
 }
 
 extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
-                                   int64_t Cin, const float* w, int64_t Cout, const float* bias,
-                                   const float* bn_scale, const float* bn_shift,
-                                   const float* residual, int32_t relu, float* z_out, float* y,
-                                   void* workspace, size_t ws_bytes, m3d_stream_t s) {
-    int rc = wino_check(B, H, W, D, Cin, Cout);
+                                   int64_t Cin, const float* w, int64_t Cout, int64_t OD,
+                                   int32_t pz, const float* bias, const float* bn_scale,
+                                   const float* bn_shift, const float* residual, int32_t relu,
+                                   float* z_out, float* y, void* workspace, size_t ws_bytes,
+                                   m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
-    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, D);
+    const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
     hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
                        (int)Cin, (int)Cout, 0, ws.V);
@@ -1068,15 +1078,18 @@ extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t
     return check_launch("conv3d winograd fwd");
 }
 
+// dx [B,H,W,D,Cin] = conv_transpose(dz [B,H,W,OD,Cout]): a 'same'-type 3x3x3
+// correlation of dz with the flipped, transposed kernel, tiles over dx's grid,
+// dz read at z = 2tz - (2 - pz) + k.
 extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H,
-                                        int64_t W, int64_t D, int64_t Cin, int64_t Cout, float* dx,
-                                        int32_t accumulate, void* workspace, size_t ws_bytes,
-                                        m3d_stream_t s) {
-    int rc = wino_check(B, H, W, D, Cin, Cout);
+                                        int64_t W, int64_t D, int64_t Cin, int64_t Cout,
+                                        int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                                        void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
-    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, D);
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz);
     // same layout with the roles of Cin/Cout swapped (V'[64][Cout][Cin], U'[64][T][Cout])
     WinoWs ws = wino_ws(workspace, g, Cout, Cin);
     hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
@@ -1097,13 +1110,13 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
 
 extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H,
                                           int64_t W, int64_t D, int64_t Cin, int64_t Cout,
-                                          float* dw, void* workspace, size_t ws_bytes,
-                                          m3d_stream_t s) {
-    int rc = wino_check(B, H, W, D, Cin, Cout);
+                                          int64_t OD, int32_t pz, float* dw, void* workspace,
+                                          size_t ws_bytes, m3d_stream_t s) {
+    int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
-    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, Cin, Cout))
+    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, D);
+    const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);   // V <- dW_hat, U <- B^T x, M <- A dz
     if (hipMemsetAsync(ws.V, 0, sizeof(float) * 64 * (size_t)Cin * Cout, st(s)) != hipSuccess)
         return check_launch("memset dW_hat");

@@ -246,14 +246,17 @@ __global__ __launch_bounds__(1024) void nms_reduce_kernel(const uint64_t* __rest
 }
 
 // ---- ProposalLayer ----------------------------------------------------------
+// gidx (optional): the anchor's index in the whole volume's anchor list when
+// this rank holds a depth slab of it (the key then sorts in global order).
 __global__ void score_keys_kernel(const float* __restrict__ probs, int64_t A,
-                                  int64_t* __restrict__ keys) {
+                                  const int64_t* __restrict__ gidx, int64_t* __restrict__ keys) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A) return;
     float s = probs[i * 2 + 1];
     if (s == 0.0f) s = 0.0f;
     const uint32_t o = float_ord(s) ^ 0x80000000u;   // signed-orderable
-    const uint64_t k = ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    const uint32_t idx = (uint32_t)(gidx ? gidx[i] : i);
+    const uint64_t k = ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - idx);
     keys[i] = (int64_t)k;
 }
 
@@ -393,9 +396,15 @@ extern "C" int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int
 }
 
 extern "C" int m3d_score_keys(const float* probs, int64_t A, int64_t* keys, m3d_stream_t s) {
+    return m3d_score_keys_mapped(probs, A, nullptr, keys, s);
+}
+
+extern "C" int m3d_score_keys_mapped(const float* probs, int64_t A, const int64_t* gidx,
+                                     int64_t* keys, m3d_stream_t s) {
     if (A <= 0) return M3D_OK;
+    if (A > 0xFFFFFFFFll) return einval("score_keys: more than 2^32 anchors");
     hipLaunchKernelGGL(score_keys_kernel, dim3(grid_for(A, 256)), dim3(256), 0, st(s), probs, A,
-                       keys);
+                       gidx, keys);
     return check_launch("score_keys_kernel");
 }
 

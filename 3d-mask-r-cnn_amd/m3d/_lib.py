@@ -42,6 +42,7 @@ _SIGS = {
     "m3d_nms3d_workspace_bytes": [c_i64],
     "m3d_nms3d": [c_p, c_p, c_i64, c_i32, c_f, c_i32, c_p, c_p, c_p, c_sz, c_p],
     "m3d_score_keys": [c_p, c_i64, c_p, c_p],
+    "m3d_score_keys_mapped": [c_p, c_i64, c_p, c_p, c_p],
     "m3d_proposal_decode": [c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p],
     "m3d_proposal_gather": [c_p, c_p, c_p, c_i32, c_p, c_p],
     "m3d_conv3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_i32, c_i64,
@@ -54,13 +55,13 @@ _SIGS = {
                               c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                               c_p, c_p],
     "m3d_gemm_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_p],
-    "m3d_conv3d_wino_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64],
-    "m3d_conv3d_fwd_wino": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p,
-                            c_i32, c_p, c_p, c_p, c_sz, c_p],
-    "m3d_conv3d_bwd_data_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32,
-                                 c_p, c_sz, c_p],
-    "m3d_conv3d_bwd_weight_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
-                                   c_sz, c_p],
+    "m3d_conv3d_wino_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64],
+    "m3d_conv3d_fwd_wino": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
+                            c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32,
+                                 c_p, c_i32, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_weight_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                   c_i32, c_p, c_p, c_sz, c_p],
     "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,

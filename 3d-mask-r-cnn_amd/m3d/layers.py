@@ -48,6 +48,44 @@ class ProposalLayer:
             return out, torch.cat(counts)
         return out
 
+    def call_slab(self, inputs, sg, local_index):
+        """The same proposals when this rank holds one depth slab of the volume
+        (m3d.slab): probs/deltas [1,A_local,*] are the slab's RPN rows,
+        local_index [A_local] their global anchor indices, anchors [1,A,6] the
+        whole volume's.  Each slab's top-k candidates (global-order keys) are
+        all-gathered, merged into the global top-k, and every rank runs the same
+        decode + 3-D NMS -> rpn_rois [1,proposal_count,6] identical on all ranks
+        and to the unsharded layer."""
+        probs, deltas, anchors = inputs
+        if probs.shape[0] != 1:
+            raise ValueError("depth-slab proposals need IMAGES_PER_GPU = 1")
+        A = anchors.shape[1]
+        k = min(self.pre_nms_limit, A)
+        with torch.no_grad():
+            pb = probs[0].detach().float().contiguous()
+            db = deltas[0].detach().float().contiguous()
+            keys = ops.score_keys(pb, local_index)
+            kl = min(k, keys.shape[0])
+            vals, pos = torch.topk(keys, kl, sorted=False)
+            ck = torch.full((k,), torch.iinfo(torch.int64).min, device=pb.device, dtype=torch.int64)
+            cp = torch.zeros((k, 2), device=pb.device)
+            cd = torch.zeros((k, 6), device=pb.device)
+            ck[:kl], cp[:kl], cd[:kl] = vals, pb[pos], db[pos]
+            gk = sg.all_gather(ck).reshape(-1)
+            gp = sg.all_gather(cp).reshape(-1, 2)
+            gd = sg.all_gather(cd).reshape(-1, 6)
+            top, where = torch.topk(gk, k, sorted=True)
+            gidx = 0xFFFFFFFF - (top & 0xFFFFFFFF)
+            sel_p = gp.index_select(0, where).contiguous()
+            sel_d = gd.index_select(0, where).contiguous()
+            sel_a = anchors[0].detach().float().index_select(0, gidx).contiguous()
+            order = torch.arange(k, device=pb.device, dtype=torch.int64)
+            boxes, scores = ops.proposal_decode(sel_p, sel_d, sel_a, order, self.rpn_bbox_std_dev,
+                                                self.image_depth)
+            keep, num = ops.non_max_suppression_3d_padded(boxes, scores, self.proposal_count,
+                                                          self.nms_threshold)
+            return ops.proposal_gather(boxes, keep, num, self.proposal_count)[None]
+
     def compute_output_shape(self, input_shape):
         return (None, self.proposal_count, 6)
 

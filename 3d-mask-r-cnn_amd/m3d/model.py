@@ -44,6 +44,34 @@ class RPNTargets:
         self.pos_idx = torch.from_numpy(pos_idx.astype(np.int64)).to(device)
         self.gt_bbox = torch.from_numpy(gt.reshape(-1, 6).astype(np.float32)).to(device)
         self.n_cls, self.n_pos = len(cls_idx), len(pos_idx)
+        # K.mean denominators (global counts; a depth slab holds only part of the anchors)
+        self.cls_denom, self.pos_denom = self.n_cls, self.n_pos
+
+    @classmethod
+    def for_slab(cls, rpn_match, rpn_bbox, local_index, device):
+        """The targets of one depth slab (m3d.slab): rpn_match [1,A,1] and
+        rpn_bbox [1,n,6] of the WHOLE volume, local_index [A_local] the global
+        anchor index of each local RPN row.  Loss terms are restricted to the
+        slab's anchors and divided by the whole volume's counts, so the sum of
+        the ranks' losses is the single-volume loss."""
+        m = np.asarray(rpn_match).reshape(-1)
+        if np.asarray(rpn_match).shape[0] != 1:
+            raise ValueError("depth-slab sharding runs one volume (IMAGES_PER_GPU = 1)")
+        gidx = np.asarray(local_index, np.int64)
+        lm = m[gidx]
+        t = cls.__new__(cls)
+        cls_idx = np.nonzero(lm != 0)[0]
+        pos_idx = np.nonzero(lm == 1)[0]
+        gpos = np.nonzero(m == 1)[0]                               # global positive order
+        rows = np.searchsorted(gpos, gidx[pos_idx])
+        rb = np.asarray(rpn_bbox, np.float32).reshape(-1, 6)
+        t.cls_idx = torch.from_numpy(cls_idx.astype(np.int64)).to(device)
+        t.cls_labels = torch.from_numpy((lm[cls_idx] == 1).astype(np.int64)).to(device)
+        t.pos_idx = torch.from_numpy(pos_idx.astype(np.int64)).to(device)
+        t.gt_bbox = torch.from_numpy(rb[rows].reshape(-1, 6)).to(device)
+        t.n_cls, t.n_pos = len(cls_idx), len(pos_idx)
+        t.cls_denom, t.pos_denom = int((m != 0).sum()), len(gpos)
+        return t
 
 
 def rpn_class_loss(t: RPNTargets, rpn_class_logits, alpha=0.90, gamma=1.5):
@@ -56,7 +84,7 @@ def rpn_class_loss(t: RPNTargets, rpn_class_logits, alpha=0.90, gamma=1.5):
     p_t = probs.gather(1, t.cls_labels[:, None])[:, 0]
     ce = torch.pow(1.0 - p_t, gamma) * ce
     alpha_t = torch.where(t.cls_labels == 1, torch.full_like(ce, alpha), torch.full_like(ce, 1.0 - alpha))
-    return (alpha_t * ce).mean()
+    return (alpha_t * ce).sum() / t.cls_denom
 
 
 def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
@@ -70,7 +98,7 @@ def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     zm = torch.tensor([0., 0., 1., 0., 0., 1.], device=diff.device)
     h_xy = torch.where(ad < 1.0, 0.5 * diff * diff, ad - 0.5) * xy
     h_z = torch.where(ad < 0.5, 0.5 * diff * diff, 0.5 * ad - 0.25) * zm
-    return (h_xy + h_z).mean()
+    return (h_xy + h_z).sum() / (6 * t.pos_denom)
 
 
 # ---------------------------------------------------------------------------

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib
+from . import _lib, slab
 from ._lib import check, ptr, stream
 
 
@@ -25,15 +25,19 @@ WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
 WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "128"))
 
 
-def use_winograd(geo, cin, cout):
+def use_winograd(geo, cin, cout, in_sp):
+    """'same' 3x3x3 stride-1 convs, or their z-halo-extended depth-slab form
+    (z pad 0/1, input depth = output depth + halo planes)."""
     # below 128 channels the (bandwidth-bound) transforms cost more than the
     # 3.375x MFMA saving (measured: res2*_branch2b 64->64 is no faster)
-    return (WINOGRAD and geo.k == (3, 3, 3) and geo.stride == (1, 1, 1) and geo.pad == (1, 1, 1)
+    return (WINOGRAD and geo.k == (3, 3, 3) and geo.stride == (1, 1, 1) and geo.pad[:2] == (1, 1)
+            and tuple(geo.out[:2]) == tuple(in_sp[:2]) and geo.pad[2] in (0, 1)
+            and 0 <= in_sp[2] - geo.out[2] <= 2
             and cin % 32 == 0 and cout % 32 == 0 and min(cin, cout) >= WINO_MIN_C)
 
 
-def _wino_ws(B, H, W, D, cin, cout, dev):
-    n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, cin, cout))
+def _wino_ws(B, H, W, D, OD, cin, cout, dev):
+    n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, cin, cout))
     return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
 
 
@@ -106,10 +110,11 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.bn = (mean, rstd, scale)
         else:
             ctx.bn = None
-        ctx.wino = use_winograd(geo, Cin, Cout) and res_mode != 2
+        ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
         if ctx.wino:
-            ws, wsb = _wino_ws(B, H, W, D, Cin, Cout, x.device)
-            check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, ptr(b), ptr(scale),
+            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
+            check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
+                                           ptr(b), ptr(scale),
                                            ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
                                            ptr(ws), wsb, stream()), "conv3d_fwd_wino")
         else:
@@ -150,16 +155,18 @@ class _ConvBNAct(torch.autograd.Function):
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
         if ctx.wino:
-            ws, wsb = _wino_ws(B, H, W, D, Cin, Cout, x.device)
+            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
             if grads.get("kernel") is not None:
-                check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout,
-                                                   ptr(grads["kernel"]), ptr(ws), wsb, stream()),
+                check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout, OD,
+                                                   geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
+                                                   stream()),
                       "conv3d_bwd_weight_wino")
             dx = None
             if ctx.need_dx:
                 dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
-                check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, ptr(dx), 0,
-                                                 ptr(ws), wsb, stream()), "conv3d_bwd_data_wino")
+                check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                 geo.pad[2], ptr(dx), 0, ptr(ws), wsb, stream()),
+                      "conv3d_bwd_data_wino")
             return dx, (dres if need_res else None), None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
@@ -191,6 +198,18 @@ class _ConvBNAct(torch.autograd.Function):
         return dx, dr, None, None, None, None, None, None, None, None
 
 
+def _slab_extend(x, geo):
+    """Under depth-slab sharding (m3d.slab.active), give a z-spanning window
+    its neighbours' halo planes; z padding stays only where the volume ends."""
+    if slab.current() is None or geo.k[2] == 1:
+        return x, geo
+    r = geo.pad[2]
+    if geo.stride[2] != 1 or geo.out[2] != x.shape[3] or 2 * r != geo.k[2] - 1:
+        raise ValueError("depth-slab sharding needs z-stride 1 and symmetric 'same' z padding")
+    xe, nlo = slab.halo_z(x, r)
+    return xe, ConvGeom(geo.k, geo.stride, (geo.pad[0], geo.pad[1], r - nlo), geo.out)
+
+
 def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True):
     """Functional entry: ``layer`` is a Conv3D parameter group from params.py."""
     w = layer.kernel.data
@@ -201,6 +220,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)
     if residual is not None:
         residual = residual.contiguous()
+    x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
                             need_dx and x.requires_grad)
@@ -236,7 +256,8 @@ def max_pool3d(x, k, stride, padding="same"):
         out, pad = tuple(o for o, _ in op), tuple(p for _, p in op)
     else:
         out, pad = tuple(valid_out(n, kk, s) for n, kk, s in zip(sp, k, stride)), (0, 0, 0)
-    return _MaxPool.apply(x.contiguous(), tuple(k), tuple(stride), pad, out)
+    x, geo = _slab_extend(x.contiguous(), ConvGeom(tuple(k), tuple(stride), pad, out))
+    return _MaxPool.apply(x.contiguous(), tuple(k), tuple(stride), geo.pad, out)
 
 
 class _Subsample221(torch.autograd.Function):

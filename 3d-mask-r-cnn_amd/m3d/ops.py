@@ -272,6 +272,16 @@ def topk_order(probs, k):
     return (0xFFFFFFFF - (vals & 0xFFFFFFFF)).to(torch.int64)
 
 
+def score_keys(probs, global_index=None):
+    """int64 top-k keys of probs[:,1] (score desc, lower GLOBAL index first);
+    global_index [A] int64 maps rows to whole-volume anchor indices (depth slabs)."""
+    A = probs.shape[0]
+    keys = torch.empty(A, device=probs.device, dtype=torch.int64)
+    gi = None if global_index is None else _c(global_index, torch.int64)
+    check(_L().m3d_score_keys_mapped(ptr(probs), A, ptr(gi), ptr(keys), stream()), "score_keys")
+    return keys
+
+
 def proposal_decode(probs, deltas, anchors, order, std_dev, image_depth):
     k = order.shape[0]
     boxes = torch.empty((k, 6), device=probs.device, dtype=torch.float32)

@@ -53,3 +53,68 @@ def data_parallel_train_step(model, image, targets, world, proposals=True):
     model.sgd_step()
     return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
             "rpn_rois": out["rpn_rois"]}
+
+
+# ---------------------------------------------------------------------------
+# depth-slab sharding of one volume (BASELINE configs[4])
+# ---------------------------------------------------------------------------
+def level_hw(model):
+    """(H_l, W_l) of P2..P6 for the model's IMAGE_SHAPE (strides (4,8,16,32,64) in y/x)."""
+    from .anchors import compute_backbone_shapes
+    shapes = compute_backbone_shapes(model.config, model.config.IMAGE_SHAPE)
+    return [(int(h), int(w)) for h, w, _ in shapes]
+
+
+class SlabRPN:
+    """One RPN training step on a volume split into depth slabs, one per rank.
+
+    Every rank holds the full (replicated) parameters, the slab [z0,z1) of the
+    input volume and of every activation; halo planes move point-to-point
+    (m3d.slab), the loss is the global one (partial sums / global counts), the
+    weight gradients are SUM-all-reduced (they are partial sums of one
+    gradient), SGD runs replicated, proposals are merged globally."""
+
+    def __init__(self, model, sg, rpn_match, rpn_bbox):
+        from .model import RPNTargets
+        from .slab import SlabGroup  # noqa: F401
+        self.model, self.sg = model, sg
+        apl = model.rpn.apl
+        gi = sg.local_anchor_index(level_hw(model), apl)
+        self.local_index = torch.from_numpy(gi).to(model.device)
+        self.targets = RPNTargets.for_slab(rpn_match, rpn_bbox, gi, model.device)
+
+    def slice(self, volume):
+        """The rank's slab of a whole [B,H,W,D,C] volume."""
+        return volume[:, :, :, self.sg.z0:self.sg.z1].contiguous()
+
+    def forward(self, image_slab, proposals=True):
+        from . import slab
+        m = self.model
+        with slab.active(self.sg):
+            fmaps = m.features(image_slab)
+            logits, probs, bbox = m.rpn(fmaps)
+        rois = None
+        if proposals:
+            rois = m.proposal_layer.call_slab([probs, bbox, m.anchors], self.sg, self.local_index)
+        return {"rpn_class_logits": logits, "rpn_class": probs, "rpn_bbox": bbox, "rpn_rois": rois,
+                "feature_maps": fmaps}
+
+    def train_step(self, image_slab, proposals=True):
+        from . import slab
+        m = self.model
+        m.store.zero_grad()
+        out = self.forward(image_slab, proposals=False)
+        lc, lb = m.losses(out, self.targets)
+        total = lc * m.LOSS_WEIGHTS["rpn_class_loss"] + lb * m.LOSS_WEIGHTS["rpn_bbox_loss"]
+        with slab.active(self.sg):          # halo gradients flow during backward
+            total.backward()
+        m.rpn.finish_backward()
+        self.sg.all_reduce_sum_(m.store.grad_flat)
+        m.sgd_step()
+        if proposals:
+            out["rpn_rois"] = m.proposal_layer.call_slab([out["rpn_class"], out["rpn_bbox"], m.anchors],
+                                                         self.sg, self.local_index)
+        parts = torch.stack([total.detach(), lc.detach(), lb.detach()])
+        self.sg.all_reduce_sum_(parts)
+        return {"loss": parts[0], "rpn_class_loss": parts[1], "rpn_bbox_loss": parts[2],
+                "rpn_rois": out["rpn_rois"]}

@@ -121,6 +121,11 @@ int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int32_t max_ou
  *   zero rows after (core/models.py:476-485).
  * ------------------------------------------------------------------------- */
 int m3d_score_keys(const float* probs /*[A,2]*/, int64_t A, int64_t* keys, m3d_stream_t s);
+/* Same keys for a depth slab of the volume: gidx[i] is local anchor i's index
+ * in the whole volume's (y,x,z,a)-ordered anchor list (NULL = identity), so
+ * the merged top-k over all slabs has the single-volume order. */
+int m3d_score_keys_mapped(const float* probs, int64_t A, const int64_t* gidx, int64_t* keys,
+                          m3d_stream_t s);
 int m3d_proposal_decode(const float* probs, const float* deltas, const float* anchors,
                         const int64_t* order, int64_t k, const float std_dev[6],
                         float image_depth, float* boxes /*[k,6]*/, float* scores /*[k]*/,
@@ -165,23 +170,30 @@ int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,
                           int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dw,
                           m3d_stream_t s);
 
-/* Winograd F(2x2x2,3x3x3) versions of the three passes for stride-1 'same'
- * 3x3x3 convs (every 3x3x3 conv of the graph: res*_branch2b, fpn_p*,
- * rpn_conv_shared1): 3.375x fewer multiplies, the 64 point-wise products run
- * as batched fp32-MFMA GEMMs.  Cin, Cout multiples of 32.  Same epilogue as
- * m3d_conv3d_fwd (res_mode 1 only).  workspace: m3d_conv3d_wino_workspace_bytes. */
-size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
-                                       int64_t Cout);
+/* Winograd F(2x2x2,3x3x3) versions of the three passes for stride-1 3x3x3
+ * convs with 'same' padding in y/x (every 3x3x3 conv of the graph:
+ * res*_branch2b, fpn_p*, rpn_conv_shared1): 3.375x fewer multiplies, the 64
+ * point-wise products run as batched fp32-MFMA GEMMs.  Cin, Cout multiples of
+ * 32.  Same epilogue as m3d_conv3d_fwd (res_mode 1 only).
+ * z geometry: x has depth D, y depth OD, z pad-before pz.  'same' is OD == D,
+ * pz == 1; a depth slab extended by z-halo planes from its neighbours (multi-
+ * GPU depth-slab sharding) has D = OD + #halo planes and pz = 1 - (lower halo
+ * present).  Requires pz in {0,1}, 0 <= D - OD <= 2.
+ * workspace: m3d_conv3d_wino_workspace_bytes(B,H,W,D,OD,Cin,Cout). */
+size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD,
+                                       int64_t Cin, int64_t Cout);
 int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
-                        const float* w, int64_t Cout, const float* bias, const float* bn_scale,
-                        const float* bn_shift, const float* residual, int32_t relu, float* z_out,
-                        float* y, void* workspace, size_t ws_bytes, m3d_stream_t s);
+                        const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                        const float* bn_scale, const float* bn_shift, const float* residual,
+                        int32_t relu, float* z_out, float* y, void* workspace, size_t ws_bytes,
+                        m3d_stream_t s);
 int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
-                             int64_t D, int64_t Cin, int64_t Cout, float* dx, int32_t accumulate,
-                             void* workspace, size_t ws_bytes, m3d_stream_t s);
+                             int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
+                             float* dx, int32_t accumulate, void* workspace, size_t ws_bytes,
+                             m3d_stream_t s);
 int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
-                               int64_t D, int64_t Cin, int64_t Cout, float* dw, void* workspace,
-                               size_t ws_bytes, m3d_stream_t s);
+                               int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
+                               float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
 
 /* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
  * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],
