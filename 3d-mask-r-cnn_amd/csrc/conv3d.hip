@@ -1028,14 +1028,15 @@ static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, in
     if (B * H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
     return M3D_OK;
 }
-// Workspace: V [64][Cin][Cout] + U [64][T][max C] + M [64][T][max C], T the
-// larger of the fwd (tiles over OD) and bwd-data (tiles over D) tile counts.
+// Workspace: V [64][Cin][Cout] + U [64][T][C1] + M [64][T][C2] with
+// {C1, C2} = {Cin, Cout} (fwd / wgrad) or {Cout, Cin} (bwd-data), T the larger
+// of the fwd (tiles over OD) and bwd-data (tiles over D) tile counts.
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {
     const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1);
-    const size_t C = (size_t)(Cin > Cout ? Cin : Cout);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + 2 * al(sizeof(float) * 64 * (size_t)g.T * C);
+    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + al(sizeof(float) * 64 * (size_t)g.T * Cin) +
+           al(sizeof(float) * 64 * (size_t)g.T * Cout);
 }
 
 struct WinoWs { float *V, *U, *M; };

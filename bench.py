@@ -184,6 +184,49 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14)):
     return res
 
 
+# ---------------------------------------------------------------- depth-slab leg
+def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
+    """BASELINE configs[4]: ONE S^3 volume per step, split into depth slabs over
+    all ranks (halo exchange + SUM gradient all-reduce over RCCL, merged
+    proposals); strong scaling -- the total work is fixed as N grows."""
+    from m3d import slab
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, synthetic_rpn_targets, synthetic_volume
+    from m3d.parallel import SlabRPN
+    cfg = synthetic_rpn_config(S)
+    model = RPN(cfg, device=dev, seed=1)
+    sg = slab.SlabGroup(S, rank, world)
+    match, bbox = synthetic_rpn_targets(model.anchors.shape[1], cfg.RPN_TRAIN_ANCHORS_PER_IMAGE, seed=2)
+    srpn = SlabRPN(model, sg, match, bbox)
+    image = srpn.slice(synthetic_volume(S, seed=100)).to(dev)
+    for _ in range(warmup):
+        r = srpn.train_step(image, proposals=proposals)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = srpn.train_step(image, proposals=proposals)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    out = {"workload": f"configs[4]: RPN training step on ONE {S}^3 volume depth-slab sharded over "
+                       f"{world} GPU(s) ({sg.Dl} planes/rank), halo exchange + grad all-reduce over RCCL",
+           "size": S, "n_gpus": world, "steps": steps, "ms_per_step": round(el / steps * 1e3, 2),
+           "volumes_per_s": round(steps / el, 4), "scaling": "strong",
+           "loss": round(float(r["loss"]), 6),
+           "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    del model, srpn, image
+    torch.cuda.empty_cache()
+    return out
+
+
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(model, S, depth_slab=0, threads=None):
     """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
@@ -218,6 +261,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=128)
     ap.add_argument("--no-proposals", action="store_true")
+    ap.add_argument("--slab-size", type=int, default=256,
+                    help="depth-slab leg volume size (configs[4]); 0 disables the leg")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / ROIAlign / CPU legs")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
     args = ap.parse_args()
@@ -274,6 +319,14 @@ def main():
                                   f"{S}^3 x1 volume per GPU",
                       "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
                       "anchors": int(model.anchors.shape[1])}}
+    if args.slab_size and not args.no_extras:
+        del r
+        torch.cuda.empty_cache()
+        try:
+            out["depth_slab"] = depth_slab_leg(args.slab_size, args.steps, args.warmup, rank, world, dev,
+                                               proposals=props)
+        except Exception as e:  # report, never hide
+            out["depth_slab"] = {"error": repr(e)}
     if rank == 0 and not args.no_extras:
         with torch.no_grad():
             fmaps = model.features(image)

@@ -196,3 +196,38 @@ def test_batched_gemm_f32(cuda, nb, M, K, N, relu):
     _lib.check(L.m3d_gemm_f32(Ad.data_ptr(), Bd.data_ptr(), Cd.data_ptr(), nb, M, K, N, bd.data_ptr(),
                               relu, 1, _lib.stream()), "gemm")
     close(Cd, ref)
+
+
+@pytest.mark.parametrize("D,OD,pz", [(6, 6, 1), (7, 6, 1), (7, 6, 0), (8, 6, 0), (5, 5, 1)])
+def test_winograd_z_halo_geometry(cuda, D, OD, pz):
+    """Winograd fwd / bwd-data / bwd-weight on a z-halo-extended depth slab
+    (input depth D, output depth OD, z pad-before pz) vs float64 torch conv3d."""
+    import torch.nn.functional as F
+    from m3d import _lib
+    L = _lib.load()
+    H, W, Ci, Co = 6, 5, 128, 160
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((1, H, W, D, Ci), generator=g)
+    w = torch.randn((3, 3, 3, Ci, Co), generator=g) * 0.05
+    dy = torch.randn((1, H, W, OD, Co), generator=g)
+    pz_hi = OD + 2 - pz - D
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    xc = F.pad(xr.permute(0, 4, 1, 2, 3), (pz, pz_hi, 1, 1, 1, 1))
+    yr = F.conv3d(xc, wr.permute(4, 3, 0, 1, 2)).permute(0, 2, 3, 4, 1)
+    (yr * dy.double()).sum().backward()
+    xd, wd, dyd = x.to(cuda), w.to(cuda), dy.to(cuda)
+    nb = int(L.m3d_conv3d_wino_workspace_bytes(1, H, W, D, OD, Ci, Co))
+    ws = torch.empty(nb // 4 + 1, device=cuda)
+    y = torch.empty((1, H, W, OD, Co), device=cuda)
+    _lib.check(L.m3d_conv3d_fwd_wino(xd.data_ptr(), 1, H, W, D, Ci, wd.data_ptr(), Co, OD, pz, None, None,
+                                     None, None, 0, None, y.data_ptr(), ws.data_ptr(), nb, _lib.stream()))
+    dx = torch.empty((1, H, W, D, Ci), device=cuda)
+    _lib.check(L.m3d_conv3d_bwd_data_wino(dyd.data_ptr(), wd.data_ptr(), 1, H, W, D, Ci, Co, OD, pz,
+                                          dx.data_ptr(), 0, ws.data_ptr(), nb, _lib.stream()))
+    dw = torch.zeros((3, 3, 3, Ci, Co), device=cuda)
+    _lib.check(L.m3d_conv3d_bwd_weight_wino(xd.data_ptr(), dyd.data_ptr(), 1, H, W, D, Ci, Co, OD, pz,
+                                            dw.data_ptr(), ws.data_ptr(), nb, _lib.stream()))
+    close(y, yr)
+    close(dx, xr.grad)
+    close(dw, wr.grad)
