@@ -147,6 +147,134 @@ __device__ __forceinline__ void scatter_sample(float* __restrict__ img, int W, i
     }
 }
 
+struct Pyr {
+    const float* fmaps[4];
+    float* gmaps[4];
+    int H[4], W[4], D[4];
+};
+
+// ---- trilinear z-line kernel (C % 4 == 0) ---------------------------------
+// One wave per output line (n, y, x): the wave walks the cd samples of the
+// line in z.  The 4 (y, x) corner columns of a line are contiguous in memory
+// along z ([H][W][D][C] layout), and a sample whose floor plane equals the
+// previous sample's ceil plane reuses those 4 rows from registers.  The 4
+// waves of a workgroup are 4 consecutive x of one y, so their corner columns
+// overlap in L1/L2, and the block index is remapped XCD-contiguously so the
+// lines of one ROI stay in one XCD's L2.  Per-sample arithmetic is exactly
+// make_sample + tri (bit-identical to the per-sample kernels).
+__device__ __forceinline__ int64_t xcd_block() {
+    const int64_t nb = gridDim.x, L = blockIdx.x, xcd = L % 8, q8 = nb / 8, r8 = nb % 8;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+}
+
+struct LineArgs {
+    const float* image;          // crop: [B,H,W,D,C]
+    const int32_t* box_ind;
+    const float* boxes;          // crop: [N,6]; pyramid: boxes_adj [B*N,6]
+    const int32_t* levels;       // pyramid
+    int64_t N;                   // pyramid: boxes per image
+    int64_t lines;               // (#boxes) * ch * cw
+    int H, W, D, C, ch, cw, cd;
+    float extrap;
+    float* out;
+};
+
+__device__ __forceinline__ float4 tri4(const float4& a, const float4& b, const float4& c,
+                                       const float4& d, const float4& e, const float4& g,
+                                       const float4& h, const float4& i, float yl, float xl,
+                                       float zl) {
+    float4 r;
+    r.x = tri(a.x, b.x, c.x, d.x, e.x, g.x, h.x, i.x, yl, xl, zl);
+    r.y = tri(a.y, b.y, c.y, d.y, e.y, g.y, h.y, i.y, yl, xl, zl);
+    r.z = tri(a.z, b.z, c.z, d.z, e.z, g.z, h.z, i.z, yl, xl, zl);
+    r.w = tri(a.w, b.w, c.w, d.w, e.w, g.w, h.w, i.w, yl, xl, zl);
+    return r;
+}
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+// Output rows are written once and never re-read here: non-temporal stores
+// keep them from evicting the feature-map corner rows from L2.
+__device__ __forceinline__ void st_nt(float4* p, const float4& v) {
+    f4v t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(p));
+}
+
+template <bool PYR>
+__global__ __launch_bounds__(256) void line_fwd_kernel(LineArgs a, Pyr P) {
+    const int64_t line = xcd_block() * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (line >= a.lines) return;
+    int64_t t = line;
+    const int x = (int)(t % a.cw); t /= a.cw;
+    const int y = (int)(t % a.ch);
+    const int64_t n = t / a.ch;
+    int H, W, D;
+    const float* img;
+    if (PYR) {
+        const int l = a.levels[n] - 2;
+        H = P.H[l]; W = P.W[l]; D = P.D[l];
+        img = P.fmaps[l] + (size_t)(n / a.N) * H * W * D * a.C;
+    } else {
+        H = a.H; W = a.W; D = a.D;
+        img = a.image + (size_t)a.box_ind[n] * H * W * D * a.C;
+    }
+    const float* box = a.boxes + n * 6;
+    const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
+    const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
+    const float in_x = axis_coord(x1, x2, W, a.cw, x, axis_scale(x1, x2, W, a.cw));
+    const float zsc = axis_scale(z1, z2, D, a.cd);
+    const int C4 = a.C >> 2;
+    float4* o = reinterpret_cast<float4*>(a.out + line * (int64_t)a.cd * a.C);
+    const bool yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
+    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
+    if (yx_oob) {
+        for (int z = 0; z < a.cd; ++z)
+            for (int c = lane; c < C4; c += 64) st_nt(o + (int64_t)z * C4 + c, ex);
+        return;
+    }
+    const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
+    const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+    const float yl = in_y - (float)ty, xl = in_x - (float)lx;
+    const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
+    const float4* base = reinterpret_cast<const float4*>(img);
+    const float4* col[4] = {base + ty * rowW + lx * rowD, base + ty * rowW + rx * rowD,
+                            base + by * rowW + lx * rowD, base + by * rowW + rx * rowD};
+    for (int c = lane; c < C4; c += 64) {
+        int pk = -1;
+        float4 kv[4];
+        for (int z = 0; z < a.cd; ++z) {
+            const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
+            float4 r;
+            if (in_z < 0 || in_z > (float)(D - 1)) {
+                r = ex;
+            } else {
+                const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+                const float zl = in_z - (float)fz;
+                float4 fv[4];
+                if (fz == pk) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fv[q] = kv[q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
+                }
+                if (kz != fz) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) kv[q] = fv[q];
+                }
+                pk = kz;
+                // tri(tlf, tlk, trf, trk, blf, blk, brf, brk): tl = (ty,lx), tr = (ty,rx), ...
+                r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
+                if (PYR) { r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w); }
+            }
+            st_nt(o + (int64_t)z * C4 + c, r);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ kernels
 __global__ __launch_bounds__(256) void crop_fwd_kernel(const float* __restrict__ image, int B,
                                                        int H, int W, int D, int C,
@@ -296,11 +424,6 @@ __global__ __launch_bounds__(256) void crop_bwd_boxes_kernel(
 }
 
 // ---- PyramidROIAlign ----------------------------------------------------------
-struct Pyr {
-    const float* fmaps[4];
-    float* gmaps[4];
-    int H[4], W[4], D[4];
-};
 
 // Box preparation + level assignment (core/models.py:611-649), one thread per (b,n).
 __global__ void pyramid_prep_kernel(const float* __restrict__ boxes,
@@ -436,6 +559,13 @@ extern "C" int m3d_crop_and_resize3d_fwd(const float* image, int64_t B, int64_t 
     if (rc) return rc;
     const int64_t total = N * ch * cw * cd;
     if (total == 0) return M3D_OK;
+    if (method == 0 && (C & 3) == 0) {
+        LineArgs a{image, box_ind, boxes, nullptr, 0, N * ch * cw, (int)H, (int)W, (int)D, (int)C,
+                   ch, cw, cd, extrapolation, crops};
+        hipLaunchKernelGGL(line_fwd_kernel<false>, dim3(grid_for(a.lines, 4)), dim3(256), 0, st(s), a,
+                           Pyr{});
+        return check_launch("line_fwd_kernel");
+    }
     hipLaunchKernelGGL(crop_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), image,
                        (int)B, (int)H, (int)W, (int)D, (int)C, boxes, box_ind, total, ch, cw, cd,
                        method, extrapolation, crops);
@@ -512,6 +642,12 @@ extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
     rc = check_launch("pyramid_prep_kernel");
     if (rc) return rc;
     const int64_t total = B * N * ph * pw * pd;
+    if ((C & 3) == 0) {
+        LineArgs a{nullptr, nullptr, boxes_adj, levels, N, B * N * ph * pw, 0, 0, 0, (int)C, ph, pw, pd,
+                   0.0f, out};
+        hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, st(s), a, P);
+        return check_launch("line_fwd_kernel");
+    }
     hipLaunchKernelGGL(pyramid_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
                        (int)C, boxes_adj, levels, N, total, ph, pw, pd, out);
     return check_launch("pyramid_fwd_kernel");

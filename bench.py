@@ -120,10 +120,10 @@ def time_direct_conv(model, fmaps, reps=5):
 
 
 # ---------------------------------------------------------------- ROIAlign roofline
-def roi_boxes(n, S, seed=3):
-    """128 ROIs with log-uniform cube-root pixel volume in [24,128]."""
+def roi_boxes(n, S, seed=3, hi=128):
+    """n ROIs with log-uniform cube-root pixel volume in [24, hi]."""
     rng = np.random.default_rng(seed)
-    side = np.exp(rng.uniform(np.log(24), np.log(128), n))
+    side = np.exp(rng.uniform(np.log(24), np.log(hi), n))
     asp = np.exp(rng.uniform(-0.3, 0.3, (n, 3)))
     ext = side[:, None] * asp / S
     ext = np.minimum(ext, 0.95)
@@ -135,13 +135,11 @@ def unique_voxels(boxes, fshapes, pool, S):
     """|U|: distinct input voxels touched by all 8-corner samples (host, exact float32 maths)."""
     from oracle import ops_ref as R
     bx, lvl = R.roi_prepare(boxes[0], (S, S, S))
-    total = 0
+    keys, off = [], 0
     for li in range(4):
         sel = np.nonzero(lvl == li + 2)[0]
-        if not len(sel):
-            continue
         H, W, D = fshapes[li]
-        keys = set()
+        base, off = off, off + H * W * D
         for b in bx[sel]:
             coords = []
             for ax, (n, Sz) in enumerate(zip(pool, (H, W, D))):
@@ -149,17 +147,16 @@ def unique_voxels(boxes, fshapes, pool, S):
                 sc = np.float32((b2 - b1) * np.float32(Sz - 1)) / np.float32(n - 1)
                 c = np.float32(b1 * np.float32(Sz - 1)) + np.arange(n, dtype=np.float32) * sc
                 coords.append(np.unique(np.concatenate([np.floor(c), np.ceil(c)]).astype(np.int64)))
-            g = np.stack(np.meshgrid(*coords, indexing="ij"), -1).reshape(-1, 3)
-            keys.update(map(tuple, g))
-        total += len(keys)
-    return total
+            g = np.meshgrid(*coords, indexing="ij")
+            keys.append(base + ((g[0] * W + g[1]) * D + g[2]).ravel())
+    return int(np.unique(np.concatenate(keys)).size) if keys else 0
 
 
-def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14)):
+def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14), hi=128):
     from m3d import layers
     maps = [f.detach().contiguous() for f in fmaps[:4]]
     C = maps[0].shape[-1]
-    boxes = torch.from_numpy(roi_boxes(n_rois, S)).to(maps[0].device)
+    boxes = torch.from_numpy(roi_boxes(n_rois, S, hi=hi)).to(maps[0].device)
     meta = torch.zeros((1, 18), device=maps[0].device)
     meta[0, 5:8] = S
     res = {}
@@ -180,7 +177,7 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14)):
         res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "algorithmic_bytes": alg,
                            "gather_bytes": 8 * 4.0 * n_rois * p ** 3 * C,
                            "GBps": round(alg / t / 1e9, 1), "frac_hbm": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": _pmc_traffic(f"pyramid_fwd_pool{p}_S{S}")}
+                           "traffic": _pmc_traffic(f"pyramid_fwd_pool{p}_S{S}_N{n_rois}")}
     return res
 
 
@@ -227,6 +224,21 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     return out
 
 
+def roi_leg_large(S, dev, n_rois=512):
+    """configs[3] shapes: PyramidROIAlign 7^3 and 14^3 of 512 proposals on the
+    P2..P5 maps of a frozen S^3 forward (boxes log-uniform in [24, S] px, so
+    levels 2-4 are hit at 256^3)."""
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, synthetic_volume
+    model = RPN(synthetic_rpn_config(S), device=dev, seed=1)
+    with torch.no_grad():
+        fmaps = model.features(synthetic_volume(S).to(dev))
+    r = time_roi_align(fmaps, S, n_rois=n_rois, hi=S)
+    r["config"] = f"{n_rois} ROIs on P2..P5 of a {S}^3 volume, C=256"
+    del model, fmaps
+    return r
+
+
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(model, S, depth_slab=0, threads=None):
     """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
@@ -264,6 +276,7 @@ def main():
     ap.add_argument("--slab-size", type=int, default=256,
                     help="depth-slab leg volume size (configs[4]); 0 disables the leg")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / ROIAlign / CPU legs")
+    ap.add_argument("--roi-size", type=int, default=256, help="large-volume ROIAlign leg (0: off)")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
     args = ap.parse_args()
 
@@ -341,6 +354,12 @@ def main():
             out["roi_align"] = {"error": repr(e)}
         del fmaps
         torch.cuda.empty_cache()
+        if args.roi_size:
+            try:
+                out["roi_align_256"] = roi_leg_large(args.roi_size, dev)
+            except Exception as e:
+                out["roi_align_256"] = {"error": repr(e)}
+            torch.cuda.empty_cache()
         if world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(model, S, args.cpu_slab)

@@ -15,6 +15,7 @@ import bench  # noqa: E402
 
 leg = sys.argv[1]
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+NR = 128 if S == 128 else 512          # configs[2] / configs[3] ROI counts (bench.py)
 if leg == "gemm":
     print(bench.time_dominant_kernel(S, reps=3))
 else:
@@ -27,4 +28,5 @@ else:
     if leg == "direct":
         print(bench.time_direct_conv(model, fmaps, reps=3))
     else:
-        print(bench.time_roi_align(fmaps, S, reps=3, pools=(int(leg[3:]),)))
+        print(bench.time_roi_align(fmaps, S, n_rois=NR, reps=3, pools=(int(leg[3:]),),
+                                   hi=128 if S == 128 else S))
