@@ -25,6 +25,7 @@
 // channel-split stores (RPN class|bbox heads write their concatenated outputs
 // directly).
 #include "common.h"
+#include <stdlib.h>
 
 namespace m3d {
 
@@ -125,9 +126,10 @@ __device__ __forceinline__ void epi_store(const ConvP& p, const Epi& e, int64_t 
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
-    constexpr int BK = 32;
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
+__global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP p, Epi e) {
+    static_assert(BK == 32 || BK == 64, "BK");
+    static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     static_assert(WM * WN == 4, "4 waves");
     static_assert(TM >= 1 && TN >= 1, "tile");
@@ -138,8 +140,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
     constexpr int LDB = BT ? (BK + 4) : BN;
     constexpr int A_SZ = BM * LDA;
     constexpr int B_SZ = BT ? BN * LDB : BK * LDB;
-    constexpr int AQ = AVEC ? BM / 32 : BM / 8;      // A elements (float4 or float) per thread
-    constexpr int BQ = BN / 32;                      // B float4 per thread
+    constexpr int KC4 = BK / 4;                      // float4 columns of a k-tile row
+    constexpr int RPP = 256 / KC4;                   // tile rows loaded per pass
+    constexpr int AQ = AVEC ? BM / RPP : BM / 8;     // A elements (float4 or float) per thread
+    constexpr int BQ = BT ? BN / RPP : BK * BN / 1024;   // B float4 per thread
     __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -170,12 +174,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
     // offsets (tensor bytes < 4 GiB is checked on the host)
     int a_y[AVEC ? AQ : 1], a_x[AVEC ? AQ : 1], a_z[AVEC ? AQ : 1], a_off[AVEC ? AQ : 1];
     bool a_ok[AVEC ? AQ : 1];
-    const int a_col4 = tid & 7;
+    const int a_col4 = tid % KC4;
     const int rowW = p.D * p.C, rowH = p.W * rowW;
     if (AVEC) {
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
-            const int64_t m = m0 + (tid >> 3) + 32 * q;
+            const int64_t m = m0 + tid / KC4 + RPP * q;
             a_ok[q] = m < p.M;
             int b, oy, ox, oz;
             decompose(a_ok[q] ? m : 0, p.OH, p.OW, p.OD, b, oy, ox, oz);
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
             const int wt = p.flip ? (ntaps - 1 - tap) : tap;
 #pragma unroll
             for (int q = 0; q < BQ; ++q) {
-                const int n = n0 + (tid >> 3) + 32 * q;
+                const int n = n0 + tid / KC4 + RPP * q;
                 rb[q] = bload4(rsB, n < p.N ? (uint32_t)((wt * p.N + n) * p.C + c0 + a_col4 * 4) * 4u
                                             : M3D_OOB);
             }
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         if (AVEC) {
 #pragma unroll
             for (int q = 0; q < AQ; ++q)
-                *reinterpret_cast<float4*>(As + ((tid >> 3) + 32 * q) * LDA + a_col4 * 4) = ra[q];
+                *reinterpret_cast<float4*>(As + (tid / KC4 + RPP * q) * LDA + a_col4 * 4) = ra[q];
         } else {
 #pragma unroll
             for (int q = 0; q < AQ; ++q) As[((tid >> 5) + 8 * q) * LDA + (tid & 31)] = rs[q];
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         } else {
 #pragma unroll
             for (int q = 0; q < BQ; ++q)
-                *reinterpret_cast<float4*>(Bs + ((tid >> 3) + 32 * q) * LDB + a_col4 * 4) = rb[q];
+                *reinterpret_cast<float4*>(Bs + (tid / KC4 + RPP * q) * LDB + a_col4 * 4) = rb[q];
         }
     };
 
@@ -297,15 +301,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
         if (kt + 1 < nk) load_tile(kt + 1);
         const float* As = smem + buf * (A_SZ + B_SZ);
         const float* Bs = As + A_SZ;
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks) {
         // fragments: lane (l32, h) owns row l32 of each 32-row tile and the 16
-        // k values 16h..16h+15 of this k-tile (MFMA step s consumes k = 16h+s)
+        // k values 32ks+16h .. +15 of this k-tile (MFMA step s consumes k = 32ks+16h+s)
         float4 af[TM][4];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 af[i][q] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + i * 32 + l32) * LDA +
-                                                            h * 16 + 4 * q);
+                                                            ks * 32 + h * 16 + 4 * q);
         float4 bf[BT ? TN : 1][4];
         if (BT) {
 #pragma unroll
@@ -313,11 +319,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     bf[j][q] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + j * 32 + l32) * LDB +
-                                                                h * 16 + 4 * q);
+                                                                ks * 32 + h * 16 + 4 * q);
         }
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            const int kk = h * 16 + s;
+            const int kk = ks * 32 + h * 16 + s;
             float b[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
@@ -329,6 +335,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvP p, Epi e) {
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i][s >> 2], s & 3), b[j],
                                                                       acc[i][j], 0, 0, 0);
+        }
         }
         if (kt + 1 < nk) store_tile(buf ^ 1);
         __syncthreads();
@@ -513,22 +520,42 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 }
 
 // ------------------------------------------------------------------ dispatch
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC>
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
 static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
     dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC>), grid, dim3(256), 0, s, p, e);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK>), grid, dim3(256), 0, s, p, e);
+}
+
+// M3D_GEMM_BK=64 selects 64-deep k-tiles (1 block/CU: measured 25-30% slower
+// than 32-deep at 2 blocks/CU; kept for A/B testing)
+static int gemm_bk_env() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_BK"); return e ? atoi(e) : 32; }();
+    return v;
+}
+
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC>
+static void launch_gemm_bk(bool bk64, const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
+    if constexpr (AVEC) {
+        if (bk64) {
+            launch_gemm<BM, BN, WM, WN, BT, AVEC, 64>(p, e, s, nbatch);
+            return;
+        }
+    }
+    launch_gemm<BM, BN, WM, WN, BT, AVEC, 32>(p, e, s, nbatch);
 }
 
 template <bool BT, bool AVEC>
 static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch = 1) {
+    // 64-deep k-tiles when a k-tile stays inside one tap (C % 64 == 0)
+    const bool bk64 = AVEC && p.C % 64 == 0 && gemm_bk_env() == 64;
     if (p.N <= 32) {
-        launch_gemm<128, 32, 4, 1, BT, AVEC>(p, e, s, nbatch);
+        launch_gemm<128, 32, 4, 1, BT, AVEC, 32>(p, e, s, nbatch);
     } else if (p.N <= 64) {
-        launch_gemm<128, 64, 4, 1, BT, AVEC>(p, e, s, nbatch);
+        launch_gemm_bk<128, 64, 4, 1, BT, AVEC>(bk64, p, e, s, nbatch);
     } else {
         const int64_t blocks128 = ((p.M + 127) / 128) * ((p.N + 127) / 128) * nbatch;
-        if (blocks128 < 512) launch_gemm<64, 128, 2, 2, BT, AVEC>(p, e, s, nbatch);
-        else launch_gemm<128, 128, 2, 2, BT, AVEC>(p, e, s, nbatch);
+        if (blocks128 < 512) launch_gemm_bk<64, 128, 2, 2, BT, AVEC>(bk64, p, e, s, nbatch);
+        else launch_gemm_bk<128, 128, 2, 2, BT, AVEC>(bk64, p, e, s, nbatch);
     }
 }
 

@@ -75,14 +75,14 @@ def main():
                                                         OH, OW, OD, *stride, *g.pad, dw.data_ptr(), st()))
         tw = timeit(wg)
         if k == 3 and stride == (1, 1, 1) and cin % 32 == 0:
-            nb = int(L.m3d_conv3d_wino_workspace_bytes(1, H, W, D, cin, cout))
+            nb = int(L.m3d_conv3d_wino_workspace_bytes(1, H, W, D, D, cin, cout))
             ws = torch.empty(nb // 4 + 1, device=dev)
-            fw = lambda: _lib.check(L.m3d_conv3d_fwd_wino(x.data_ptr(), 1, H, W, D, cin, w.data_ptr(), cout,  # noqa: E731
+            fw = lambda: _lib.check(L.m3d_conv3d_fwd_wino(x.data_ptr(), 1, H, W, D, cin, w.data_ptr(), cout, D, 1,  # noqa: E731
                                                           b.data_ptr(), None, None, None, 1, None, y.data_ptr(),
                                                           ws.data_ptr(), nb, st()))
-            dw_ = lambda: _lib.check(L.m3d_conv3d_bwd_data_wino(dz.data_ptr(), w.data_ptr(), 1, H, W, D, cin, cout,  # noqa: E731
+            dw_ = lambda: _lib.check(L.m3d_conv3d_bwd_data_wino(dz.data_ptr(), w.data_ptr(), 1, H, W, D, cin, cout, D, 1,  # noqa: E731
                                                                 dx.data_ptr(), 0, ws.data_ptr(), nb, st()))
-            ww = lambda: _lib.check(L.m3d_conv3d_bwd_weight_wino(x.data_ptr(), dz.data_ptr(), 1, H, W, D, cin, cout,  # noqa: E731
+            ww = lambda: _lib.check(L.m3d_conv3d_bwd_weight_wino(x.data_ptr(), dz.data_ptr(), 1, H, W, D, cin, cout, D, 1,  # noqa: E731
                                                                  dw.data_ptr(), ws.data_ptr(), nb, st()))
             a, b2, c = timeit(fw), timeit(dw_), timeit(ww)
             print(f"{'  +wino ' + name:22s} {fl / a / 1e12:9.1f} {fl / b2 / 1e12:9.1f} {fl / c / 1e12:9.1f}   "
