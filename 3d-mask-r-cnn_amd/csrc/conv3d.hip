@@ -123,6 +123,53 @@ __device__ __forceinline__ void epi_store(const ConvP& p, const Epi& e, int64_t 
     }
 }
 
+// Four consecutive output channels n..n+3 of row m (same op order as epi_store,
+// element-wise): 16-byte loads / stores when the row strides allow it.
+__device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast<const float4*>(q); }
+__device__ __forceinline__ void st4(float* q, const float4& v) { *reinterpret_cast<float4*>(q) = v; }
+
+__device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t m, int n, float4 v) {
+    if (e.split > 0 || (e.ldy & 3)) {
+        epi_store(p, e, m, n, v.x);
+        epi_store(p, e, m, n + 1, v.y);
+        epi_store(p, e, m, n + 2, v.z);
+        epi_store(p, e, m, n + 3, v.w);
+        return;
+    }
+    int b = 0, oy = 0, ox = 0, oz = 0;
+    if (!e.simple || e.res_mode == 2) decompose(m, p.OH, p.OW, p.OD, b, oy, ox, oz);
+    if (e.bias) {
+        const float4 bb = ld4(e.bias + n);
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+    }
+    if (e.z) st4(e.z + m * p.N + n, v);
+    if (e.scale) {
+        const float4 sc = ld4(e.scale + n), sh = ld4(e.shift + n);
+        v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
+        v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
+    }
+    const int64_t yrow = e.simple ? m
+                                  : (((int64_t)b * e.YH + (int64_t)oy * e.ysy) * e.YW +
+                                     (int64_t)ox * e.ysx) * e.YD + (int64_t)oz * e.ysz;
+    if (e.res_mode) {
+        const float4 r = e.res_mode == 1
+                             ? ld4(e.res + yrow * e.ldy + n)
+                             : ld4(e.res + ((((int64_t)b * (p.OH >> 1) + (oy >> 1)) * (p.OW >> 1) +
+                                             (ox >> 1)) * p.OD + oz) * p.N + n);
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    if (e.relu) {
+        v.x = v.x > 0.0f ? v.x : 0.0f; v.y = v.y > 0.0f ? v.y : 0.0f;
+        v.z = v.z > 0.0f ? v.z : 0.0f; v.w = v.w > 0.0f ? v.w : 0.0f;
+    }
+    float* dst = e.y + yrow * e.ldy + n;
+    if (e.accumulate) {
+        const float4 o = ld4(dst);
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    st4(dst, v);
+}
+
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
@@ -341,19 +388,31 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP 
         __syncthreads();
     }
 
-    // epilogue: D[row][col], col = lane&31 (n), row = (r&3) + 8(r>>2) + 4h (m)
+    // epilogue: D[row][col], col = lane&31 (n), row = (r&3) + 8(r>>2) + 4h (m).
+    // The tile is staged through LDS (row stride BN+8: the two lane halves
+    // write rows 4 apart = 32 banks apart, conflict-free) and leaves as
+    // row-contiguous float4s: 16-byte stores and one epilogue evaluation per
+    // 4 channels instead of per element.  (The k-loop ended on a barrier.)
+    constexpr int LDT = BN + 8;
+    static_assert(BM * LDT <= 2 * (A_SZ + B_SZ), "epilogue tile must fit the k-loop LDS");
+    float* Ts = smem;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn * TN * 32 + j * 32 + l32;
-            if (n >= p.N) continue;
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < p.M) epi_store(p, e, m, n, acc[i][j][r]);
-            }
-        }
+            for (int r = 0; r < 16; ++r)
+                Ts[(wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * TN * 32 + j * 32 +
+                   l32] = acc[i][j][r];
+    __syncthreads();
+    constexpr int C4T = BN / 4;
+#pragma unroll 4
+    for (int idx = tid; idx < BM * C4T; idx += 256) {
+        const int row = idx / C4T, c4 = idx % C4T;
+        const int64_t m = m0 + row;
+        const int n = n0 + c4 * 4;
+        if (m < p.M && n < p.N) epi_store4(p, e, m, n, *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4));
+    }
 }
 
 // -------------------------------------------------------------------------
