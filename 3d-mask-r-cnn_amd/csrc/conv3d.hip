@@ -622,7 +622,7 @@ template <int BI, int BJ, int WI, int WJ, bool AVEC>
 static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s, int nbatch = 1) {
     const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;                   // aim >= 1024 blocks
-    const int64_t max_splits = (p.M + 1023) / 1024;                 // >= 1024 m per block
+    const int64_t max_splits = (p.M + 255) / 256;                   // >= 256 m per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     int64_t mper = (p.M + splits - 1) / splits;
