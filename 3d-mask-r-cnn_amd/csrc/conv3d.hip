@@ -173,8 +173,8 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
-__global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP p, Epi e) {
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF>
+__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_gemm_kernel(ConvP p, Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -191,7 +191,11 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP 
     constexpr int RPP = 256 / KC4;                   // tile rows loaded per pass
     constexpr int AQ = AVEC ? BM / RPP : BM / 8;     // A elements (float4 or float) per thread
     constexpr int BQ = BT ? BN / RPP : BK * BN / 1024;   // B float4 per thread
-    __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
+    // NBUF 2: double-buffered LDS (one barrier per k-tile); NBUF 1: one LDS
+    // stage (two barriers per k-tile) so 3 workgroups fit a CU.  Both keep the
+    // next k-tile's global loads in flight in registers during the MFMAs.
+    static_assert(NBUF == 1 || NBUF == 2, "NBUF");
+    __shared__ __attribute__((aligned(16))) float smem[NBUF * (A_SZ + B_SZ)];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP 
     store_tile(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
+        const int buf = NBUF == 2 ? (kt & 1) : 0;
         if (kt + 1 < nk) load_tile(kt + 1);
         const float* As = smem + buf * (A_SZ + B_SZ);
         const float* Bs = As + A_SZ;
@@ -384,8 +388,16 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP 
                                                                       acc[i][j], 0, 0, 0);
         }
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
-        __syncthreads();
+        if (NBUF == 2) {
+            if (kt + 1 < nk) store_tile(buf ^ 1);
+            __syncthreads();
+        } else {
+            __syncthreads();
+            if (kt + 1 < nk) {
+                store_tile(0);
+                __syncthreads();
+            }
+        }
     }
 
     // epilogue: D[row][col], col = lane&31 (n), row = (r&3) + 8(r>>2) + 4h (m).
@@ -394,24 +406,34 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : 2) void conv_gemm_kernel(ConvP 
     // row-contiguous float4s: 16-byte stores and one epilogue evaluation per
     // 4 channels instead of per element.  (The k-loop ended on a barrier.)
     constexpr int LDT = BN + 8;
-    static_assert(BM * LDT <= 2 * (A_SZ + B_SZ), "epilogue tile must fit the k-loop LDS");
+    constexpr int HALVES = (BM * LDT <= NBUF * (A_SZ + B_SZ)) ? 1 : 2;   // staged in row halves
+    constexpr int HR = BM / HALVES;
+    static_assert(HR * LDT <= NBUF * (A_SZ + B_SZ), "epilogue tile must fit the k-loop LDS");
+    static_assert(HALVES == 1 || (TM * 32) % HR == 0 || HR % (TM * 32) == 0, "wave rows vs halves");
     float* Ts = smem;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                Ts[(wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * TN * 32 + j * 32 +
-                   l32] = acc[i][j][r];
-    __syncthreads();
     constexpr int C4T = BN / 4;
+#pragma unroll
+    for (int hf = 0; hf < HALVES; ++hf) {
+        if (hf) __syncthreads();                 // previous half fully read
+        if ((wm * TM * 32) / HR == hf) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        Ts[(wm * TM * 32 - hf * HR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT +
+                           wn * TN * 32 + j * 32 + l32] = acc[i][j][r];
+        }
+        __syncthreads();
 #pragma unroll 4
-    for (int idx = tid; idx < BM * C4T; idx += 256) {
-        const int row = idx / C4T, c4 = idx % C4T;
-        const int64_t m = m0 + row;
-        const int n = n0 + c4 * 4;
-        if (m < p.M && n < p.N) epi_store4(p, e, m, n, *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4));
+        for (int idx = tid; idx < HR * C4T; idx += 256) {
+            const int row = idx / C4T, c4 = idx % C4T;
+            const int64_t m = m0 + hf * HR + row;
+            const int n = n0 + c4 * 4;
+            if (m < p.M && n < p.N)
+                epi_store4(p, e, m, n, *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4));
+        }
     }
 }
 
@@ -579,10 +601,22 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 }
 
 // ------------------------------------------------------------------ dispatch
+// M3D_GEMM_NBUF=1|2 selects the single- / double-buffered LDS k-loop (A/B testing)
+static int gemm_nbuf_env() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_NBUF"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
 static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
     dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK>), grid, dim3(256), 0, s, p, e);
+    if constexpr (BK == 32 && AVEC) {      // (the scalar-A loader spills at 3 blocks/CU)
+        if (gemm_nbuf_env() == 1) {
+            hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1>), grid, dim3(256), 0, s, p, e);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 2>), grid, dim3(256), 0, s, p, e);
 }
 
 // M3D_GEMM_BK=64 selects 64-deep k-tiles (1 block/CU: measured 25-30% slower
