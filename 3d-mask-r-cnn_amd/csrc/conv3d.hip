@@ -46,6 +46,7 @@ struct ConvP {
     // batched GEMMs (Winograd points): blockIdx.z selects the batch; A, W and Y
     // advance by these element strides (0 for ordinary convs)
     int64_t bsa, bsw, bsy;
+    int dly = 1, dlx = 1, dlz = 1;   // dilation (fwd only; mrcnn_mask_conv3b)
 };
 
 struct Epi {
@@ -65,7 +66,15 @@ struct Epi {
     int ysy, ysx, ysz;
     int accumulate;
     int simple;       // y row == m (same grid, unit store stride)
+    int deconv = 0;   // > 0: 2x2x2 stride-2 transposed conv, n = tap * deconv + o
 };
+
+// activation codes (Epi::relu): 0 none, 1 ReLU, 2 sigmoid (mrcnn_mask)
+__device__ __forceinline__ float act(int code, float v) {
+    if (code == 1) return v > 0.0f ? v : 0.0f;
+    if (code == 2) return 1.0f / (1.0f + expf(-v));
+    return v;
+}
 
 // Raw buffer loads: 32-bit byte offsets, and an out-of-range offset returns 0
 // -- used for the implicit zero padding of im2col so the loaders are
@@ -98,22 +107,36 @@ __device__ __forceinline__ void decompose(int64_t m64, int OH, int OW, int OD, i
     b = (int)t3;
 }
 
+// row of the output tensor that GEMM row m / column n lands in (strided,
+// (2,2,1)-upsampled or 2x2x2-deconvolved stores); n is reduced to the channel.
+__device__ __forceinline__ int64_t out_row(const ConvP& p, const Epi& e, int b, int oy, int ox, int oz,
+                                           int& n) {
+    if (e.deconv) {
+        const int t = n / e.deconv;
+        n -= t * e.deconv;
+        return (((int64_t)b * e.YH + 2 * oy + (t >> 2)) * e.YW + 2 * ox + ((t >> 1) & 1)) * e.YD + 2 * oz +
+               (t & 1);
+    }
+    return (((int64_t)b * e.YH + (int64_t)oy * e.ysy) * e.YW + (int64_t)ox * e.ysx) * e.YD +
+           (int64_t)oz * e.ysz;
+}
+
 __device__ __forceinline__ void epi_store(const ConvP& p, const Epi& e, int64_t m, int n, float v) {
     int b = 0, oy = 0, ox = 0, oz = 0;
     if (!e.simple || e.res_mode == 2) decompose(m, p.OH, p.OW, p.OD, b, oy, ox, oz);
+    const int64_t zrow = m * p.N + n;
+    const int64_t yrow = e.simple ? m : out_row(p, e, b, oy, ox, oz, n);
     if (e.bias) v += e.bias[n];
-    if (e.z) e.z[m * p.N + n] = v;
+    if (e.z) e.z[zrow] = v;
     if (e.scale) v = v * e.scale[n] + e.shift[n];
-    const int64_t yrow = e.simple ? m
-                                  : (((int64_t)b * e.YH + (int64_t)oy * e.ysy) * e.YW +
-                                     (int64_t)ox * e.ysx) * e.YD + (int64_t)oz * e.ysz;
     if (e.res_mode == 1) {
         v += e.res[yrow * e.ldy + n];
     } else if (e.res_mode == 2) {
         const int64_t rrow = (((int64_t)b * (p.OH >> 1) + (oy >> 1)) * (p.OW >> 1) + (ox >> 1)) * p.OD + oz;
         v += e.res[rrow * p.N + n];
     }
-    if (e.relu) v = v > 0.0f ? v : 0.0f;
+    v = act(e.relu, v);
+    if (e.res_mode == 3) v += e.res[yrow * e.ldy + n];      // Add() after the activation
     if (e.split > 0 && n >= e.split) {
         e.y2[yrow * e.ldy2 + (n - e.split)] = v;
     } else {
@@ -138,20 +161,19 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
     }
     int b = 0, oy = 0, ox = 0, oz = 0;
     if (!e.simple || e.res_mode == 2) decompose(m, p.OH, p.OW, p.OD, b, oy, ox, oz);
+    const int64_t zrow = m * p.N + n;
+    const int64_t yrow = e.simple ? m : out_row(p, e, b, oy, ox, oz, n);   // (n -> channel)
     if (e.bias) {
         const float4 bb = ld4(e.bias + n);
         v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
     }
-    if (e.z) st4(e.z + m * p.N + n, v);
+    if (e.z) st4(e.z + zrow, v);
     if (e.scale) {
         const float4 sc = ld4(e.scale + n), sh = ld4(e.shift + n);
         v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
         v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
     }
-    const int64_t yrow = e.simple ? m
-                                  : (((int64_t)b * e.YH + (int64_t)oy * e.ysy) * e.YW +
-                                     (int64_t)ox * e.ysx) * e.YD + (int64_t)oz * e.ysz;
-    if (e.res_mode) {
+    if (e.res_mode == 1 || e.res_mode == 2) {
         const float4 r = e.res_mode == 1
                              ? ld4(e.res + yrow * e.ldy + n)
                              : ld4(e.res + ((((int64_t)b * (p.OH >> 1) + (oy >> 1)) * (p.OW >> 1) +
@@ -159,8 +181,11 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     if (e.relu) {
-        v.x = v.x > 0.0f ? v.x : 0.0f; v.y = v.y > 0.0f ? v.y : 0.0f;
-        v.z = v.z > 0.0f ? v.z : 0.0f; v.w = v.w > 0.0f ? v.w : 0.0f;
+        v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
+    }
+    if (e.res_mode == 3) {
+        const float4 r = ld4(e.res + yrow * e.ldy + n);
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     float* dst = e.y + yrow * e.ldy + n;
     if (e.accumulate) {
@@ -253,7 +278,8 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
         if (AVEC) {
             const int tap = k0 / p.C;
             const int c0 = k0 - tap * p.C;
-            const int ky = tap / taps_kwkd, kx = (tap / taps_kd) % p.kw, kz = tap % taps_kd;
+            const int ky = tap / taps_kwkd * p.dly, kx = (tap / taps_kd) % p.kw * p.dlx,
+                      kz = tap % taps_kd * p.dlz;
             const int toff = ky * rowH + kx * rowW + kz * p.C + c0;
 #pragma unroll
             for (int q = 0; q < AQ; ++q) {
@@ -269,7 +295,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
             if (k < p.K) {
                 tap = k / p.C;
                 c = k - tap * p.C;
-                ky = tap / taps_kwkd; kx = (tap / taps_kd) % p.kw; kz = tap % taps_kd;
+                ky = tap / taps_kwkd * p.dly; kx = (tap / taps_kd) % p.kw * p.dlx; kz = tap % taps_kd * p.dlz;
             }
 #pragma unroll
             for (int q = 0; q < AQ; ++q) {
@@ -412,7 +438,6 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     static_assert(HALVES == 1 || (TM * 32) % HR == 0 || HR % (TM * 32) == 0, "wave rows vs halves");
     float* Ts = smem;
     constexpr int C4T = BN / 4;
-#pragma unroll
     for (int hf = 0; hf < HALVES; ++hf) {
         if (hf) __syncthreads();                 // previous half fully read
         if ((wm * TM * 32) / HR == hf) {
@@ -426,8 +451,10 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                            wn * TN * 32 + j * 32 + l32] = acc[i][j][r];
         }
         __syncthreads();
-#pragma unroll 4
-        for (int idx = tid; idx < HR * C4T; idx += 256) {
+#pragma unroll
+        for (int q = 0; q < (HR * C4T + 255) / 256; ++q) {
+            const int idx = tid + 256 * q;
+            if (HR * C4T % 256 && idx >= HR * C4T) break;
             const int row = idx / C4T, c4 = idx % C4T;
             const int64_t m = m0 + hf * HR + row;
             const int n = n0 + c4 * 4;
@@ -1041,6 +1068,124 @@ static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, i
     return M3D_OK;
 }
 
+// Strided batched GEMM: C[b] (+)= act(A[b] B[b] + bias), A[b] rows of stride
+// lda (K <= lda) at A + b*bsa, B[b] = B + b*bsb [K][N], C[b] = C + b*bsc [M][N].
+// Split-K is this call with batch = #K-slices (bsa = slice width, bsb =
+// slice*N) into a workspace, then m3d_splitk_reduce.
+extern "C" int m3d_gemm_f32_ex(const float* A, int64_t lda, int64_t bsa, const float* Bm,
+                               int64_t bsb, float* C, int64_t bsc, int64_t batch, int64_t M,
+                               int64_t K, int64_t N, const float* bias, int32_t act_code,
+                               int32_t accumulate, m3d_stream_t s) {
+    if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm: dimensions must be positive");
+    if (N % 4) return einval("gemm: N must be a multiple of 4");
+    if (lda < K) return einval("gemm: lda < K");
+    if (M > 0x7FFFFFFF || lda > 0x7FFFFFFF || N > 0x7FFFFFFF)
+        return einval("gemm: dimension larger than 2^31");
+    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
+    if (M * lda >= lim || K * N >= lim || M * N >= lim)
+        return einval("gemm: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p{};
+    p.a = A; p.B = 1; p.H = 1; p.W = (int)M; p.D = 1; p.C = (int)lda;   // rows along "x"
+    p.OH = 1; p.OW = (int)M; p.OD = 1;
+    p.kh = p.kw = p.kd = 1; p.sy = p.sx = p.sz = 1;
+    p.M = M; p.K = (int)K; p.w = Bm; p.N = (int)N;
+    p.bsa = bsa; p.bsw = bsb; p.bsy = bsc;
+    Epi e{};
+    e.bias = bias; e.relu = act_code; e.accumulate = accumulate;
+    e.y = C; e.ldy = N; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)M;
+    e.ysy = e.ysx = e.ysz = 1;
+    const bool vec = K % 32 == 0 && lda % 4 == 0 && bsa % 4 == 0 && ((uintptr_t)A & 15) == 0;
+    if (vec) dispatch_gemm<false, true>(p, e, st(s), (int)batch);
+    else dispatch_gemm<false, false>(p, e, st(s), (int)batch);
+    return check_launch("m3d_gemm_f32_ex");
+}
+
+// out[m][n] = act((sum_z ws[z][m][n] + bias[n]) * scale[n] + shift[n]), z in
+// order (deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                            int64_t M, int N,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            int act_code, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * N) return;
+    const int n = (int)(i % N);
+    float v = ws[i];
+    for (int z = 1; z < splits; ++z) v += ws[(int64_t)z * M * N + i];
+    if (bias) v += bias[n];
+    if (scale) v = v * scale[n] + shift[n];
+    out[i] = act(act_code, v);
+}
+
+extern "C" int m3d_splitk_reduce(const float* ws, int32_t splits, int64_t M, int64_t N,
+                                 const float* bias, const float* bn_scale, const float* bn_shift,
+                                 int32_t act_code, float* out, m3d_stream_t s) {
+    if (splits <= 0 || M < 0 || N <= 0) return einval("splitk_reduce: bad dimensions");
+    if ((bn_scale == nullptr) != (bn_shift == nullptr))
+        return einval("splitk_reduce: bn_scale and bn_shift must be given together");
+    if (M == 0) return M3D_OK;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(M * N, 256)), dim3(256), 0, st(s), ws, splits,
+                       M, (int)N, bias, bn_scale, bn_shift, act_code, out);
+    return check_launch("splitk_reduce_kernel");
+}
+
+// Conv3DTranspose(Cout, (2,2,2), strides=2, 'valid') (mrcnn_mask_deconv,
+// core/models.py:1228-1232): y[2i+a, 2j+b, 2k+c, o] = act(bias[o] +
+// sum_c x[i,j,k,c] w[a,b,c,o,cin]), Keras kernel [2,2,2,Cout,Cin].  One GEMM
+// rows = input voxels, K = Cin, columns = (tap, o) read from the kernel as
+// B^T, scattered by the epilogue to the 8 output voxels of each input voxel.
+extern "C" int m3d_deconv3d_k2s2(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                 int64_t Cin, const float* w, int64_t Cout, const float* bias,
+                                 int32_t act_code, float* y, m3d_stream_t s) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0 || Cin <= 0 || Cout <= 0)
+        return einval("deconv3d: tensor dimensions must be positive");
+    if (Cout % 4 || Cin % 32) return einval("deconv3d: Cout % 4 == 0 and Cin % 32 == 0 required");
+    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
+    if (B * H * W * D * Cin >= lim || B * H * W * D * 8 * Cout >= lim)
+        return einval("deconv3d: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p{};
+    p.a = x; p.B = (int)B; p.H = (int)H; p.W = (int)W; p.D = (int)D; p.C = (int)Cin;
+    p.OH = (int)H; p.OW = (int)W; p.OD = (int)D;
+    p.kh = p.kw = p.kd = 1; p.sy = p.sx = p.sz = 1;
+    p.M = B * H * W * D; p.K = (int)Cin; p.w = w; p.N = (int)(8 * Cout);
+    Epi e{};
+    e.bias = bias; e.relu = act_code; e.y = y; e.ldy = Cout;
+    e.YH = (int)(2 * H); e.YW = (int)(2 * W); e.YD = (int)(2 * D);
+    e.ysy = e.ysx = e.ysz = 1; e.simple = 0; e.deconv = (int)Cout;
+    dispatch_gemm<true, true>(p, e, st(s));
+    return check_launch("conv_gemm_kernel(deconv)");
+}
+
+extern "C" int m3d_conv3d_fwd_dil(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                  int64_t Cin, const float* w, int32_t kh, int32_t kw, int32_t kd,
+                                  int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
+                                  int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                                  int32_t dly, int32_t dlx, int32_t dlz, const float* bias,
+                                  const float* bn_scale, const float* bn_shift,
+                                  const float* residual, int32_t res_mode, int32_t act_code,
+                                  float* z_out, float* y, int64_t ldy, float* y2, int64_t ldy2,
+                                  int64_t split_n, m3d_stream_t s) {
+    int rc = conv_check(B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
+    if (rc) return rc;
+    if (dly <= 0 || dlx <= 0 || dlz <= 0) return einval("conv3d: dilation must be positive");
+    if ((bn_scale == nullptr) != (bn_shift == nullptr))
+        return einval("conv3d: bn_scale and bn_shift must be given together");
+    if (res_mode < 0 || res_mode > 3) return einval("conv3d: res_mode must be 0..3");
+    if (act_code < 0 || act_code > 2) return einval("conv3d: activation must be 0 (none), 1 (relu), 2 (sigmoid)");
+    if (res_mode != 0 && residual == nullptr) return einval("conv3d: residual missing");
+    if (res_mode == 2 && ((OH & 1) || (OW & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
+    if (split_n > 0 && y2 == nullptr) return einval("conv3d: split output needs y2");
+    ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
+            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0, 0, 0, 0};
+    p.dly = dly; p.dlx = dlx; p.dlz = dlz;
+    Epi e{bias, bn_scale, bn_shift, residual, res_mode, act_code, z_out, y, ldy > 0 ? ldy : Cout,
+          y2, ldy2, (int)split_n, (int)OH, (int)OW, (int)OD, 1, 1, 1, 0, 1};
+    if (Cin % 32 == 0) dispatch_gemm<false, true>(p, e, st(s));
+    else dispatch_gemm<false, false>(p, e, st(s));
+    return check_launch("conv_gemm_kernel(fwd)");
+}
+
 extern "C" int m3d_conv3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
                               int64_t Cin, const float* w, int32_t kh, int32_t kw, int32_t kd,
                               int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
@@ -1049,20 +1194,9 @@ extern "C" int m3d_conv3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, i
                               const float* residual, int32_t res_mode, int32_t relu, float* z_out,
                               float* y, int64_t ldy, float* y2, int64_t ldy2, int64_t split_n,
                               m3d_stream_t s) {
-    int rc = conv_check(B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
-    if (rc) return rc;
-    if ((bn_scale == nullptr) != (bn_shift == nullptr))
-        return einval("conv3d: bn_scale and bn_shift must be given together");
-    if (res_mode != 0 && residual == nullptr) return einval("conv3d: residual missing");
-    if (res_mode == 2 && ((OH & 1) || (OW & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
-    if (split_n > 0 && y2 == nullptr) return einval("conv3d: split output needs y2");
-    ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
-            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0, 0, 0, 0};
-    Epi e{bias, bn_scale, bn_shift, residual, res_mode, relu, z_out, y, ldy > 0 ? ldy : Cout,
-          y2, ldy2, (int)split_n, (int)OH, (int)OW, (int)OD, 1, 1, 1, 0, 1};
-    if (Cin % 32 == 0) dispatch_gemm<false, true>(p, e, st(s));
-    else dispatch_gemm<false, false>(p, e, st(s));
-    return check_launch("conv_gemm_kernel(fwd)");
+    return m3d_conv3d_fwd_dil(x, B, H, W, D, Cin, w, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px,
+                              pz, 1, 1, 1, bias, bn_scale, bn_shift, residual, res_mode, relu, z_out,
+                              y, ldy, y2, ldy2, split_n, s);
 }
 
 extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, int64_t H,

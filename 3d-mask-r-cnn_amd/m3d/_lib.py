@@ -62,6 +62,17 @@ _SIGS = {
                                  c_p, c_i32, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_weight_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                    c_i32, c_p, c_p, c_sz, c_p],
+    "m3d_gemm_f32_ex": [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
+                        c_i32, c_i32, c_p],
+    "m3d_splitk_reduce": [c_p, c_i32, c_i64, c_i64, c_p, c_p, c_p, c_i32, c_p, c_p],
+    "m3d_conv3d_fwd_dil": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_i32, c_i64,
+                           c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                           c_i32, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_p, c_p, c_i64, c_p,
+                           c_i64, c_i64, c_p],
+    "m3d_deconv3d_k2s2": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i32, c_p, c_p],
+    "m3d_head_outputs": [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p],
+    "m3d_refine_detections": [c_p, c_p, c_p, c_i64, c_i32, c_p, c_p, c_f, c_p, c_p, c_p, c_p],
+    "m3d_detections_gather": [c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p],
     "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,

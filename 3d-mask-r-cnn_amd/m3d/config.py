@@ -108,3 +108,14 @@ def synthetic_rpn_config(size: int, depth: int | None = None, **overrides) -> Co
     )
     d.update(overrides)
     return Config(**d)
+
+
+def synthetic_mrcnn_config(size: int, depth: int | None = None, **overrides) -> Config:
+    """MaskRCNN inference on the rats preset (configs/mrcnn/scp_mrcnn_rats.json head
+    sizes: FPN_CLASSIF_FC_LAYERS_SIZE 512, HEAD_CONV_CHANNEL 256, POOL 7, MASK_POOL 14,
+    DETECTION_NMS_THRESHOLD 0.3) with BASELINE configs[3]'s 512 proposals."""
+    d = dict(MODE="inference", POST_NMS_ROIS_INFERENCE=512, FPN_CLASSIF_FC_LAYERS_SIZE=512,
+             HEAD_CONV_CHANNEL=256, DETECTION_MAX_INSTANCES=40, DETECTION_MIN_CONFIDENCE=0.3,
+             DETECTION_NMS_THRESHOLD=0.3, MASK_SHAPE=[28, 28, 28])
+    d.update(overrides)
+    return synthetic_rpn_config(size, depth, **d)

@@ -214,7 +214,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     """Functional entry: ``layer`` is a Conv3D parameter group from params.py."""
     w = layer.kernel.data
     b = layer.bias.data if layer.bias is not None else None
-    grads = layer.grad_dict(bn)
+    grads = layer.grad_dict(bn) if torch.is_grad_enabled() else None   # inference: no z / grads
     bnt = None
     if bn is not None:
         bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)

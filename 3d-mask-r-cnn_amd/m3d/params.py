@@ -90,6 +90,8 @@ class ParamStore:
                 v.uniform_(-lim, lim, generator=g)
             elif isinstance(p.init, tuple) and p.init[0] == "normal":
                 v.normal_(0.0, p.init[1], generator=g)
+            elif isinstance(p.init, tuple) and p.init[0] == "const":
+                v.copy_(torch.as_tensor(p.init[1], dtype=torch.float32).reshape(p.shape))
             else:
                 raise ValueError(p.init)
         self.flat = flat.to(device).requires_grad_(True)

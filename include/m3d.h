@@ -203,6 +203,66 @@ int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64
 int m3d_gemm_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
                  int64_t N, const float* bias, int32_t relu, int32_t accumulate, m3d_stream_t s);
 
+/* Strided batched GEMM: for b < batch, C + b*bsc [M][N] (+)= act(A[b] B[b] + bias)
+ * with A[b] = A + b*bsa (rows of stride lda >= K), B[b] = B + b*bsb [K][N]; act
+ * 0 none / 1 ReLU / 2 sigmoid.  Split-K: batch = #K-slices of width kc (bsa =
+ * kc, bsb = kc*N, bsc = M*N) into a workspace, then m3d_splitk_reduce:
+ * out[m][n] = act((sum_z ws[z][m][n] + bias[n]) * bn_scale[n] + bn_shift[n])
+ * in a fixed z order.  Used for the head convolutions whose kernel covers the
+ * whole ROI (mrcnn_class_conv1, core/models.py:1128-1130: K = pool^3 * C). */
+int m3d_gemm_f32_ex(const float* A, int64_t lda, int64_t bsa, const float* B, int64_t bsb,
+                    float* C, int64_t bsc, int64_t batch, int64_t M, int64_t K, int64_t N,
+                    const float* bias, int32_t act, int32_t accumulate, m3d_stream_t s);
+int m3d_splitk_reduce(const float* ws, int32_t splits, int64_t M, int64_t N, const float* bias,
+                      const float* bn_scale, const float* bn_shift, int32_t act, float* out,
+                      m3d_stream_t s);
+
+/* m3d_conv3d_fwd with dilation (dly,dlx,dlz) (mrcnn_mask_conv3b, dilation
+ * (2,2,2), core/models.py:1214-1218), activation act = 0 / 1 ReLU / 2 sigmoid
+ * (mrcnn_mask), and res_mode 3 = residual added AFTER the activation
+ * (KL.Add of two activated branches, mrcnn_mask_res3). */
+int m3d_conv3d_fwd_dil(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                       const float* w, int32_t kh, int32_t kw, int32_t kd, int64_t Cout,
+                       int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
+                       int32_t py, int32_t px, int32_t pz, int32_t dly, int32_t dlx, int32_t dlz,
+                       const float* bias, const float* bn_scale, const float* bn_shift,
+                       const float* residual, int32_t res_mode, int32_t act, float* z_out,
+                       float* y, int64_t ldy, float* y2, int64_t ldy2, int64_t split_n,
+                       m3d_stream_t s);
+
+/* KL.Conv3DTranspose(Cout, (2,2,2), strides=2) (mrcnn_mask_deconv,
+ * core/models.py:1228-1232): x [B,H,W,D,Cin], Keras kernel w [2,2,2,Cout,Cin],
+ * y [B,2H,2W,2D,Cout] = act(bias + sum_cin x * w) (no overlap at stride 2).
+ * Cin % 32 == 0, Cout % 4 == 0. */
+int m3d_deconv3d_k2s2(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                      const float* w, int64_t Cout, const float* bias, int32_t act, float* y,
+                      m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * Mask R-CNN head glue (core/models.py:1121-1190, 1415-1575).
+ * m3d_head_outputs: raw [N][ldr] = [class logits (C) | bbox deltas (6C)] of
+ *   the two TimeDistributed Dense layers -> logits [N,C] clipped to [-10,10],
+ *   probs [N,C] softmax, bbox [N,C,6].
+ * m3d_refine_detections: per ROI of refine_detections_graph: fg prob >=
+ *   min_conf, class-1 deltas * BBOX_STD_DEV applied to the pixel ROI
+ *   (apply_box_deltas_3d_graph, core/utils.py:412-458), clip to the image,
+ *   min size (1,1,0.5 px).  boxes_px [N,6], nms_boxes [N,4] (y1,x1,y2,x2),
+ *   scores [N] (-FLT_MAX for filtered ROIs).  Then m3d_nms3d(mode 1,
+ *   DETECTION_MAX_INSTANCES, DETECTION_NMS_THRESHOLD) on (nms_boxes, scores).
+ * m3d_detections_gather: det [max_inst, 8] = (normalised box, class 1, score)
+ *   of the kept ROIs in NMS order, zero rows after *num_keep.
+ * image_meta: one row (compose_image_meta), image shape at [5:8].
+ * ------------------------------------------------------------------------- */
+int m3d_head_outputs(const float* raw, int64_t N, int64_t ldr, int32_t num_classes, float* logits,
+                     float* probs, float* bbox, m3d_stream_t s);
+int m3d_refine_detections(const float* rois, const float* probs, const float* deltas, int64_t N,
+                          int32_t num_classes, const float* image_meta,
+                          const float bbox_std_dev[6], float min_conf, float* boxes_px,
+                          float* nms_boxes, float* scores, m3d_stream_t s);
+int m3d_detections_gather(const float* boxes_px, const float* scores, const int32_t* keep,
+                          const int32_t* num_keep, int32_t max_inst, const float* image_meta,
+                          float* det, m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
  * ------------------------------------------------------------------------- */

@@ -234,3 +234,38 @@ def test_apply_box_deltas_identity_and_scale():
     d = np.array([[0, 0, 0, math.log(2.0), 0, 0]], np.float32)
     out = R.apply_box_deltas(a, d)
     np.testing.assert_allclose(out[0, [0, 3]], [0.0, 0.8], atol=1e-6)
+
+
+def test_heads_ref_deconv_matches_torch_conv_transpose():
+    """oracle/heads_ref.py's Conv3DTranspose restatement vs torch's transposed conv."""
+    import torch
+    from oracle import heads_ref as HR
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((2, 3, 2, 4, 5), generator=g, dtype=torch.float64)
+    w = torch.randn((2, 2, 2, 6, 5), generator=g, dtype=torch.float64)
+    b = torch.randn((6,), generator=g, dtype=torch.float64)
+    pt = torch.nn.functional.conv_transpose3d(x.permute(0, 4, 1, 2, 3), w.permute(4, 3, 0, 1, 2), b, stride=2)
+    assert torch.allclose(pt.permute(0, 2, 3, 4, 1), HR.deconv_k2s2(x, w, b), atol=1e-12)
+
+
+def test_heads_ref_refine_detections_known_answer():
+    """Zero deltas keep the ROI; confidence / min-size filters; 2-D NMS over the
+    (y,x) footprint suppresses a z-shifted duplicate; padding rows are zero."""
+    from oracle import heads_ref as HR
+    rois = np.array([[0.1, 0.1, 0.1, 0.3, 0.3, 0.3],      # kept (score .9)
+                     [0.1, 0.1, 0.6, 0.3, 0.3, 0.9],      # same y/x footprint: suppressed
+                     [0.5, 0.5, 0.1, 0.7, 0.7, 0.2],      # kept (score .8)
+                     [0.5, 0.5, 0.5, 0.5, 0.5, 0.5],      # zero size: dropped
+                     [0.8, 0.1, 0.1, 0.9, 0.2, 0.2]],     # below confidence
+                    np.float32)
+    fg = np.array([0.9, 0.85, 0.8, 0.95, 0.1], np.float32)
+    probs = np.stack([1 - fg, fg], 1)
+    deltas = np.zeros((5, 2, 6), np.float32)
+    meta = np.zeros(18, np.float32)
+    meta[5:8] = [100, 100, 10]
+    det, kept = HR.refine_detections(rois, probs, deltas, meta, [0.1] * 6, 0.5, 0.3, 4)
+    assert list(kept) == [0, 2]
+    np.testing.assert_allclose(det[0, :6], rois[0], atol=1e-6)
+    np.testing.assert_allclose(det[1, :6], rois[2], atol=1e-6)
+    assert det[0, 7] == np.float32(0.9) and det[1, 7] == np.float32(0.8)
+    assert np.all(det[2:] == 0)
