@@ -239,6 +239,39 @@ def roi_leg_large(S, dev, n_rois=512):
     return r
 
 
+def mrcnn_inference_leg(S, steps, warmup, dev):
+    """BASELINE configs[3]: full Mask R-CNN inference on one S^3 volume --
+    backbone + FPN + RPN forward, ProposalLayer (3-D NMS, 512 proposals),
+    PyramidROIAlign 7^3 -> classifier head -> DetectionLayer (2-D NMS) ->
+    PyramidROIAlign 14^3 -> mask head.  Random-init weights: the detection
+    count is whatever the synthetic volume yields (reported)."""
+    from m3d.config import synthetic_mrcnn_config
+    from m3d.heads import MaskRCNN
+    from m3d.model import compose_image_meta, synthetic_volume
+    cfg = synthetic_mrcnn_config(S)
+    model = MaskRCNN(cfg, device=dev, seed=1)
+    image = synthetic_volume(S, seed=100).to(dev)
+    meta = torch.from_numpy(compose_image_meta(0, [S, S, S, 1], [S, S, S, 1], [0, 0, 0, S, S, S], 1.0,
+                                               [0, 1])[None]).to(dev)
+    for _ in range(warmup):
+        out = model.detect(image, meta)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = model.detect(image, meta)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n_det = int((out["detections"][0, :, 7] > 0).sum())
+    res = {"workload": f"configs[3]: MaskRCNN inference, one {S}^3 volume, {cfg.POST_NMS_ROIS_INFERENCE} "
+                       f"proposals, ROIAlign 7^3/14^3, classifier + DetectionLayer + mask head",
+           "size": S, "ms_per_volume": round(el / steps * 1e3, 2), "volumes_per_s": round(steps / el, 4),
+           "detections": n_det, "max_instances": int(cfg.DETECTION_MAX_INSTANCES),
+           "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    del model, out
+    torch.cuda.empty_cache()
+    return res
+
+
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(model, S, depth_slab=0, threads=None):
     """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
@@ -277,6 +310,7 @@ def main():
                     help="depth-slab leg volume size (configs[4]); 0 disables the leg")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / ROIAlign / CPU legs")
     ap.add_argument("--roi-size", type=int, default=256, help="large-volume ROIAlign leg (0: off)")
+    ap.add_argument("--infer-size", type=int, default=256, help="MaskRCNN inference leg size (0: off)")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
     args = ap.parse_args()
 
@@ -360,6 +394,12 @@ def main():
             except Exception as e:
                 out["roi_align_256"] = {"error": repr(e)}
             torch.cuda.empty_cache()
+        if args.infer_size:
+            try:
+                out["mrcnn_inference"] = mrcnn_inference_leg(args.infer_size, max(3, args.steps // 2),
+                                                             1, dev)
+            except Exception as e:
+                out["mrcnn_inference"] = {"error": repr(e)}
         if world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(model, S, args.cpu_slab)

@@ -3,6 +3,7 @@ passes of scripts/gpu_prof.sh:  kernels_for_pmc.py LEG [S]
   gemm    the dominant kernel's largest launch (batched Winograd GEMM of rpn_conv_shared1)
   direct  rpn_conv_shared1 as a direct implicit-GEMM conv on P2
   roi7 / roi14  PyramidROIAlign 7^3 / 14^3 at configs[2] shapes
+  infer   MaskRCNN inference (configs[3]) x3 after one warm-up
 The priced kernel's dispatches are the LAST ones of its name in the trace."""
 import os
 import sys
@@ -18,6 +19,8 @@ S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 NR = 128 if S == 128 else 512          # configs[2] / configs[3] ROI counts (bench.py)
 if leg == "gemm":
     print(bench.time_dominant_kernel(S, reps=3))
+elif leg == "infer":
+    print(bench.mrcnn_inference_leg(S, 3, 1, torch.device("cuda")))
 else:
     from m3d.config import synthetic_rpn_config
     from m3d.model import RPN, synthetic_volume
