@@ -523,10 +523,14 @@ __global__ void mask_targets_kernel(const uint8_t* __restrict__ masks, int H, in
     const int x = (int)(t % mw); t /= mw;
     const int y = (int)(t % mh);
     const int64_t p = t / mh;
+    const int g = assign[p];
+    if (g < 0) {      // not a positive ROI (DetectionTargetLayer padding rows)
+        out[i] = 0.0f;
+        return;
+    }
     const Sample s = make_sample(boxes + p * 6, H, W, D, mh, mw, md, y, x, z);
     float v = 0.0f;   // extrapolation_value 0
     if (!s.oob) {
-        const int g = assign[p];
         auto M = [&](int yy, int xx, int zz) {
             return (float)masks[(((int64_t)yy * W + xx) * D + zz) * G + g];
         };

@@ -1,0 +1,89 @@
+"""Training-target layers on the GPU.
+
+``DetectionTargetLayer(config, train_rois_per_image, roi_positive_ratio,
+bbox_std_dev, use_mini_mask, mask_shape, images_per_gpu,
+positive_iou_threshold, negative_iou_threshold)([proposals, gt_class_ids,
+gt_boxes, gt_masks])`` -> [rois, target_gt_boxes, target_class_ids,
+target_bbox, target_mask] (core/models.py:1043-1118 / detection_targets_graph
+736-1040): sampling, box refinement and mask targets run as two libm3d
+launches per image (m3d_detection_targets + m3d_mask_targets3d), sizes fixed
+by TRAIN_ROIS_PER_IMAGE, nothing returns to the host.  When ``config`` is
+given, the IoU thresholds come from RPN_POSITIVE_IOU / RPN_NEGATIVE_IOU as in
+the reference.  The reference's tf.random.shuffle becomes a seeded random
+order (``seed`` advances per call), so runs are reproducible.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from ._lib import check, ptr, stream
+
+
+class DetectionTargetLayer:
+    def __init__(self, config, train_rois_per_image, roi_positive_ratio, bbox_std_dev, use_mini_mask,
+                 mask_shape, images_per_gpu, positive_iou_threshold=0.5, negative_iou_threshold=0.1,
+                 seed=0, name="proposal_targets", **kwargs):
+        self.config = config
+        self.T = int(train_rois_per_image)
+        self.ratio = float(roi_positive_ratio)
+        self.std = [float(np.float32(v)) for v in bbox_std_dev]
+        self.use_mini_mask = bool(use_mini_mask)
+        self.mask_shape = tuple(int(v) for v in mask_shape)
+        self.images_per_gpu = int(images_per_gpu)
+        self.pos_thr = float(positive_iou_threshold)
+        self.neg_thr = float(negative_iou_threshold)
+        if config is not None:            # detection_targets_graph(config=...) overrides (core/models.py:750-758)
+            self.T = int(getattr(config, "TRAIN_ROIS_PER_IMAGE", 256))
+            self.ratio = float(getattr(config, "ROI_POSITIVE_RATIO", 0.5))
+            self.std = [float(np.float32(v)) for v in getattr(config, "BBOX_STD_DEV", self.std)]
+            self.use_mini_mask = bool(getattr(config, "USE_MINI_MASK", True))
+            self.mask_shape = tuple(int(v) for v in getattr(config, "MASK_SHAPE", (28, 28, 28)))
+            self.pos_thr = float(getattr(config, "RPN_POSITIVE_IOU", 0.25))
+            self.neg_thr = float(getattr(config, "RPN_NEGATIVE_IOU", 0.15))
+        self.seed = int(seed)
+        self.name = name
+
+    def __call__(self, inputs, seed=None):
+        proposals, gt_class_ids, gt_boxes, gt_masks = inputs
+        ops._dev(proposals, gt_class_ids, gt_boxes, gt_masks)
+        L = _lib.load()
+        B, N = proposals.shape[:2]
+        G = gt_boxes.shape[1]
+        T = self.T
+        dev = proposals.device
+        mh, mw, md = self.mask_shape
+        out = {k: torch.zeros((B, T, 6), device=dev) for k in ("rois", "gt", "deltas", "mask_boxes")}
+        cls = torch.zeros((B, T), device=dev, dtype=torch.int32)
+        assign = torch.empty((B, T), device=dev, dtype=torch.int32)
+        counts = torch.zeros((B, 2), device=dev, dtype=torch.int32)
+        masks = torch.empty((B, T, mh, mw, md), device=dev)
+        wsb = int(L.m3d_detection_targets_workspace_bytes(N))
+        ws = torch.empty(max(wsb // 4, 1), device=dev, dtype=torch.int32)
+        sd = (_lib.c_f * 6)(*self.std)
+        s0 = self.seed if seed is None else int(seed)
+        for b in range(B):
+            p = proposals[b].detach().float().contiguous()
+            gc = gt_class_ids[b].to(torch.int32).contiguous()
+            gb = gt_boxes[b].detach().float().contiguous()
+            check(L.m3d_detection_targets(ptr(p), N, ptr(gc), ptr(gb), G, T, self.ratio, self.pos_thr,
+                                          self.neg_thr, sd, 1 if self.use_mini_mask else 0,
+                                          (s0 * 1000003 + b) & 0xFFFFFFFF, out["rois"][b].data_ptr(),
+                                          out["gt"][b].data_ptr(), cls[b].data_ptr(), out["deltas"][b].data_ptr(),
+                                          out["mask_boxes"][b].data_ptr(), assign[b].data_ptr(),
+                                          counts[b].data_ptr(), ptr(ws), wsb, stream()), "detection_targets")
+            m = gt_masks[b]
+            H, W, D, Gm = m.shape
+            mu8 = m.to(torch.uint8).contiguous()
+            check(L.m3d_mask_targets3d(ptr(mu8), H, W, D, Gm, out["mask_boxes"][b].data_ptr(),
+                                       assign[b].data_ptr(), T, mh, mw, md, masks[b].data_ptr(), stream()),
+                  "mask_targets3d")
+        if seed is None:
+            self.seed += 1
+        self.last_counts = counts
+        return [out["rois"], out["gt"], cls, out["deltas"], masks]
+
+    def compute_output_shape(self, input_shape):
+        return [(None, self.T, 6), (None, self.T, 6), (None, self.T), (None, self.T, 6),
+                (None, self.T) + self.mask_shape]

@@ -92,7 +92,8 @@ int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
  * round_half_even(CropAndResize3D(float(gt_masks[..., assign[p]]), rois[p],
  * (mh,mw,md), trilinear, extrapolation 0)), reading the boolean masks
  * [H,W,D,G] (uint8) in place instead of materialising the [P,H,W,D,1] gather.
- * rois are the (mini-mask-normalised when USE_MINI_MASK) positive boxes. */
+ * rois are the (mini-mask-normalised when USE_MINI_MASK) positive boxes;
+ * rows with assign[p] < 0 are written as zeros. */
 int m3d_mask_targets3d(const uint8_t* gt_masks, int64_t H, int64_t W, int64_t D, int64_t G,
                        const float* rois, const int32_t* assign, int64_t P, int32_t mh,
                        int32_t mw, int32_t md, float* out /*[P,mh,mw,md]*/, m3d_stream_t s);
@@ -262,6 +263,29 @@ int m3d_refine_detections(const float* rois, const float* probs, const float* de
 int m3d_detections_gather(const float* boxes_px, const float* scores, const int32_t* keep,
                           const int32_t* num_keep, int32_t max_inst, const float* image_meta,
                           float* det, m3d_stream_t s);
+
+/* ---------------------------------------------------------------------------
+ * DetectionTargetLayer (detection_targets_graph, core/models.py:736-1040) for
+ * one image, one workgroup, padded fixed-size outputs (no host round trip).
+ * proposals [N,6] (zero rows = padding), gt_class_ids [G], gt_boxes [G,6]
+ * normalised (zero rows = padding); N <= 16384, G <= 256.  Positives: IoU max
+ * >= positive_iou_threshold, negatives: < negative_iou_threshold; each set in
+ * a seeded random order (replaces tf.random.shuffle), positive_count =
+ * min(int(f32(T)*ratio), #pos), negatives fill up to T, zero padding after.
+ * Outputs [T,...]: rois, roi_gt_boxes, class_ids, deltas
+ * (box_refinement_graph / bbox_std_dev), mask_boxes (mini-mask normalised if
+ * use_mini_mask) and mask_assign (original GT index, -1 for non-positive
+ * rows) for m3d_mask_targets3d; counts[2] = (positives, negatives) (optional).
+ * workspace: m3d_detection_targets_workspace_bytes(N). */
+size_t m3d_detection_targets_workspace_bytes(int64_t N);
+int m3d_detection_targets(const float* proposals, int64_t N, const int32_t* gt_class_ids,
+                          const float* gt_boxes, int64_t G, int32_t train_rois_per_image,
+                          float roi_positive_ratio, float positive_iou_threshold,
+                          float negative_iou_threshold, const float bbox_std_dev[6],
+                          int32_t use_mini_mask, uint32_t seed, float* rois, float* roi_gt_boxes,
+                          int32_t* class_ids, float* deltas, float* mask_boxes,
+                          int32_t* mask_assign, int32_t* counts, void* workspace, size_t ws_bytes,
+                          m3d_stream_t s);
 
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.

@@ -128,3 +128,90 @@ def refine_detections(rois, probs, deltas, image_meta, bbox_std_dev, min_conf, n
     det[:k, 6] = 1.0
     det[:k, 7] = s2[sel]
     return det, conf[ok][sel]
+
+
+# ---------------------------------------------------------------------------
+# DetectionTargetLayer (core/models.py:736-1040)
+# ---------------------------------------------------------------------------
+def _mix32(x):
+    x = np.uint32(x)
+    x ^= x >> np.uint32(16)
+    x = np.uint32((int(x) * 0x7feb352d) & 0xFFFFFFFF)
+    x ^= x >> np.uint32(15)
+    x = np.uint32((int(x) * 0x846ca68b) & 0xFFFFFFFF)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def shuffle_keys(n, seed):
+    """The seeded random order that replaces tf.random.shuffle (30-bit keys, index tie-break)."""
+    return [int(_mix32((i * 0x9E3779B9 & 0xFFFFFFFF) ^ seed)) >> 2 for i in range(n)]
+
+
+def overlaps_graph(b1, b2):
+    """core/models.py:695-733, float32."""
+    f = np.float32
+    b1 = np.asarray(b1, f)[:, None]
+    b2 = np.asarray(b2, f)[None]
+    y1 = np.maximum(b1[..., 0], b2[..., 0]); x1 = np.maximum(b1[..., 1], b2[..., 1])
+    z1 = np.maximum(b1[..., 2], b2[..., 2]); y2 = np.minimum(b1[..., 3], b2[..., 3])
+    x2 = np.minimum(b1[..., 4], b2[..., 4]); z2 = np.minimum(b1[..., 5], b2[..., 5])
+    inter = np.maximum(y2 - y1, f(0)) * np.maximum(x2 - x1, f(0)) * np.maximum(z2 - z1, f(0))
+    v1 = (b1[..., 3] - b1[..., 0]) * (b1[..., 4] - b1[..., 1]) * (b1[..., 5] - b1[..., 2])
+    v2 = (b2[..., 3] - b2[..., 0]) * (b2[..., 4] - b2[..., 1]) * (b2[..., 5] - b2[..., 2])
+    return (inter / np.maximum(v1 + v2 - inter, f(1e-10))).astype(f)
+
+
+def box_refinement(box, gt):
+    """core/utils.py:616-650 (the module's final box_refinement_graph), float32."""
+    f = np.float32
+    eps = f(1e-6)
+    h, w, d = box[:, 3] - box[:, 0], box[:, 4] - box[:, 1], box[:, 5] - box[:, 2]
+    cy, cx, cz = box[:, 0] + f(0.5) * h, box[:, 1] + f(0.5) * w, box[:, 2] + f(0.5) * d
+    gh, gw, gd = gt[:, 3] - gt[:, 0], gt[:, 4] - gt[:, 1], gt[:, 5] - gt[:, 2]
+    gcy, gcx, gcz = gt[:, 0] + f(0.5) * gh, gt[:, 1] + f(0.5) * gw, gt[:, 2] + f(0.5) * gd
+    return np.stack([(gcy - cy) / np.maximum(h, eps), (gcx - cx) / np.maximum(w, eps),
+                     (gcz - cz) / np.maximum(d, eps), np.log(np.maximum(gh, eps) / np.maximum(h, eps)),
+                     np.log(np.maximum(gw, eps) / np.maximum(w, eps)),
+                     np.log(np.maximum(gd, eps) / np.maximum(d, eps))], 1).astype(f)
+
+
+def detection_targets(proposals, gt_class_ids, gt_boxes, T, ratio, pos_thr, neg_thr, std, use_mini_mask,
+                      seed):
+    """One image -> rois, roi_gt_boxes, class_ids, deltas, mask_boxes, mask_assign (all [T,...])."""
+    f = np.float32
+    P = np.asarray(proposals, f)
+    gtb = np.asarray(gt_boxes, f)
+    pv = np.nonzero(np.abs(P).sum(1) != 0)[0]
+    gv = np.nonzero(np.abs(gtb).sum(1) != 0)[0]
+    out = [np.zeros((T, 6), f), np.zeros((T, 6), f), np.zeros(T, np.int32), np.zeros((T, 6), f),
+           np.zeros((T, 6), f), np.full(T, -1, np.int32)]
+    if len(pv) == 0 or len(gv) == 0:
+        return out
+    ov = overlaps_graph(P[pv], gtb[gv])
+    iou_max = ov.max(1)
+    arg = gv[ov.argmax(1)]
+    keys = shuffle_keys(len(P), seed)
+    pos = [i for i, m in zip(pv, iou_max) if m >= f(pos_thr)]
+    neg = [i for i, m in zip(pv, iou_max) if m < f(neg_thr)]
+    pos.sort(key=lambda i: (keys[i], i))
+    neg.sort(key=lambda i: (keys[i], i))
+    pc = min(int(f(T) * f(ratio)), len(pos))
+    nc = max(min(T - pc, len(neg)), 0)
+    amap = dict(zip(pv, arg))
+    sel_p = np.array(pos[:pc], np.int64)
+    sel_n = np.array(neg[:nc], np.int64)
+    out[0][:pc] = P[sel_p]
+    out[0][pc:pc + nc] = P[sel_n]
+    if pc:
+        g = np.array([amap[i] for i in sel_p])
+        out[1][:pc] = gtb[g]
+        out[2][:pc] = np.asarray(gt_class_ids)[g]
+        out[3][:pc] = box_refinement(P[sel_p], gtb[g]) / np.asarray(std, f)
+        if use_mini_mask:
+            ext = np.stack([gtb[g, 3] - gtb[g, 0], gtb[g, 4] - gtb[g, 1], gtb[g, 5] - gtb[g, 2]], 1)
+            out[4][:pc] = (P[sel_p] - np.concatenate([gtb[g, :3], gtb[g, :3]], 1)) / np.concatenate([ext, ext], 1)
+        else:
+            out[4][:pc] = P[sel_p]
+        out[5][:pc] = g
+    return out

@@ -1,0 +1,67 @@
+"""GPU DetectionTargetLayer (m3d/targets.py) vs the float32 restatement of
+detection_targets_graph (oracle/heads_ref.py) with the same seeded sampling
+order: selected ROIs, GT assignment, class ids and mask targets bit-exact,
+box-refinement deltas to float32 log rounding."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import heads_ref as HR
+from oracle import ops_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(rng, N, G, H=32, W=32, D=16):
+    gt = np.zeros((G, 6), np.float32)
+    for g in range(G - 1):                              # last GT row = zero padding
+        lo = rng.uniform(0.05, 0.6, 3)
+        gt[g] = np.concatenate([lo, lo + rng.uniform(0.15, 0.35, 3)])
+    props = np.zeros((N, 6), np.float32)
+    for i in range(N - 7):                              # trailing zero padding rows
+        g = gt[rng.integers(0, G - 1)]
+        jit = rng.normal(0, 0.06, 6).astype(np.float32) if i % 3 else rng.uniform(-0.5, 0.5, 6).astype(np.float32)
+        b = np.clip(g + jit, 0, 1)
+        props[i] = np.concatenate([np.minimum(b[:3], b[3:]), np.maximum(b[:3], b[3:]) + 0.01])
+    props = np.clip(props, 0, 1).astype(np.float32)
+    props[-7:] = 0
+    cls = rng.integers(1, 3, G).astype(np.int32)
+    masks = rng.uniform(size=(H, W, D, G)) > 0.5
+    return props, cls, gt, masks
+
+
+@pytest.mark.parametrize("N,G,T,mini", [(300, 5, 64, False), (2000, 9, 128, True), (40, 3, 128, False)])
+def test_detection_targets(cuda, N, G, T, mini):
+    from m3d.targets import DetectionTargetLayer
+    rng = np.random.default_rng(N)
+    props, cls, gt, masks = _case(rng, N, G)
+    std = [0.1, 0.1, 0.1, 0.213, 0.21, 0.15]
+    layer = DetectionTargetLayer(None, T, 0.33, std, mini, (8, 8, 8), 1, positive_iou_threshold=0.5,
+                                 negative_iou_threshold=0.3)
+    seed = 12345
+    outs = layer([torch.from_numpy(x[None]).to(cuda) for x in (props, cls, gt, masks)], seed=seed)
+    rois, tgt, tcls, tdel, tmask = (o[0].cpu().numpy() for o in outs)
+    ref = HR.detection_targets(props, cls, gt, T, 0.33, 0.5, 0.3, std, mini, (seed * 1000003) & 0xFFFFFFFF)
+    assert np.array_equal(rois, ref[0])
+    assert np.array_equal(tgt, ref[1])
+    assert np.array_equal(tcls, ref[2])
+    pc = int((ref[5] >= 0).sum())
+    assert pc > 0 and np.array_equal(layer.last_counts[0].cpu().numpy()[0], pc)
+    np.testing.assert_allclose(tdel, ref[3], rtol=2e-6, atol=2e-6)
+    # mask targets: tf.round(CropAndResize3D(gt mask of the assigned GT, mask box))
+    want = np.zeros_like(tmask)
+    for r in range(pc):
+        img = masks[..., ref[5][r]].astype(np.float32)[None, ..., None]
+        crop = R.crop_and_resize_3d(img, ref[4][r:r + 1], np.zeros(1, np.int32), (8, 8, 8))
+        want[r] = np.round(crop[0, ..., 0])
+    assert np.array_equal(tmask, want)
+
+
+def test_detection_targets_empty_gt(cuda):
+    from m3d.targets import DetectionTargetLayer
+    props = np.random.default_rng(0).uniform(0, 1, (50, 6)).astype(np.float32)
+    layer = DetectionTargetLayer(None, 32, 0.5, [0.1] * 6, False, (4, 4, 4), 1)
+    outs = layer([torch.from_numpy(x[None]).to(cuda) for x in
+                  (props, np.zeros(3, np.int32), np.zeros((3, 6), np.float32), np.zeros((8, 8, 8, 3), bool))])
+    for o in outs:
+        assert float(o.abs().sum()) == 0.0
