@@ -76,6 +76,9 @@ _SIGS = {
     "m3d_detection_targets_workspace_bytes": [c_i64],
     "m3d_detection_targets": [c_p, c_i64, c_p, c_p, c_i64, c_i32, c_f, c_f, c_f, c_p, c_i32, ctypes.c_uint32,
                               c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_rpn_targets_workspace_bytes": [c_i64, c_i64, c_i64],
+    "m3d_rpn_targets": [c_p, c_i64, c_p, c_i64, c_f, c_f, c_i32, c_f, c_i32, c_i32, c_p, ctypes.c_uint32, c_p,
+                        c_p, c_i64, c_p, c_sz, c_p, c_p],
     "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
@@ -89,7 +92,7 @@ _SIGS = {
     "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
-             "m3d_detection_targets_workspace_bytes": c_sz,
+             "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_conv3d_wino_workspace_bytes": c_sz}
 
 EXPORTED = tuple(_SIGS)

@@ -14,6 +14,8 @@ order (``seed`` advances per call), so runs are reproducible.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -87,3 +89,43 @@ class DetectionTargetLayer:
     def compute_output_shape(self, input_shape):
         return [(None, self.T, 6), (None, self.T, 6), (None, self.T), (None, self.T, 6),
                 (None, self.T) + self.mask_shape]
+
+
+def build_rpn_targets(anchors, gt_class_ids, gt_boxes, config, seed=0, list_cap=None):
+    """build_rpn_targets(anchors, gt_class_ids, gt_boxes, config)
+    (core/data_generators.py:2031-2178) on the GPU.
+
+    anchors: device tensor [A,6], normalised (RPN.get_anchors); gt_boxes: [G,6]
+    pixel or normalised (the reference's auto-detection: GT with max > 2 are
+    divided by (H,W,D,H,W,D) and clipped to [0,1]).  Returns (rpn_match [A]
+    int32, rpn_bbox [RPN_TRAIN_ANCHORS_PER_IMAGE, 6] float32), device tensors.
+    The dropped negatives are a seeded random subset (np.random.choice in the
+    reference)."""
+    L = _lib.load()
+    ops._dev(anchors)
+    dev = anchors.device
+    A = anchors.shape[0]
+    total = int(getattr(config, "RPN_TRAIN_ANCHORS_PER_IMAGE", 2048))
+    gt = np.asarray(gt_boxes, np.float32).reshape(-1, 6)
+    G = gt.shape[0]
+    if G and float(np.max(np.abs(gt))) > 2.0:           # anchors are normalised: normalise the GT
+        H = int(getattr(config, "IMAGE_SIZE", config.IMAGE_SHAPE[0]))
+        W = int(getattr(config, "IMAGE_SIZE", config.IMAGE_SHAPE[1]))
+        D = int(getattr(config, "IMAGE_DEPTH", config.IMAGE_SHAPE[2]))
+        gt = np.clip(gt / np.array([H, W, D, H, W, D], np.float32), 0.0, 1.0).astype(np.float32)
+    gtd = torch.from_numpy(np.ascontiguousarray(gt)).to(dev)
+    match8 = torch.empty((A,), device=dev, dtype=torch.int8)
+    bbox = torch.empty((total, 6), device=dev, dtype=torch.float32)
+    cap = int(list_cap or min(A, 1 << 20))
+    wsb = int(L.m3d_rpn_targets_workspace_bytes(A, G, cap))
+    ws = torch.empty(max(wsb, 1), device=dev, dtype=torch.uint8)
+    sd = (_lib.c_f * 6)(*[float(np.float32(v)) for v in config.RPN_BBOX_STD_DEV])
+    cnt = (ctypes.c_int32 * 2)()
+    check(L.m3d_rpn_targets(ptr(anchors.contiguous()), A, ptr(gtd), G,
+                            float(getattr(config, "RPN_POSITIVE_IOU", 0.15)),
+                            float(getattr(config, "RPN_NEGATIVE_IOU", 0.05)), total,
+                            float(getattr(config, "RPN_POSITIVE_RATIO", 0.5)),
+                            int(getattr(config, "ATSS_TOPK", 24)), int(getattr(config, "ATSS_MIN_POS_PER_GT", 4)),
+                            sd, int(seed) & 0xFFFFFFFF, ptr(match8), ptr(bbox), cap, ptr(ws), wsb, cnt,
+                            stream()), "rpn_targets")
+    return match8.to(torch.int32), bbox

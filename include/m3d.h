@@ -287,6 +287,24 @@ int m3d_detection_targets(const float* proposals, int64_t N, const int32_t* gt_c
                           int32_t* mask_assign, int32_t* counts, void* workspace, size_t ws_bytes,
                           m3d_stream_t s);
 
+/* build_rpn_targets (ATSS, core/data_generators.py:2031-2178) for one volume
+ * on the device-resident anchors [A,6] (normalised) and GT boxes [G,6]
+ * (normalised, G <= 256): rpn_match [A] int8 (1 / -1 / 0) and rpn_bbox
+ * [total,6] (deltas of the positives in anchor order / RPN_BBOX_STD_DEV).
+ * Per-GT top-k / ATSS threshold without an [A x G] matrix (per-GT lists of
+ * the anchors with IoU > 0, capacity list_cap each); ties where the reference
+ * is implementation-defined go to the larger IoU, then the smaller anchor
+ * index; np.random.choice of the dropped negatives -> a seeded random subset.
+ * Synchronises the stream (the balancing needs the label counts on the host),
+ * counts_out[2] = final (positives, negatives) if non-NULL.
+ * workspace: m3d_rpn_targets_workspace_bytes(A, G, list_cap). */
+size_t m3d_rpn_targets_workspace_bytes(int64_t A, int64_t G, int64_t list_cap);
+int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
+                    float pos_iou, float neg_iou, int32_t total, float positive_ratio,
+                    int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
+                    uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
+                    void* workspace, size_t ws_bytes, int32_t* counts_out, m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
  * ------------------------------------------------------------------------- */

@@ -215,3 +215,88 @@ def detection_targets(proposals, gt_class_ids, gt_boxes, T, ratio, pos_thr, neg_
             out[4][:pc] = P[sel_p]
         out[5][:pc] = g
     return out
+
+
+# ---------------------------------------------------------------------------
+# build_rpn_targets (core/data_generators.py:2031-2178)
+# ---------------------------------------------------------------------------
+def compute_overlaps_3d(b1, b2):
+    """core/utils.py:78-143, float32."""
+    f = np.float32
+    b1 = np.asarray(b1, f)
+    b2 = np.asarray(b2, f)
+
+    def norm(b):
+        out = b.copy()
+        out[:, :3] = np.minimum(b[:, :3], b[:, 3:])
+        out[:, 3:] = np.maximum(b[:, :3], b[:, 3:])
+        return out
+    b1, b2 = norm(b1), norm(b2)
+    e1, e2 = b1[:, None], b2[None]
+    h = np.maximum(np.minimum(e1[..., 3], e2[..., 3]) - np.maximum(e1[..., 0], e2[..., 0]), f(0))
+    w = np.maximum(np.minimum(e1[..., 4], e2[..., 4]) - np.maximum(e1[..., 1], e2[..., 1]), f(0))
+    d = np.maximum(np.minimum(e1[..., 5], e2[..., 5]) - np.maximum(e1[..., 2], e2[..., 2]), f(0))
+    inter = h * w * d
+    v1 = ((b1[:, 3] - b1[:, 0]) * (b1[:, 4] - b1[:, 1]) * (b1[:, 5] - b1[:, 2]))[:, None]
+    v2 = ((b2[:, 3] - b2[:, 0]) * (b2[:, 4] - b2[:, 1]) * (b2[:, 5] - b2[:, 2]))[None]
+    union = np.maximum(v1 + v2 - inter, f(1e-10))
+    return np.clip(inter / union, f(0), f(1)).astype(f)
+
+
+def neg_keys(idx, seed):
+    """The seeded order that picks the kept negatives (replaces np.random.choice)."""
+    return [(int(_mix32((int(i) * 0x9E3779B9 & 0xFFFFFFFF) ^ seed)), -int(i)) for i in idx]
+
+
+def build_rpn_targets(anchors, gt_boxes_norm, pos_iou, neg_iou, total, ratio, atss_topk, atss_min_pos, std,
+                      seed):
+    """Restatement of the reference with its implementation-defined orders fixed:
+    top-k / ties by (IoU desc, index asc); kept negatives = the target_neg
+    smallest seeded keys.  anchors [A,6], gt [G,6] normalised."""
+    f = np.float32
+    A, G = len(anchors), len(gt_boxes_norm)
+    match = np.zeros(A, np.int32)
+    bbox = np.zeros((total, 6), f)
+    if G == 0:
+        match[:] = -1
+        return match, bbox
+    ov = compute_overlaps_3d(anchors, gt_boxes_norm)
+    iou_max = ov.max(1)
+    match[ov.argmax(0)] = 1
+    match[iou_max < f(neg_iou)] = -1
+    match[iou_max >= f(pos_iou)] = 1
+    for g in range(G):
+        ious = ov[:, g]
+        if not np.any(ious > 0):
+            continue
+        k = min(atss_topk, A)
+        order = np.lexsort((np.arange(A), -ious))[:k]      # IoU desc, index asc
+        vals = ious[order].astype(np.float64)
+        mu = float(np.float32(vals.mean()))
+        sd = float(np.float32(vals.std()))
+        thr = np.float32(max(pos_iou, mu + sd))
+        cand = np.nonzero(ious >= thr)[0]
+        if cand.size < atss_min_pos:
+            cand = order[:atss_min_pos]
+        match[cand] = 1
+    target_pos = int(round(total * ratio))
+    pos = np.nonzero(match == 1)[0]
+    if pos.size > target_pos:
+        keep = pos[np.lexsort((pos, -iou_max[pos]))][:target_pos]
+        drop = np.setdiff1d(pos, keep)
+        match[drop] = 0
+    neg = np.nonzero(match == -1)[0]
+    target_neg = int(min(len(neg), total - int(np.sum(match == 1))))
+    if len(neg) > target_neg:
+        keys = neg_keys(neg, seed)
+        kept = set(int(neg[j]) for j in sorted(range(len(neg)), key=lambda j: keys[j])[:max(target_neg, 0)])
+        match[[i for i in neg if int(i) not in kept]] = 0
+    pos = np.nonzero(match == 1)[0]
+    if pos.size:
+        g = ov[pos].argmax(1)
+        a = np.asarray(anchors, f)[pos]
+        gb = np.asarray(gt_boxes_norm, f)[g]
+        d = box_refinement(a, gb) / np.asarray(std, f)
+        n = min(len(d), total)
+        bbox[:n] = d[:n]
+    return match, bbox

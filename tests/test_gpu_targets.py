@@ -65,3 +65,25 @@ def test_detection_targets_empty_gt(cuda):
                   (props, np.zeros(3, np.int32), np.zeros((3, 6), np.float32), np.zeros((8, 8, 8, 3), bool))])
     for o in outs:
         assert float(o.abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("S,D,G,topk,minpos", [(64, 16, 6, 24, 4), (64, 32, 12, 64, 20), (64, 16, 1, 24, 4)])
+def test_build_rpn_targets(cuda, S, D, G, topk, minpos):
+    """ATSS RPN targets on the GPU vs the numpy restatement (same tie rules and
+    seeded negative subset): rpn_match identical, rpn_bbox to log rounding."""
+    from m3d.anchors import get_anchors
+    from m3d.config import synthetic_rpn_config
+    from m3d.targets import build_rpn_targets
+    cfg = synthetic_rpn_config(S, depth=D, RPN_POSITIVE_IOU=0.3, RPN_NEGATIVE_IOU=0.1,
+                               RPN_TRAIN_ANCHORS_PER_IMAGE=512, ATSS_TOPK=topk, ATSS_MIN_POS_PER_GT=minpos)
+    anchors = get_anchors(cfg)
+    rng = np.random.default_rng(S + G)
+    lo = rng.uniform(0, [S - 24, S - 24, D - 6], (G, 3))
+    gt_px = np.concatenate([lo, lo + rng.uniform([8, 8, 2], [24, 24, 6], (G, 3))], 1).astype(np.float32)
+    m, b = build_rpn_targets(torch.from_numpy(anchors).to(cuda), np.ones(G, np.int32), gt_px, cfg, seed=9)
+    gt_n = np.clip(gt_px / np.array([S, S, D, S, S, D], np.float32), 0, 1).astype(np.float32)
+    rm, rb = HR.build_rpn_targets(anchors, gt_n, 0.3, 0.1, 512, 0.5, topk, minpos, cfg.RPN_BBOX_STD_DEV, 9)
+    m = m.cpu().numpy()
+    assert np.array_equal(m, rm), (np.sum(m != rm), np.sum(m == 1), np.sum(rm == 1))
+    assert (m == 1).sum() > 0 and (m == -1).sum() > 0
+    np.testing.assert_allclose(b.cpu().numpy(), rb, rtol=1e-5, atol=1e-5)
