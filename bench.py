@@ -172,11 +172,18 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14), hi=128):
         e1.record()
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / reps / 1e3
-        u = unique_voxels(boxes.cpu().numpy(), fshapes, (p, p, p), S)
+        bnp = boxes.cpu().numpy()
+        u = unique_voxels(bnp, fshapes, (p, p, p), S)
         alg = 4.0 * n_rois * p ** 3 * C + 4.0 * C * u
+        # per-ROI bound: sum over ROIs of each ROI's own unique voxels (what any
+        # kernel that does not share rows between different ROIs must read)
+        u_roi = sum(unique_voxels(bnp[:, i:i + 1], fshapes, (p, p, p), S) for i in range(n_rois))
+        per_roi = 4.0 * n_rois * p ** 3 * C + 4.0 * C * u_roi
         res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "algorithmic_bytes": alg,
                            "gather_bytes": 8 * 4.0 * n_rois * p ** 3 * C,
                            "GBps": round(alg / t / 1e9, 1), "frac_hbm": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                           "per_roi_bytes": per_roi,
+                           "frac_hbm_per_roi": round(per_roi / t / 1e9 / HBM_PEAK_GBS, 4),
                            "traffic": _pmc_traffic(f"pyramid_fwd_pool{p}_S{S}_N{n_rois}")}
     return res
 
