@@ -16,6 +16,19 @@ from . import _lib, slab
 from ._lib import check, ptr, stream
 
 
+# Per-layer work records for the roofline accounting of bench.py: when set to
+# a list, every conv / pool / subsample forward appends
+# (kind, direct_flops, executed_flops, compulsory_bytes).  executed_flops is
+# the MFMA work of the algorithm actually run (the 64 batched GEMMs for a
+# Winograd layer); compulsory bytes = input + weights + residual + output.
+LAYER_LOG = None
+
+
+def _log(kind, direct_flops, exec_flops, nbytes):
+    if LAYER_LOG is not None:
+        LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes)))
+
+
 def _L():
     return _lib.load()
 
@@ -122,6 +135,14 @@ class _ConvBNAct(torch.autograd.Function):
                                       *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
                                       ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
                                       None, 0, 0, stream()), "conv3d_fwd")
+        if LAYER_LOG is not None:
+            direct = 2.0 * (y.numel() // Cout) * kh * kw * kd * Cin * Cout
+            exe = direct
+            if ctx.wino:
+                tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // 2)
+                exe = 2.0 * 64 * tiles * Cin * Cout
+            nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
+            _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
         ctx.save_for_backward(x, w, y, z)
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -234,6 +255,7 @@ class _MaxPool(torch.autograd.Function):
         am = torch.empty((B, *out, C), device=x.device, dtype=torch.uint8)
         check(_L().m3d_maxpool3d_fwd(ptr(x), B, H, W, D, C, *k, *stride, *pad, *out, ptr(y), ptr(am),
                                      stream()), "maxpool3d_fwd")
+        _log("maxpool", 0, 0, 4.0 * (x.numel() + y.numel()))
         ctx.save_for_backward(am)
         ctx.cfg = (tuple(x.shape), k, stride, pad, out)
         return y
@@ -268,6 +290,7 @@ class _Subsample221(torch.autograd.Function):
         B, H, W, D, C = x.shape
         y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, D, C), device=x.device, dtype=torch.float32)
         check(_L().m3d_subsample221_fwd(ptr(x), B, H, W, D, C, ptr(y), stream()), "subsample221")
+        _log("subsample", 0, 0, 4.0 * (x.numel() + y.numel()))
         ctx.shape = tuple(x.shape)
         return y
 
@@ -310,6 +333,9 @@ class _RPNOut(torch.autograd.Function):
                                        bbox[b].data_ptr() + off * apl * 6 * 4, 6 * apl, 2 * apl,
                                        stream()), "rpn_out_fwd")
                 off += r
+        if LAYER_LOG is not None:
+            f = 2.0 * B * sum(rows) * Cin * 8 * apl
+            _log("conv1", f, f, 4.0 * (sum(s.numel() for s in shared) + w24.numel() + logits.numel() + bbox.numel()))
         ctx.save_for_backward(w24, *shared)
         ctx.grads, ctx.rows, ctx.apl = grads, rows, apl
         return logits, bbox

@@ -231,6 +231,50 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     return out
 
 
+# ---------------------------------------------------------------- forward roofline
+def fwd_roofline(model, image, reps=3):
+    """Per-stage forward roofline: every conv / pool of the
+    backbone, FPN and RPN head is logged once (m3d.nn.LAYER_LOG) with its
+    direct-conv FLOPs, the MFMA FLOPs the chosen algorithm executes (Winograd
+    GEMMs for the 3^3 layers) and its compulsory HBM bytes (in + w + residual
+    + out).  t_roof = sum_l max(F_exec_l / P_mfma, B_l / P_hbm); frac =
+    t_roof / t_measured (HIP events, no_grad forward of that stage).  The SURVEY
+    form with direct FLOPs is reported too (it exceeds 1 where Winograd beats
+    the direct-conv bound)."""
+    from m3d import nn as mnn
+    stages = {}
+
+    def run(name, fn):
+        mnn.LAYER_LOG = []
+        with torch.no_grad():
+            r = fn()
+        torch.cuda.synchronize()
+        rec, mnn.LAYER_LOG = mnn.LAYER_LOG, None
+        with torch.no_grad():
+            t = _event_time(fn, reps)
+        t_exec = sum(max(fe / (F32_MFMA_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9)) for _, _, fe, b in rec)
+        t_dir = sum(max(fd / (F32_MFMA_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9)) for _, fd, _, b in rec)
+        nb = sum(b for *_, b in rec)
+        stages[name] = {"ms": round(t * 1e3, 3), "layers": len(rec),
+                        "direct_tflop": round(sum(r_[1] for r_ in rec) / 1e12, 4),
+                        "executed_tflop": round(sum(r_[2] for r_ in rec) / 1e12, 4),
+                        "compulsory_gb": round(nb / 1e9, 3),
+                        "roofline_ms": round(t_exec * 1e3, 3), "frac_roofline": round(t_exec / t, 4),
+                        "frac_roofline_direct_flops": round(t_dir / t, 4),
+                        "hbm_frac": round(nb / t / (HBM_PEAK_GBS * 1e9), 4)}
+        return r
+
+    _, C2, C3, C4, C5 = run("backbone", lambda: model.backbone(image))
+    fm = run("fpn", lambda: model.fpn(C2, C3, C4, C5))
+    run("rpn_head", lambda: model.rpn(fm)[:2])
+    tot_ms = sum(v["ms"] for v in stages.values())
+    roof = sum(v["roofline_ms"] for v in stages.values())
+    stages["total"] = {"ms": round(tot_ms, 3), "roofline_ms": round(roof, 3),
+                       "frac_roofline": round(roof / tot_ms, 4),
+                       "compulsory_gb": round(sum(v["compulsory_gb"] for v in stages.values()), 3)}
+    return stages
+
+
 def roi_leg_large(S, dev, n_rois=512):
     """configs[3] shapes: PyramidROIAlign 7^3 and 14^3 of 512 proposals on the
     P2..P5 maps of a frozen S^3 forward (boxes log-uniform in [24, S] px, so
@@ -238,11 +282,18 @@ def roi_leg_large(S, dev, n_rois=512):
     from m3d.config import synthetic_rpn_config
     from m3d.model import RPN, synthetic_volume
     model = RPN(synthetic_rpn_config(S), device=dev, seed=1)
+    image = synthetic_volume(S).to(dev)
     with torch.no_grad():
-        fmaps = model.features(synthetic_volume(S).to(dev))
+        fmaps = model.features(image)
     r = time_roi_align(fmaps, S, n_rois=n_rois, hi=S)
     r["config"] = f"{n_rois} ROIs on P2..P5 of a {S}^3 volume, C=256"
-    del model, fmaps
+    del fmaps
+    torch.cuda.empty_cache()
+    try:
+        r["fwd_roofline"] = fwd_roofline(model, image)
+    except Exception as e:  # report, never hide
+        r["fwd_roofline"] = {"error": repr(e)}
+    del model, image
     return r
 
 
@@ -394,6 +445,10 @@ def main():
         except Exception as e:
             out["roi_align"] = {"error": repr(e)}
         del fmaps
+        try:
+            out["fwd_roofline"] = fwd_roofline(model, image)
+        except Exception as e:
+            out["fwd_roofline"] = {"error": repr(e)}
         torch.cuda.empty_cache()
         if args.roi_size:
             try:
