@@ -258,6 +258,16 @@ class MaskRCNN:
                                         int(c.DETECTION_MAX_INSTANCES), float(c.DETECTION_NMS_THRESHOLD),
                                         int(c.IMAGES_PER_GPU), name="mrcnn_detection")
 
+    def load_weights(self, filepath, by_name=True, skip_mismatch=False, exclude=()):
+        """keras_model.load_weights(filepath, by_name=True, ...) on the Keras-H5 format (m3d.weights)."""
+        from .weights import load_weights
+        return load_weights(self.store, filepath, by_name=by_name, skip_mismatch=skip_mismatch, exclude=exclude)
+
+    def save_weights(self, filepath):
+        """keras_model.save_weights(filepath): Keras-H5 layout, readable by the reference."""
+        from .weights import save_weights
+        save_weights(self.store, filepath)
+
     @torch.no_grad()
     def detect(self, image, image_meta):
         _, C2, C3, C4, C5 = self.backbone(image)

@@ -171,6 +171,16 @@ class RPN:
         return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
                 "rpn_rois": out["rpn_rois"]}
 
+    def load_weights(self, filepath, by_name=True, skip_mismatch=False, exclude=()):
+        """keras_model.load_weights(filepath, by_name=True, ...) on the Keras-H5 format (m3d.weights)."""
+        from .weights import load_weights
+        return load_weights(self.store, filepath, by_name=by_name, skip_mismatch=skip_mismatch, exclude=exclude)
+
+    def save_weights(self, filepath):
+        """keras_model.save_weights(filepath): Keras-H5 layout, readable by the reference."""
+        from .weights import save_weights
+        save_weights(self.store, filepath)
+
     def sgd_step(self):
         s = self.store
         L = _lib.load()
