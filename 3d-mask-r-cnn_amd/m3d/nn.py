@@ -24,6 +24,20 @@ from ._lib import check, ptr, stream
 LAYER_LOG = None
 
 
+# Gradient-ready hook of the data-parallel path (m3d.parallel.OverlappedAllReduce):
+# when set, every conv unit registers its gradient tensors in forward
+# (use(key, tensors)) and reports them final once its backward has enqueued
+# the weight/BN gradient kernels (done(key)), so finished buckets of the flat
+# gradient buffer are all-reduced while the rest of the backward runs.
+GRAD_HOOK = None
+
+
+def _grad_done(grads):
+    h = grads.get("_hook") if grads else None
+    if h is not None:
+        h[0].done(h[1])
+
+
 def _log(kind, direct_flops, exec_flops, nbytes):
     if LAYER_LOG is not None:
         LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes)))
@@ -188,6 +202,7 @@ class _ConvBNAct(torch.autograd.Function):
                 check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                  geo.pad[2], ptr(dx), 0, ptr(ws), wsb, stream()),
                       "conv3d_bwd_data_wino")
+            _grad_done(grads)
             return dx, (dres if need_res else None), None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
@@ -207,6 +222,7 @@ class _ConvBNAct(torch.autograd.Function):
             check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
                                         OD, *geo.stride, *geo.pad, ptr(dx), 0, stream()),
                   "conv3d_bwd_data")
+        _grad_done(grads)
         dr = None
         if need_res:
             if ctx.res_mode == 1:
@@ -236,6 +252,10 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     w = layer.kernel.data
     b = layer.bias.data if layer.bias is not None else None
     grads = layer.grad_dict(bn) if torch.is_grad_enabled() else None   # inference: no z / grads
+    if grads is not None and GRAD_HOOK is not None:
+        key = layer.name
+        GRAD_HOOK.use(key, [t for t in grads.values() if t is not None])
+        grads = dict(grads, _hook=(GRAD_HOOK, key))
     bnt = None
     if bn is not None:
         bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)

@@ -2,8 +2,9 @@
 
 One process per GPU.  Every rank runs the full RPN step on its own volume
 (weak scaling: per-GPU work is fixed as N grows) and the gradients, which
-live in ONE flat buffer (params.ParamStore.grad_flat), are averaged with a
-single bucketed all-reduce before the fused SGD kernel -- the reference's
+live in ONE flat buffer (params.ParamStore.grad_flat), are averaged with
+bucketed all-reduces that start during the backward as soon as a bucket's
+gradients are final (OverlappedAllReduce), before the fused SGD kernel -- the reference's
 equivalent is ParallelModel's in-graph tower replication
 (core/parallel_model.py:15-90).  Buckets are contiguous slices of the flat
 buffer, so no packing copies are needed.
@@ -41,15 +42,114 @@ def allreduce_mean_(flat: torch.Tensor, world: int, bucket=BUCKET_FLOATS):
     return flat
 
 
-def data_parallel_train_step(model, image, targets, world, proposals=True):
-    """model.train_step with the gradient average inserted before SGD."""
+class OverlappedAllReduce:
+    """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the
+    backward pass (the MI355X/RCCL counterpart of DDP's gradient buckets).
+
+    Buckets are contiguous slices of ``grad_flat`` (no packing copies).  In
+    forward every conv unit registers the gradient views it will write
+    (``use``, via m3d.nn.GRAD_HOOK); its backward reports them final
+    (``done``) right after enqueuing their kernels, and a bucket whose every
+    intersecting parameter is final is all-reduced at once with
+    ``async_op=True``: RCCL's stream waits for the compute stream at that
+    point and then runs concurrently with the rest of the backward.  The
+    backward finalises the flat buffer from its end (RPN head, FPN, stage 5,
+    ...) to its start (stem), so buckets launch tail-first.  Parameters that
+    no unit registers (the fused RPN class/bbox head, folded in by
+    finish_backward) keep their buckets until ``finish``, which launches the
+    rest, waits for all, and averages."""
+
+    def __init__(self, store, world, bucket=BUCKET_FLOATS):
+        self.store, self.world = store, world
+        flat = store.grad_flat
+        self.base = flat.data_ptr()
+        self.esize = flat.element_size()
+        n = flat.numel()
+        self.bounds = [(s, min(s + bucket, n)) for s in range(0, n, bucket)]
+        self.param_of = {}
+        self.param_buckets = []
+        for i, p in enumerate(store.params):
+            self.param_of[p.offset] = i
+            b0, b1 = p.offset // bucket, (p.offset + max(p.numel, 1) - 1) // bucket
+            self.param_buckets.append(list(range(b0, b1 + 1)))
+        self.bucket = bucket
+        self._pending0 = [0] * len(self.bounds)
+        for pb in self.param_buckets:
+            for b in pb:
+                self._pending0[b] += 1
+        self.reset()
+
+    def reset(self):
+        self.pending_params = list(self._pending0)
+        self.param_left = {}                  # param index -> outstanding uses
+        self.key_params = {}
+        self.key_uses = {}
+        self.finished = set()
+        self.launched = [None] * len(self.bounds)
+        self.order = []
+
+    def _param(self, t):
+        off = (t.data_ptr() - self.base) // self.esize
+        return self.param_of[off]
+
+    def use(self, key, tensors):
+        if key not in self.key_params:
+            self.key_params[key] = [self._param(t) for t in tensors]
+        self.key_uses[key] = self.key_uses.get(key, 0) + 1
+
+    def done(self, key):
+        self.key_uses[key] -= 1
+        if self.key_uses[key] > 0:
+            return
+        for pi in self.key_params[key]:
+            if pi in self.finished:
+                continue
+            self.finished.add(pi)
+            for b in self.param_buckets[pi]:
+                self.pending_params[b] -= 1
+                if self.pending_params[b] == 0:
+                    self._launch(b)
+
+    def _launch(self, b):
+        if self.launched[b] is None:
+            s, e = self.bounds[b]
+            self.launched[b] = dist.all_reduce(self.store.grad_flat[s:e], op=dist.ReduceOp.SUM,
+                                               async_op=True)
+            self.order.append(b)
+
+    def finish(self):
+        self.n_early = len(self.order)        # buckets launched during the backward
+        for b in range(len(self.bounds)):
+            self._launch(b)
+        for w in self.launched:
+            w.wait()
+        self.store.grad_flat.mul_(1.0 / self.world)
+
+
+def data_parallel_train_step(model, image, targets, world, proposals=True, overlap=True):
+    """model.train_step with the gradient average inserted before SGD; with
+    ``overlap`` the buckets are all-reduced during the backward."""
+    from . import nn as mnn
     model.store.zero_grad()
-    out = model.forward(image, proposals=proposals)
-    lc, lb = model.losses(out, targets)
-    total = lc * model.LOSS_WEIGHTS["rpn_class_loss"] + lb * model.LOSS_WEIGHTS["rpn_bbox_loss"]
-    total.backward()
+    hook = None
+    if world > 1 and overlap:
+        hook = getattr(model, "_dp_hook", None)
+        if hook is None or hook.world != world:
+            hook = model._dp_hook = OverlappedAllReduce(model.store, world)
+        hook.reset()
+        mnn.GRAD_HOOK = hook
+    try:
+        out = model.forward(image, proposals=proposals)
+        lc, lb = model.losses(out, targets)
+        total = lc * model.LOSS_WEIGHTS["rpn_class_loss"] + lb * model.LOSS_WEIGHTS["rpn_bbox_loss"]
+        total.backward()
+    finally:
+        mnn.GRAD_HOOK = None
     model.rpn.finish_backward()
-    allreduce_mean_(model.store.grad_flat, world)
+    if hook is not None:
+        hook.finish()
+    else:
+        allreduce_mean_(model.store.grad_flat, world)
     model.sgd_step()
     return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
             "rpn_rois": out["rpn_rois"]}
