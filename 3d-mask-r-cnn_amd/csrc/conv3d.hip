@@ -47,6 +47,7 @@ struct ConvP {
     // advance by these element strides (0 for ordinary convs)
     int64_t bsa, bsw, bsy;
     int dly = 1, dlx = 1, dlz = 1;   // dilation (fwd only; mrcnn_mask_conv3b)
+    int nbatch = 1;                  // batches (PERSIST: looped inside the grid)
 };
 
 struct Epi {
@@ -198,7 +199,7 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF>
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false>
 __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_gemm_kernel(ConvP p, Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
@@ -228,21 +229,35 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     // workgroups round-robin to the 8 XCDs; remap so each XCD owns a contiguous
     // run of tiles, N-tiles of one M-tile adjacent, so the im2col rows (and
     // their 3x3x3 halo) are re-read from that XCD's L2, not from HBM.
-    int64_t m0;
-    int n0;
-    {
-        const int64_t nbx = gridDim.x, nby = gridDim.y, total = nbx * nby;
-        const int64_t L = (int64_t)blockIdx.x + nbx * blockIdx.y;
-        const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
-        const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
-        m0 = (T / nby) * BM;
-        n0 = (int)(T % nby) * BN;
-    }
-    if (blockIdx.z) {
-        p.a += blockIdx.z * p.bsa;
-        p.w += blockIdx.z * p.bsw;
-        e.y += blockIdx.z * p.bsy;
-    }
+    // PERSIST: a grid of ~one wave of workgroups loops over all tiles (all
+    // batches), issuing the next tile's first k-tile loads before the current
+    // tile's epilogue, so short-K GEMMs (the Winograd point GEMMs, K = Cin)
+    // do not pay a cold prologue per tile.  gridDim.x is a multiple of 8, so a
+    // workgroup stays on its XCD and walks that XCD's contiguous tile range.
+    static_assert(!PERSIST || AVEC, "persistent mode uses the vector A loader");
+    const int64_t nbx = (p.M + BM - 1) / BM, nby = (p.N + BN - 1) / BN;
+    const int64_t per_batch = nbx * nby;
+    const int64_t total = PERSIST ? per_batch * (int64_t)p.nbatch : (int64_t)gridDim.x * gridDim.y;
+    int64_t L = PERSIST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+    const int64_t Lstep = PERSIST ? (int64_t)gridDim.x : total;
+    if (L >= total) return;
+    const float* const a_base = p.a;
+    const float* const w_base = p.w;
+    float* const y_base = e.y;
+    int64_t m0 = 0;
+    int n0 = 0;
+    auto map_tile = [&](int64_t Lt) {
+        const int64_t xcd = Lt % 8, q8 = total / 8, r8 = total % 8;
+        const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lt / 8;
+        const int64_t bz = PERSIST ? T / per_batch : (int64_t)blockIdx.z;
+        const int64_t Tt = PERSIST ? T - bz * per_batch : T;
+        m0 = (Tt / nby) * BM;
+        n0 = (int)(Tt % nby) * BN;
+        p.a = a_base + bz * p.bsa;
+        p.w = w_base + bz * p.bsw;
+        e.y = y_base + bz * p.bsy;
+    };
+    map_tile(L);
     const int taps_kd = p.kd, taps_kwkd = p.kw * p.kd;
     const int ntaps = p.kh * taps_kwkd;
 
@@ -252,22 +267,25 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     bool a_ok[AVEC ? AQ : 1];
     const int a_col4 = tid % KC4;
     const int rowW = p.D * p.C, rowH = p.W * rowW;
-    if (AVEC) {
+    __amdgpu_buffer_rsrc_t rsA, rsB;
+    auto setup_rows = [&]() {
+        if (AVEC) {
 #pragma unroll
-        for (int q = 0; q < AQ; ++q) {
-            const int64_t m = m0 + tid / KC4 + RPP * q;
-            a_ok[q] = m < p.M;
-            int b, oy, ox, oz;
-            decompose(a_ok[q] ? m : 0, p.OH, p.OW, p.OD, b, oy, ox, oz);
-            a_y[q] = oy * p.sy - p.py;
-            a_x[q] = ox * p.sx - p.px;
-            a_z[q] = oz * p.sz - p.pz;
-            a_off[q] = ((b * p.H + a_y[q]) * p.W + a_x[q]) * rowW + a_z[q] * p.C + a_col4 * 4;
+            for (int q = 0; q < AQ; ++q) {
+                const int64_t m = m0 + tid / KC4 + RPP * q;
+                a_ok[q] = m < p.M;
+                int b, oy, ox, oz;
+                decompose(a_ok[q] ? m : 0, p.OH, p.OW, p.OD, b, oy, ox, oz);
+                a_y[q] = oy * p.sy - p.py;
+                a_x[q] = ox * p.sx - p.px;
+                a_z[q] = oz * p.sz - p.pz;
+                a_off[q] = ((b * p.H + a_y[q]) * p.W + a_x[q]) * rowW + a_z[q] * p.C + a_col4 * 4;
+            }
         }
-    }
-    const __amdgpu_buffer_rsrc_t rsA =
-        make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
-    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.w, (uint64_t)p.K * p.N * 4);
+        rsA = make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
+        rsB = make_rsrc(p.w, (uint64_t)p.K * p.N * 4);
+    };
+    setup_rows();
 
     float4 ra[AVEC ? AQ : 1];
     float rs[AVEC ? 1 : AQ];
@@ -360,6 +378,12 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
         }
     };
 
+    const int nk = (p.K + BK - 1) / BK;
+    const int h = lane >> 5, l32 = lane & 31;
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    while (true) {
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -368,11 +392,6 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-    const int nk = (p.K + BK - 1) / BK;
-    const int h = lane >> 5, l32 = lane & 31;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = NBUF == 2 ? (kt & 1) : 0;
         if (kt + 1 < nk) load_tile(kt + 1);
@@ -431,6 +450,13 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     // write rows 4 apart = 32 banks apart, conflict-free) and leaves as
     // row-contiguous float4s: 16-byte stores and one epilogue evaluation per
     // 4 channels instead of per element.  (The k-loop ended on a barrier.)
+    // PERSIST: once the accumulators are staged in LDS (acc dead), map the
+    // next tile and put its first k-tile loads in flight behind this tile's
+    // global epilogue stores.
+    const int64_t m0c = m0;
+    const int n0c = n0;
+    const int64_t Ln = L + Lstep;
+    const bool more = PERSIST && Ln < total;
     constexpr int LDT = BN + 8;
     constexpr int HALVES = (BM * LDT <= NBUF * (A_SZ + B_SZ)) ? 1 : 2;   // staged in row halves
     constexpr int HR = BM / HALVES;
@@ -451,16 +477,37 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                            wn * TN * 32 + j * 32 + l32] = acc[i][j][r];
         }
         __syncthreads();
+        float* y_next = e.y;
+        if (PERSIST && more && hf == HALVES - 1) {
+            float* const yc = e.y;
+            map_tile(Ln);                        // sets p.a/p.w/e.y, m0/n0 of the next tile
+            y_next = e.y;
+            e.y = yc;
+            setup_rows();
+            load_tile(0);
+        }
 #pragma unroll
         for (int q = 0; q < (HR * C4T + 255) / 256; ++q) {
             const int idx = tid + 256 * q;
             if (HR * C4T % 256 && idx >= HR * C4T) break;
             const int row = idx / C4T, c4 = idx % C4T;
-            const int64_t m = m0 + hf * HR + row;
-            const int n = n0 + c4 * 4;
-            if (m < p.M && n < p.N)
-                epi_store4(p, e, m, n, *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4));
+            const int64_t m = m0c + hf * HR + row;
+            const int n = n0c + c4 * 4;
+            if (m < p.M && n < p.N) {
+                const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
+                if (PERSIST)   // plain C store (host-checked: simple epilogue, nothing fused)
+                    st4(e.y + m * e.ldy + n, v);
+                else
+                    epi_store4(p, e, m, n, v);
+            }
         }
+        e.y = y_next;
+    }
+    if (!more) break;
+    L = Ln;
+    __syncthreads();                             // staged tile fully read
+    store_tile(0);
+    __syncthreads();
     }
 }
 
@@ -635,10 +682,43 @@ static int gemm_nbuf_env() {
     return v;
 }
 
+// M3D_GEMM_PERSIST=0 disables the persistent tile loop of the batched
+// (Winograd) GEMMs (A/B testing; default on).
+static int gemm_persist_env() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
+    return v;
+}
+static int num_cus() {
+    static int v = [] {
+        int dev = 0, n = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    return v;
+}
+
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
 static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
     dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
     if constexpr (BK == 32 && AVEC) {      // (the scalar-A loader spills at 3 blocks/CU)
+        const int64_t tiles = (int64_t)grid.x * grid.y * nbatch;
+        const int64_t resident = (int64_t)num_cus() * (gemm_nbuf_env() == 1 ? 3 : 2);
+        const bool plain = e.simple && !e.bias && !e.scale && !e.res_mode && !e.relu && !e.z && !e.split &&
+                           !e.accumulate && !e.deconv && (e.ldy & 3) == 0;
+        if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
+            ConvP pp = p;
+            pp.nbatch = nbatch;
+            const unsigned g = (unsigned)(resident / 8 * 8);
+            if (gemm_nbuf_env() == 1)
+                hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, true>), dim3(g), dim3(256),
+                                   0, s, pp, e);
+            else
+                hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 2, true>), dim3(g), dim3(256),
+                                   0, s, pp, e);
+            return;
+        }
         if (gemm_nbuf_env() == 1) {
             hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1>), grid, dim3(256), 0, s, p, e);
             return;
