@@ -188,6 +188,67 @@ def time_roi_align(fmaps, S, n_rois=128, reps=10, pools=(7, 14), hi=128):
     return res
 
 
+def time_roi_align_bwd(fmaps, S, n_rois=128, reps=5, pools=(7, 14), hi=128):
+    """CropAndResize3DGradImage through PyramidROIAlign's backward (SURVEY.md 8d:
+    HBM / atomics): bytes = 4|grads| (read) + 32|grads| (8 corner atomic RMW)
+    + 4|P2..P5| (zero fill of the image gradients)."""
+    from m3d import _lib, ops
+    L = _lib.load()
+    maps = [f.detach().contiguous() for f in fmaps[:4]]
+    C = maps[0].shape[-1]
+    boxes = torch.from_numpy(roi_boxes(n_rois, S, hi=hi)).to(maps[0].device)
+    meta = torch.zeros((1, 18), device=maps[0].device)
+    meta[0, 5:8] = S
+    gm = [torch.empty_like(m) for m in maps]
+    gptrs = (_lib.c_p * 4)(*[g.data_ptr() for g in gm])
+    fshape = ((_lib.c_i64 * 3) * 4)(*[(_lib.c_i64 * 3)(*m.shape[1:4]) for m in maps])
+    img = sum(m.numel() for m in maps)
+    res = {}
+    for p in pools:
+        _, badj, lev = ops.pyramid_roi_align(boxes, meta, maps, (p, p, p), return_levels=True)
+        grad = torch.randn((1, n_rois, p, p, p, C), device=maps[0].device)
+
+        def launch():
+            _lib.check(L.m3d_pyramid_roi_align3d_bwd(grad.data_ptr(), badj.data_ptr(), lev.data_ptr(), 1, n_rois,
+                                                     p, p, p, gptrs, fshape, C, _lib.stream()), "roi bwd")
+        t = _event_time(launch, reps)
+        nb = 4.0 * grad.numel() * (1 + 8) + 4.0 * img
+        res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "bytes": nb, "GBps": round(nb / t / 1e9, 1),
+                           "frac_hbm": round(nb / t / 1e9 / HBM_PEAK_GBS, 4)}
+    return res
+
+
+def time_nms(dev, k=15000, max_out=6000, thr=0.7, reps=5, seed=4):
+    """NonMaxSuppression3D at the ProposalLayer's training shape (k = PRE_NMS_LIMIT
+    boxes -> POST_NMS_ROIS_TRAINING): latency-bound, reported as ms and IoU
+    pairs/s (k(k-1)/2 pairs)."""
+    from m3d import ops
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(0.05, 0.95, (k, 3))
+    ext = np.exp(rng.uniform(np.log(0.02), np.log(0.3), (k, 3))) / 2
+    boxes = torch.from_numpy(np.concatenate([c - ext, c + ext], 1).astype(np.float32)).to(dev)
+    scores = torch.from_numpy(np.sort(rng.uniform(size=k))[::-1].astype(np.float32).copy()).to(dev)
+    keep, num = ops.non_max_suppression_3d_padded(boxes, scores, max_out, thr)
+    t = _event_time(lambda: ops.non_max_suppression_3d_padded(boxes, scores, max_out, thr), reps)
+    pairs = k * (k - 1) / 2
+    return {"k": k, "max_output_size": max_out, "iou_threshold": thr, "kept": int(num.item()),
+            "ms": round(t * 1e3, 4), "pairs_per_s": round(pairs / t, 1)}
+
+
+def time_allreduce(flat, world, reps=3):
+    """Bucketed gradient all-reduce alone (RCCL over xGMI): ms and bus bandwidth
+    2(n-1)/n * bytes / t."""
+    from m3d.parallel import allreduce_mean_
+    buf = flat.clone()
+    dist.barrier()
+    t = _event_time(lambda: allreduce_mean_(buf, world), reps)
+    nb = buf.numel() * buf.element_size()
+    t_max = torch.tensor([t], device=flat.device, dtype=torch.float64)
+    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    t = float(t_max.item())
+    return {"bytes": nb, "ms": round(t * 1e3, 3), "bus_GBps": round(2 * (world - 1) / world * nb / t / 1e9, 1)}
+
+
 # ---------------------------------------------------------------- depth-slab leg
 def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     """BASELINE configs[4]: ONE S^3 volume per step, split into depth slabs over
@@ -424,6 +485,13 @@ def main():
                                   f"{S}^3 x1 volume per GPU",
                       "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
                       "anchors": int(model.anchors.shape[1])}}
+    if world > 1 and not args.no_extras:
+        try:
+            ar = time_allreduce(model.store.grad_flat, world)
+        except Exception as e:  # report, never hide
+            ar = {"error": repr(e)}
+        if rank == 0:
+            out["allreduce"] = ar
     if args.slab_size and not args.no_extras:
         del r
         torch.cuda.empty_cache()
@@ -444,7 +512,15 @@ def main():
             out["roi_align"] = time_roi_align(fmaps, S)
         except Exception as e:
             out["roi_align"] = {"error": repr(e)}
+        try:
+            out["roi_align_bwd"] = time_roi_align_bwd(fmaps, S)
+        except Exception as e:
+            out["roi_align_bwd"] = {"error": repr(e)}
         del fmaps
+        try:
+            out["nms"] = time_nms(dev)
+        except Exception as e:
+            out["nms"] = {"error": repr(e)}
         try:
             out["fwd_roofline"] = fwd_roofline(model, image)
         except Exception as e:
