@@ -361,6 +361,33 @@ static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {
     if (gx < 1) gx = 1;
 }
 
+namespace m3d {
+// Frozen-BN affine of one layer in one launch: rstd = 1/sqrt(var + eps),
+// scale = gamma * rstd, shift = beta - mean * scale (BatchNorm inference,
+// core/models.py:102-114; replaces five elementwise launches per layer).
+__global__ void bn_affine_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 const float* __restrict__ mean, const float* __restrict__ var,
+                                 float eps, int C, float* __restrict__ scale,
+                                 float* __restrict__ shift, float* __restrict__ rstd) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float r = 1.0f / sqrtf(var[c] + eps);
+    const float sc = gamma[c] * r;
+    rstd[c] = r;
+    scale[c] = sc;
+    shift[c] = beta[c] - mean[c] * sc;
+}
+}  // namespace m3d
+
+extern "C" int m3d_bn_affine(const float* gamma, const float* beta, const float* mean,
+                             const float* var, float eps, int64_t C, float* scale, float* shift,
+                             float* rstd, m3d_stream_t s) {
+    if (C <= 0) return einval("bn_affine: C must be positive");
+    hipLaunchKernelGGL(bn_affine_kernel, dim3(grid_for(C, 256)), dim3(256), 0, st(s), gamma, beta,
+                       mean, var, eps, (int)C, scale, shift, rstd);
+    return check_launch("bn_affine_kernel");
+}
+
 extern "C" size_t m3d_bn_act_bwd_workspace_bytes(int64_t M, int64_t C) {
     int T, groups;
     int64_t gx;

@@ -86,6 +86,7 @@ _SIGS = {
     "m3d_upsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p],
     "m3d_subsample221_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_subsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "m3d_bn_affine": [c_p, c_p, c_p, c_p, c_f, c_i64, c_p, c_p, c_p, c_p],
     "m3d_bn_act_bwd_workspace_bytes": [c_i64, c_i64],
     "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
                        c_p, c_p, c_p, c_sz, c_p],

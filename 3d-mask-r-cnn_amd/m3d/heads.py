@@ -43,10 +43,11 @@ def _L():
 
 
 def _bn_affine(bn):
-    rstd = torch.rsqrt(bn.moving_variance + bn.eps)
-    scale = (bn.gamma.data * rstd).contiguous()
-    shift = (bn.beta.data - bn.moving_mean * scale).contiguous()
-    return scale, shift
+    aff = torch.empty((3, bn.c), device=bn.gamma.data.device, dtype=torch.float32)
+    check(_L().m3d_bn_affine(ptr(bn.gamma.data), ptr(bn.beta.data), ptr(bn.moving_mean),
+                             ptr(bn.moving_variance), float(bn.eps), bn.c, ptr(aff[1]), ptr(aff[2]),
+                             ptr(aff[0]), stream()), "bn_affine")
+    return aff[1], aff[2]
 
 
 class DenseLayer:

@@ -129,9 +129,10 @@ class _ConvBNAct(torch.autograd.Function):
         scale = shift = None
         if bn is not None:
             gamma, beta, mean, var, eps = bn
-            rstd = torch.rsqrt(var + eps)
-            scale = gamma * rstd
-            shift = beta - mean * scale
+            aff = torch.empty((3, Cout), device=x.device, dtype=torch.float32)
+            rstd, scale, shift = aff[0], aff[1], aff[2]
+            check(_L().m3d_bn_affine(ptr(gamma), ptr(beta), ptr(mean), ptr(var), float(eps), Cout,
+                                     ptr(scale), ptr(shift), ptr(rstd), stream()), "bn_affine")
             if grads is not None and grads.get("gamma") is not None:
                 z = torch.empty_like(y)
             ctx.bn = (mean, rstd, scale)

@@ -326,6 +326,11 @@ int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_
                          float* y, m3d_stream_t s);
 int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
                          float* dx, m3d_stream_t s);
+/* Frozen BatchNorm affine of one layer (core/models.py:102-114, inference
+ * mode): rstd = 1/sqrt(var+eps), scale = gamma*rstd, shift = beta - mean*scale. */
+int m3d_bn_affine(const float* gamma, const float* beta, const float* mean, const float* var,
+                  float eps, int64_t C, float* scale, float* shift, float* rstd, m3d_stream_t s);
+
 /* Backward of y = act(z*scale + shift [+ residual]) for frozen-statistics BN
  * (TRAIN_BN=False).  dpre = dy * (y > 0 if relu); dz = dpre*scale (or dpre;
  * dz may be NULL when not needed); dres = dpre (may be NULL; accumulate_res
