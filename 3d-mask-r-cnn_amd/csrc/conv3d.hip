@@ -1385,33 +1385,58 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout) {
     return w;
 }
 
-extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
-                                   int64_t Cin, const float* w, int64_t Cout, int64_t OD,
-                                   int32_t pz, const float* bias, const float* bn_scale,
-                                   const float* bn_shift, const float* residual, int32_t relu,
-                                   float* z_out, float* y, void* workspace, size_t ws_bytes,
-                                   m3d_stream_t s) {
+extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
+    return sizeof(float) * 64 * (size_t)(B * ((H + 1) / 2) * ((W + 1) / 2) * ((OD + 1) / 2)) * (size_t)Cin;
+}
+
+static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                    const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                    const float* bn_scale, const float* bn_shift, const float* residual,
+                    int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
+                    size_t ws_bytes, hipStream_t s) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
     const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
-    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+    if (u_keep) ws.U = u_keep;
+    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
                        (int)Cin, (int)Cout, 0, ws.V);
-    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
                        (int)Cin, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
     Epi e{};
     e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
-    dispatch_gemm<false, true>(p, e, st(s), 64);
+    dispatch_gemm<false, true>(p, e, s, 64);
     Epi o{};
     o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
     o.res_mode = residual ? 1 : 0; o.relu = relu; o.z = z_out; o.y = y; o.ldy = Cout;
-    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), ws.M,
+    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, s, ws.M,
                        g, (int)Cout, o);
     return check_launch("conv3d winograd fwd");
+}
+
+extern "C" int m3d_conv3d_fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                   int64_t Cin, const float* w, int64_t Cout, int64_t OD,
+                                   int32_t pz, const float* bias, const float* bn_scale,
+                                   const float* bn_shift, const float* residual, int32_t relu,
+                                   float* z_out, float* y, void* workspace, size_t ws_bytes,
+                                   m3d_stream_t s) {
+    return fwd_wino(x, B, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift, residual, relu,
+                    z_out, y, nullptr, workspace, ws_bytes, st(s));
+}
+
+extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
+                                        int64_t Cin, const float* w, int64_t Cout, int64_t OD,
+                                        int32_t pz, const float* bias, const float* bn_scale,
+                                        const float* bn_shift, const float* residual, int32_t relu,
+                                        float* z_out, float* y, float* u_keep, void* workspace,
+                                        size_t ws_bytes, m3d_stream_t s) {
+    if (!u_keep) return einval("conv3d winograd: u_keep must not be NULL");
+    return fwd_wino(x, B, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift, residual, relu,
+                    z_out, y, u_keep, workspace, ws_bytes, st(s));
 }
 
 // dx [B,H,W,D,Cin] = conv_transpose(dz [B,H,W,OD,Cout]): a 'same'-type 3x3x3
@@ -1444,10 +1469,9 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     return check_launch("conv3d winograd bwd-data");
 }
 
-extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H,
-                                          int64_t W, int64_t D, int64_t Cin, int64_t Cout,
-                                          int64_t OD, int32_t pz, float* dw, void* workspace,
-                                          size_t ws_bytes, m3d_stream_t s) {
+static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, int64_t B,
+                           int64_t H, int64_t W, int64_t D, int64_t Cin, int64_t Cout, int64_t OD,
+                           int32_t pz, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -1456,8 +1480,11 @@ extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);   // V <- dW_hat, U <- B^T x, M <- A dz
     if (hipMemsetAsync(ws.V, 0, sizeof(float) * 64 * (size_t)Cin * Cout, st(s)) != hipSuccess)
         return check_launch("memset dW_hat");
-    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
-                       (int)Cin, ws.U);
+    if (u_in)
+        ws.U = const_cast<float*>(u_in);       // the forward's transformed input, kept
+    else
+        hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
+                           (int)Cin, ws.U);
     hipLaunchKernelGGL(wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, nullptr, (int)Cout);
@@ -1468,4 +1495,19 @@ extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64
     hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s),
                        ws.V, (int)Cin, (int)Cout, dw);
     return check_launch("conv3d winograd bwd-weight");
+}
+
+extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H,
+                                          int64_t W, int64_t D, int64_t Cin, int64_t Cout,
+                                          int64_t OD, int32_t pz, float* dw, void* workspace,
+                                          size_t ws_bytes, m3d_stream_t s) {
+    return bwd_weight_wino(x, nullptr, dz, B, H, W, D, Cin, Cout, OD, pz, dw, workspace, ws_bytes, s);
+}
+
+extern "C" int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H,
+                                            int64_t W, int64_t D, int64_t Cin, int64_t Cout,
+                                            int64_t OD, int32_t pz, float* dw, void* workspace,
+                                            size_t ws_bytes, m3d_stream_t s) {
+    if (!u) return einval("conv3d winograd: u must not be NULL");
+    return bwd_weight_wino(nullptr, u, dz, B, H, W, D, Cin, Cout, OD, pz, dw, workspace, ws_bytes, s);
 }

@@ -139,12 +139,22 @@ class _ConvBNAct(torch.autograd.Function):
         else:
             ctx.bn = None
         ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
+        ctx.u = None
         if ctx.wino:
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
-            check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
-                                           ptr(b), ptr(scale),
-                                           ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
-                                           ptr(ws), wsb, stream()), "conv3d_fwd_wino")
+            if grads is not None and grads.get("kernel") is not None:
+                # training: keep the transformed input U for the weight gradient
+                nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4
+                ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32)
+                check(_L().m3d_conv3d_fwd_wino_keep(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
+                                                    ptr(b), ptr(scale), ptr(shift), ptr(residual),
+                                                    1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u),
+                                                    ptr(ws), wsb, stream()), "conv3d_fwd_wino_keep")
+            else:
+                check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
+                                               ptr(b), ptr(scale),
+                                               ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
+                                               ptr(ws), wsb, stream()), "conv3d_fwd_wino")
         else:
             check(_L().m3d_conv3d_fwd(ptr(x), B, H, W, D, Cin, ptr(w), kh, kw, kd, Cout, OH, OW, OD,
                                       *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
@@ -193,10 +203,17 @@ class _ConvBNAct(torch.autograd.Function):
         if ctx.wino:
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
             if grads.get("kernel") is not None:
-                check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout, OD,
-                                                   geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
-                                                   stream()),
-                      "conv3d_bwd_weight_wino")
+                if ctx.u is not None:
+                    check(L.m3d_conv3d_bwd_weight_wino_u(ptr(ctx.u), ptr(dz), B, H, W, D, Cin, Cout, OD,
+                                                         geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
+                                                         stream()),
+                          "conv3d_bwd_weight_wino_u")
+                    ctx.u = None
+                else:
+                    check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout, OD,
+                                                       geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
+                                                       stream()),
+                          "conv3d_bwd_weight_wino")
             dx = None
             if ctx.need_dx:
                 dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)

@@ -195,6 +195,18 @@ int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t
 int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
                                int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
                                float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
+/* Training variants: the forward keeps its transformed input U = B^T x B
+ * ([64][T][Cin], m3d_conv3d_wino_u_bytes) in caller memory (u_keep) and the
+ * weight gradient reuses it instead of transforming x again. */
+size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin);
+int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                             const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                             const float* bn_scale, const float* bn_shift, const float* residual,
+                             int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
+                             size_t ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H, int64_t W,
+                                 int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
+                                 float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
 
 /* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
  * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],
