@@ -778,21 +778,33 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
 
 
 // =========================================================================
-// Winograd F(2x2x2, 3x3x3) for stride-1 'same' 3x3x3 convs.
-//   fwd:   Y   = A^T [ (G W G^T) . (B^T X B) ] A        (per 2^3 output tile)
+// Winograd F(2x2xNZ, 3x3x3) for stride-1 'same' 3x3x3 convs: F(2,3) along y
+// and x, F(NZ,3) along z (NZ = 2, or 4 by default).
+//   fwd:   Y   = A^T [ (G W G^T) . (B^T X B) ] A        (per 2x2xNZ output tile)
 //   dgrad: dX  = same with W'[t][n][c] = W[flip t][c][n]
 //   wgrad: dW  = G^T [ sum_tiles (B^T X B) . (A dZ A^T) ] G
-// 1-D matrices (F(2,3), points 0, 1, -1, inf):
+// 1-D F(2,3), points 0, 1, -1, inf:
 //   B^T d = [d0-d2, d1+d2, d2-d1, d1-d3]      G g = [g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2]
 //   A^T m = [m0+m1+m2, m1-m2-m3]              A e = [e0, e0+e1, e0-e1, -e1]
 //   G^T v = [v0+(v1+v2)/2, (v1-v2)/2, (v1+v2)/2+v3]
-// The 64 point-wise products become 64 independent GEMMs (one per point xi)
-// run by the same MFMA kernels in batched mode: 3.375x fewer FLOPs than the
-// direct implicit GEMM.  Transformed operands live in a caller workspace,
-// xi-major: U[64][T][C], V[64][K][N], M[64][T][N].
+// 1-D F(4,3) along z, points 0, 1, -1, 1/2, -1/2, inf (exact rationals;
+// the half-integer points keep the fp32 error at the F(2,3)/direct level --
+// measured 4.3e-6 vs 4.6e-6 relative for a 256-channel direct fp32 conv, where
+// the integer points +-2 give 1.3x that and F(4,3) on all three axes 15x):
+//   B^T d = [d0/4 - 5/4 d2 + d4, -(d1+d2)/4 + d3 + d4, (d1-d2)/4 - d3 + d4,
+//            -d1/2 - d2 + d3/2 + d4, d1/2 - d2 - d3/2 + d4, d1/4 - 5/4 d3 + d5]
+//   G g   = [4 g0, 2/3 (g0+g1+g2), 2/3 (g0-g1+g2), -8/3 g0 - 4/3 g1 - 2/3 g2,
+//            -8/3 g0 + 4/3 g1 - 2/3 g2, g2]
+//   A^T m = [m0+m1+m2+m3+m4, m1-m2+(m3-m4)/2, m1+m2+(m3+m4)/4, m1-m2+(m3-m4)/8+m5]
+// The 16*(NZ+2) point-wise products (64 or 96) become independent GEMMs (one
+// per point xi) run by the same MFMA kernels in batched mode: 27*2*2*NZ /
+// (16*(NZ+2)) = 3.375x (NZ=2) or 4.5x (NZ=4) fewer FLOPs than the direct
+// implicit GEMM, and the transformed operands are 8x / 6x the tensors they
+// come from.  Transformed operands live in a caller workspace, xi-major:
+// U[P][T][C], V[P][K][N], M[P][T][N].
 // =========================================================================
 // Tile grid over the OUTPUT (depth D); the transformed input is read from a
-// tensor of depth Din at z = 2tz - pz + k ('same': Din = D, pz = 1; a depth
+// tensor of depth Din at z = NZ*tz - pz + k ('same': Din = D, pz = 1; a depth
 // slab extended by z-halo planes: Din = D + halos, pz = 1 - lower halo).
 struct WinoGeom {
     int B, H, W, D, Din, pz, TY, TX, TZ;
@@ -803,6 +815,79 @@ __device__ __forceinline__ void bt4(float& a0, float& a1, float& a2, float& a3) 
     const float t0 = a0 - a2, t1 = a1 + a2, t2 = a2 - a1, t3 = a1 - a3;
     a0 = t0; a1 = t1; a2 = t2; a3 = t3;
 }
+__device__ __forceinline__ void g3(float g0, float g1, float g2, float* o) {
+    o[0] = g0;
+    o[1] = (g0 + g1 + g2) * 0.5f;
+    o[2] = (g0 - g1 + g2) * 0.5f;
+    o[3] = g2;
+}
+__device__ __forceinline__ void at4(float m0, float m1, float m2, float m3, float& o0, float& o1) {
+    o0 = m0 + m1 + m2;
+    o1 = m1 - m2 - m3;
+}
+__device__ __forceinline__ void a4(float e0, float e1, float* o) {
+    o[0] = e0; o[1] = e0 + e1; o[2] = e0 - e1; o[3] = -e1;
+}
+__device__ __forceinline__ void gt4(float v0, float v1, float v2, float v3, float* o) {
+    o[0] = v0 + (v1 + v2) * 0.5f;
+    o[1] = (v1 - v2) * 0.5f;
+    o[2] = (v1 + v2) * 0.5f + v3;
+}
+
+// z-axis transforms of F(NZ,3): P = NZ + 2 points
+template <int NZ> struct ZT;
+template <> struct ZT<2> {
+    static constexpr int P = 4;
+    __device__ static void bt(float* d) { bt4(d[0], d[1], d[2], d[3]); }
+    __device__ static void g(const float* w, float* o) { g3(w[0], w[1], w[2], o); }
+    __device__ static void at(const float* m, float* o) { at4(m[0], m[1], m[2], m[3], o[0], o[1]); }
+    __device__ static void a(const float* e, float* o) { a4(e[0], e[1], o); }
+    __device__ static void gt(const float* v, float* o) { gt4(v[0], v[1], v[2], v[3], o); }
+};
+template <> struct ZT<4> {
+    static constexpr int P = 6;
+    __device__ static void bt(float* d) {
+        const float d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4], d5 = d[5];
+        d[0] = d0 * 0.25f - d2 * 1.25f + d4;
+        d[1] = -(d1 + d2) * 0.25f + d3 + d4;
+        d[2] = (d1 - d2) * 0.25f - d3 + d4;
+        d[3] = -d1 * 0.5f - d2 + d3 * 0.5f + d4;
+        d[4] = d1 * 0.5f - d2 - d3 * 0.5f + d4;
+        d[5] = d1 * 0.25f - d3 * 1.25f + d5;
+    }
+    __device__ static void g(const float* w, float* o) {
+        const float c23 = 2.0f / 3.0f;
+        o[0] = 4.0f * w[0];
+        o[1] = c23 * (w[0] + w[1] + w[2]);
+        o[2] = c23 * (w[0] - w[1] + w[2]);
+        o[3] = -(8.0f / 3.0f) * w[0] - (4.0f / 3.0f) * w[1] - c23 * w[2];
+        o[4] = -(8.0f / 3.0f) * w[0] + (4.0f / 3.0f) * w[1] - c23 * w[2];
+        o[5] = w[2];
+    }
+    __device__ static void at(const float* m, float* o) {
+        const float s12 = m[1] + m[2], d12 = m[1] - m[2], s34 = m[3] + m[4], d34 = m[3] - m[4];
+        o[0] = m[0] + s12 + s34;
+        o[1] = d12 + d34 * 0.5f;
+        o[2] = s12 + s34 * 0.25f;
+        o[3] = d12 + d34 * 0.125f + m[5];
+    }
+    // A = (A^T)^T: e [4] -> 6
+    __device__ static void a(const float* e, float* o) {
+        o[0] = e[0];
+        o[1] = e[0] + e[1] + e[2] + e[3];
+        o[2] = e[0] - e[1] + e[2] - e[3];
+        o[3] = e[0] + e[1] * 0.5f + e[2] * 0.25f + e[3] * 0.125f;
+        o[4] = e[0] - e[1] * 0.5f + e[2] * 0.25f - e[3] * 0.125f;
+        o[5] = e[3];
+    }
+    // G^T: v [6] -> 3
+    __device__ static void gt(const float* v, float* o) {
+        const float c23 = 2.0f / 3.0f;
+        o[0] = 4.0f * v[0] + c23 * (v[1] + v[2]) - (8.0f / 3.0f) * (v[3] + v[4]);
+        o[1] = c23 * (v[1] - v[2]) - (4.0f / 3.0f) * (v[3] - v[4]);
+        o[2] = c23 * (v[1] + v[2]) - c23 * (v[3] + v[4]) + v[5];
+    }
+};
 
 __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b, int& ty, int& tx,
                                             int& tz) {
@@ -814,16 +899,19 @@ __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b
     b = (int)(r / g.TY);
 }
 
-// U[xi][t][c] = (B^T (x) B^T (x) B^T) d, d = the 4^3 input tile at (2ty-1, 2tx-1, 2tz-1).
+// U[xi][t][c] = (B^T (x) B^T (x) Bz^T) d, d = the 4x4xP input tile at
+// (2ty-1, 2tx-1, NZ*tz-pz); xi = (a*4 + b)*P + k.
+template <int NZ>
 __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
                                                          int C, float* __restrict__ U) {
+    constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.T * C) return;
     const int c = (int)(i % C);
     const int64_t t = i / C;
     int b, ty, tx, tz;
     tile_coords(t, g, b, ty, tx, tz);
-    float d[4][4][4];
+    float d[4][4][P];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
         const int y = 2 * ty - 1 + a;
@@ -833,8 +921,8 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
             const bool ok = y >= 0 && y < g.H && xx >= 0 && xx < g.W;
             const float* row = x + ((((int64_t)b * g.H + y) * g.W + xx) * g.Din) * C + c;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int z = 2 * tz - g.pz + k;
+            for (int k = 0; k < P; ++k) {
+                const int z = NZ * tz - g.pz + k;
                 d[a][bb][k] = (ok && z >= 0 && z < g.Din) ? row[(int64_t)z * C] : 0.0f;
             }
         }
@@ -842,15 +930,15 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) bt4(d[a][bb][0], d[a][bb][1], d[a][bb][2], d[a][bb][3]);
+        for (int bb = 0; bb < 4; ++bb) ZT<NZ>::bt(d[a][bb]);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) bt4(d[a][0][k], d[a][1][k], d[a][2][k], d[a][3][k]);
+        for (int k = 0; k < P; ++k) bt4(d[a][0][k], d[a][1][k], d[a][2][k], d[a][3][k]);
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) bt4(d[0][bb][k], d[1][bb][k], d[2][bb][k], d[3][bb][k]);
+        for (int k = 0; k < P; ++k) bt4(d[0][bb][k], d[1][bb][k], d[2][bb][k], d[3][bb][k]);
     const int64_t stride = g.T * C;
     float* o = U + t * C + c;
 #pragma unroll
@@ -858,21 +946,16 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) o[(int64_t)((a * 4 + bb) * 4 + k) * stride] = d[a][bb][k];
+            for (int k = 0; k < P; ++k) o[(int64_t)((a * 4 + bb) * P + k) * stride] = d[a][bb][k];
 }
 
-__device__ __forceinline__ void g3(float g0, float g1, float g2, float* o) {
-    o[0] = g0;
-    o[1] = (g0 + g1 + g2) * 0.5f;
-    o[2] = (g0 - g1 + g2) * 0.5f;
-    o[3] = g2;
-}
-
-// V[xi][k'][n'] = (G (x) G (x) G) w.  fwd: k'=cin, n'=cout; bwd (transpose_flip):
+// V[xi][k'][n'] = (G (x) G (x) Gz) w.  fwd: k'=cin, n'=cout; bwd (transpose_flip):
 // k'=cout, n'=cin, w taken at the flipped tap.
+template <int NZ>
 __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restrict__ w, int Cin,
                                                           int Cout, int transpose_flip,
                                                           float* __restrict__ V) {
+    constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t KN = (int64_t)Cin * Cout;
     if (i >= KN) return;
@@ -889,16 +972,16 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
                 const int t = transpose_flip ? ((2 - a) * 3 + (2 - b)) * 3 + (2 - k) : (a * 3 + b) * 3 + k;
                 gw[a][b][k] = w[(int64_t)t * KN + (int64_t)cin * Cout + cout];
             }
-    float t1[3][3][4];
+    float t1[3][3][P];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) g3(gw[a][b][0], gw[a][b][1], gw[a][b][2], t1[a][b]);
-    float t2[3][4][4];
+        for (int b = 0; b < 3; ++b) ZT<NZ>::g(gw[a][b], t1[a][b]);
+    float t2[3][4][P];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < P; ++k) {
             float o[4];
             g3(t1[a][0][k], t1[a][1][k], t1[a][2][k], o);
 #pragma unroll
@@ -908,22 +991,19 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < P; ++k) {
             float o[4];
             g3(t2[0][b][k], t2[1][b][k], t2[2][b][k], o);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + b) * 4 + k) * KN] = o[a];
+            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + b) * P + k) * KN] = o[a];
         }
 }
 
-__device__ __forceinline__ void at4(float m0, float m1, float m2, float m3, float& o0, float& o1) {
-    o0 = m0 + m1 + m2;
-    o1 = m1 - m2 - m3;
-}
-
-// Y tile (2^3) = (A^T (x) A^T (x) A^T) M[.][t][n], then the conv epilogue.
+// Y tile (2x2xNZ) = (A^T (x) A^T (x) Az^T) M[.][t][n], then the conv epilogue.
+template <int NZ>
 __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, WinoGeom g,
                                                           int N, Epi e) {
+    constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.T * N) return;
     const int n = (int)(i % N);
@@ -932,30 +1012,29 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
     tile_coords(t, g, b, ty, tx, tz);
     const int64_t stride = g.T * N;
     const float* src = Mt + t * N + n;
-    float m[4][4][4];
+    float m[4][4][P];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) m[a][bb][k] = src[(int64_t)((a * 4 + bb) * 4 + k) * stride];
-    float r1[4][4][2];
+            for (int k = 0; k < P; ++k) m[a][bb][k] = src[(int64_t)((a * 4 + bb) * P + k) * stride];
+    float r1[4][4][NZ];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
-            at4(m[a][bb][0], m[a][bb][1], m[a][bb][2], m[a][bb][3], r1[a][bb][0], r1[a][bb][1]);
-    float r2[4][2][2];
+        for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
+    float r2[4][2][NZ];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < NZ; ++k)
             at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
-    float o[2][2][2];
+    float o[2][2][NZ];
 #pragma unroll
     for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < NZ; ++k)
             at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
     const float bias = e.bias ? e.bias[n] : 0.0f;
     const float sc = e.scale ? e.scale[n] : 1.0f, sh = e.scale ? e.shift[n] : 0.0f;
@@ -968,8 +1047,8 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
             const int xx = 2 * tx + bb;
             if (xx >= g.W) continue;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int z = 2 * tz + k;
+            for (int k = 0; k < NZ; ++k) {
+                const int z = NZ * tz + k;
                 if (z >= g.D) continue;
                 const int64_t row = (((int64_t)b * g.H + y) * g.W + xx) * g.D + z;
                 float v = o[a][bb][k];
@@ -986,40 +1065,41 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
     }
 }
 
-// DY[xi][t][n] = (A (x) A (x) A) e, e = the 2^3 output-gradient tile (0 outside).
+// DY[xi][t][n] = (A (x) A (x) Az) e, e = the 2x2xNZ output-gradient tile (0 outside).
+template <int NZ>
 __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict__ dz, WinoGeom g,
                                                         int N, float* __restrict__ DY) {
+    constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.T * N) return;
     const int n = (int)(i % N);
     const int64_t t = i / N;
     int b, ty, tx, tz;
     tile_coords(t, g, b, ty, tx, tz);
-    float ev[2][2][2];
+    float ev[2][2][NZ];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int y = 2 * ty + a, xx = 2 * tx + bb, z = 2 * tz + k;
+            for (int k = 0; k < NZ; ++k) {
+                const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
                 ev[a][bb][k] = (y < g.H && xx < g.W && z < g.D)
                                    ? dz[((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * N + n]
                                    : 0.0f;
             }
-    auto A4 = [](float e0, float e1, float* o) { o[0] = e0; o[1] = e0 + e1; o[2] = e0 - e1; o[3] = -e1; };
-    float t1[2][2][4];
+    float t1[2][2][P];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) A4(ev[a][bb][0], ev[a][bb][1], t1[a][bb]);
-    float t2[2][4][4];
+        for (int bb = 0; bb < 2; ++bb) ZT<NZ>::a(ev[a][bb], t1[a][bb]);
+    float t2[2][4][P];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < P; ++k) {
             float o[4];
-            A4(t1[a][0][k], t1[a][1][k], o);
+            a4(t1[a][0][k], t1[a][1][k], o);
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) t2[a][bb][k] = o[bb];
         }
@@ -1028,38 +1108,34 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < P; ++k) {
             float o[4];
-            A4(t2[0][bb][k], t2[1][bb][k], o);
+            a4(t2[0][bb][k], t2[1][bb][k], o);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + bb) * 4 + k) * stride] = o[a];
+            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + bb) * P + k) * stride] = o[a];
         }
 }
 
-__device__ __forceinline__ void gt4(float v0, float v1, float v2, float v3, float* o) {
-    o[0] = v0 + (v1 + v2) * 0.5f;
-    o[1] = (v1 - v2) * 0.5f;
-    o[2] = (v1 + v2) * 0.5f + v3;
-}
-
-// dW[t][c][n] += (G^T (x) G^T (x) G^T) dWh[.][c][n]
+// dW[t][c][n] += (G^T (x) G^T (x) Gz^T) dWh[.][c][n]
+template <int NZ>
 __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ dWh, int C,
                                                              int N, float* __restrict__ dw) {
+    constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t CN = (int64_t)C * N;
     if (i >= CN) return;
-    float v[4][4][4];
+    float v[4][4][P];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[a][b][k] = dWh[(int64_t)((a * 4 + b) * 4 + k) * CN + i];
+            for (int k = 0; k < P; ++k) v[a][b][k] = dWh[(int64_t)((a * 4 + b) * P + k) * CN + i];
     float t1[4][4][3];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) gt4(v[a][b][0], v[a][b][1], v[a][b][2], v[a][b][3], t1[a][b]);
+        for (int b = 0; b < 4; ++b) ZT<NZ>::gt(v[a][b], t1[a][b]);
     float t2[4][3][3];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -1081,10 +1157,33 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
         }
 }
 
-static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz) {
+// M3D_WINO_NZ = 2 selects the F(2x2x2) tiles (A/B testing; default 4: F(2x2x4))
+static int wino_nz() {
+    static int v = [] { const char* e = getenv("M3D_WINO_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
+    return v;
+}
+// The weight gradient keeps F(2x2x2) (M3D_WINO_WGRAD_NZ=4 for A/B): its
+// tile-summed Winograd-domain products go through G^T, whose F(4,3) rows
+// (4, 8/3, ...) amplify the fp32 summation error over the tiles ~10x -- the
+// forward / data-gradient F(2x2x4) stays at the direct conv's error level.
+static int wino_wgrad_nz() {
+    static int v = [] { const char* e = getenv("M3D_WINO_WGRAD_NZ"); return e && atoi(e) == 4 ? 4 : 2; }();
+    return v;
+}
+// M3D_WINO_DGRAD_NZ overrides the data-gradient tile (default: the forward's)
+static int wino_dgrad_nz() {
+    static int v = [] { const char* e = getenv("M3D_WINO_DGRAD_NZ"); return e ? (atoi(e) == 2 ? 2 : 4) : wino_nz(); }();
+    return v;
+}
+static int wino_points(int nz) { return 16 * (nz + 2); }
+static int wino_points() { return wino_points(wino_nz()); }
+
+static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz,
+                          int nz = -1) {
     WinoGeom g;
+    if (nz < 0) nz = wino_nz();
     g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
-    g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + 1) / 2);
+    g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
     g.T = B * g.TY * g.TX * g.TZ;
     return g;
 }
@@ -1363,30 +1462,48 @@ static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, in
     if (B * H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
     return M3D_OK;
 }
-// Workspace: V [64][Cin][Cout] + U [64][T][C1] + M [64][T][C2] with
+// Workspace: V [P][Cin][Cout] + U [P][T][C1] + M [P][T][C2] (P = 16*(NZ+2) points) with
 // {C1, C2} = {Cin, Cout} (fwd / wgrad) or {Cout, Cin} (bwd-data), T the larger
 // of the fwd (tiles over OD) and bwd-data (tiles over D) tile counts.
+// launch the F(2x2xNZ) instantiation of a Winograd transform kernel
+#define WINO_LAUNCH_NZ(nz, kern, ...)                                            \
+    do {                                                                         \
+        if ((nz) == 4) hipLaunchKernelGGL(kern<4>, __VA_ARGS__);                 \
+        else hipLaunchKernelGGL(kern<2>, __VA_ARGS__);                           \
+    } while (0)
+#define WINO_LAUNCH(kern, ...) WINO_LAUNCH_NZ(wino_nz(), kern, __VA_ARGS__)
+
+extern "C" int32_t m3d_conv3d_wino_tile_z(void) { return wino_nz(); }
+
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {
-    const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return al(sizeof(float) * 64 * (size_t)Cin * Cout) + al(sizeof(float) * 64 * (size_t)g.T * Cin) +
-           al(sizeof(float) * 64 * (size_t)g.T * Cout);
+    size_t best = 0;
+    for (int nz : {wino_nz(), wino_wgrad_nz(), wino_dgrad_nz()}) {
+        const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz);
+        const size_t P = (size_t)wino_points(nz);
+        const size_t b = al(sizeof(float) * P * (size_t)Cin * Cout) + al(sizeof(float) * P * (size_t)g.T * Cin) +
+                         al(sizeof(float) * P * (size_t)g.T * Cout);
+        best = b > best ? b : best;
+    }
+    return best;
 }
 
 struct WinoWs { float *V, *U, *M; };
-static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout) {
+static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, int nz = -1) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t P = (size_t)wino_points(nz < 0 ? wino_nz() : nz);
     char* p = (char*)ws;
     WinoWs w;
-    w.V = (float*)p; p += al(sizeof(float) * 64 * (size_t)Cin * Cout);
-    w.U = (float*)p; p += al(sizeof(float) * 64 * (size_t)g.T * Cin);
+    w.V = (float*)p; p += al(sizeof(float) * P * (size_t)Cin * Cout);
+    w.U = (float*)p; p += al(sizeof(float) * P * (size_t)g.T * Cin);
     w.M = (float*)p;
     return w;
 }
 
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
-    return sizeof(float) * 64 * (size_t)(B * ((H + 1) / 2) * ((W + 1) / 2) * ((OD + 1) / 2)) * (size_t)Cin;
+    if (wino_nz() != wino_wgrad_nz()) return 0;       // forward tiles differ from the wgrad's: nothing to keep
+    return sizeof(float) * wino_points() * (size_t)wino_geom(B, H, W, OD, OD, 1).T * (size_t)Cin;
 }
 
 static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
@@ -1401,19 +1518,19 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
     if (u_keep) ws.U = u_keep;
-    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
+    WINO_LAUNCH(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
                        (int)Cin, (int)Cout, 0, ws.V);
-    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
+    WINO_LAUNCH(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
                        (int)Cin, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
     Epi e{};
     e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
-    dispatch_gemm<false, true>(p, e, s, 64);
+    dispatch_gemm<false, true>(p, e, s, wino_points());
     Epi o{};
     o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
     o.res_mode = residual ? 1 : 0; o.relu = relu; o.z = z_out; o.y = y; o.ldy = Cout;
-    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, s, ws.M,
+    WINO_LAUNCH(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, s, ws.M,
                        g, (int)Cout, o);
     return check_launch("conv3d winograd fwd");
 }
@@ -1435,6 +1552,8 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
                                         float* z_out, float* y, float* u_keep, void* workspace,
                                         size_t ws_bytes, m3d_stream_t s) {
     if (!u_keep) return einval("conv3d winograd: u_keep must not be NULL");
+    if (wino_nz() != wino_wgrad_nz())
+        return einval("conv3d winograd: forward and weight-gradient tiles differ (m3d_conv3d_wino_u_bytes == 0)");
     return fwd_wino(x, B, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift, residual, relu,
                     z_out, y, u_keep, workspace, ws_bytes, st(s));
 }
@@ -1450,21 +1569,22 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz);
-    // same layout with the roles of Cin/Cout swapped (V'[64][Cout][Cin], U'[64][T][Cout])
-    WinoWs ws = wino_ws(workspace, g, Cout, Cin);
-    hipLaunchKernelGGL(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+    const int nz = wino_dgrad_nz();
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
+    // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
+    WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz);
+    WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
                        (int)Cin, (int)Cout, 1, ws.V);
-    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+    WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cout, ws.V, (int)Cin);
     Epi e{};
     e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
-    dispatch_gemm<false, true>(p, e, st(s), 64);
+    dispatch_gemm<false, true>(p, e, st(s), wino_points(nz));
     Epi o{};
     o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
-    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
+    WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
                        g, (int)Cin, o);
     return check_launch("conv3d winograd bwd-data");
 }
@@ -1476,23 +1596,24 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
-    WinoWs ws = wino_ws(workspace, g, Cin, Cout);   // V <- dW_hat, U <- B^T x, M <- A dz
-    if (hipMemsetAsync(ws.V, 0, sizeof(float) * 64 * (size_t)Cin * Cout, st(s)) != hipSuccess)
+    const int nz = wino_wgrad_nz();
+    const WinoGeom g = wino_geom(B, H, W, OD, D, pz, nz);
+    WinoWs ws = wino_ws(workspace, g, Cin, Cout, nz);   // V <- dW_hat, U <- B^T x, M <- A dz
+    if (hipMemsetAsync(ws.V, 0, sizeof(float) * wino_points(nz) * (size_t)Cin * Cout, st(s)) != hipSuccess)
         return check_launch("memset dW_hat");
     if (u_in)
         ws.U = const_cast<float*>(u_in);       // the forward's transformed input, kept
     else
-        hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
+        WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
                            (int)Cin, ws.U);
-    hipLaunchKernelGGL(wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+    WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, nullptr, (int)Cout);
     p.bsw = g.T * Cout;                 // dz (DY) batch stride
     p.bsy = (int64_t)Cin * Cout;        // dW_hat batch stride
-    if (Cout <= 64) launch_wgrad<128, 64, 2, 2, true>(p, ws.M, ws.V, st(s), 64);
-    else launch_wgrad<128, 128, 2, 2, true>(p, ws.M, ws.V, st(s), 64);
-    hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s),
+    if (Cout <= 64) launch_wgrad<128, 64, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
+    else launch_wgrad<128, 128, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
+    WINO_LAUNCH_NZ(nz, wino_wgrad_out_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s),
                        ws.V, (int)Cin, (int)Cout, dw);
     return check_launch("conv3d winograd bwd-weight");
 }

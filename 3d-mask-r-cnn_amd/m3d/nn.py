@@ -142,9 +142,11 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.u = None
         if ctx.wino:
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
-            if grads is not None and grads.get("kernel") is not None:
-                # training: keep the transformed input U for the weight gradient
-                nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4
+            # training: keep the transformed input U for the weight gradient when
+            # the forward and weight-gradient tiles agree (u_bytes > 0)
+            nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4 \
+                if grads is not None and grads.get("kernel") is not None else 0
+            if nu > 0:
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32)
                 check(_L().m3d_conv3d_fwd_wino_keep(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
                                                     ptr(b), ptr(scale), ptr(shift), ptr(residual),
@@ -164,8 +166,9 @@ class _ConvBNAct(torch.autograd.Function):
             direct = 2.0 * (y.numel() // Cout) * kh * kw * kd * Cin * Cout
             exe = direct
             if ctx.wino:
-                tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // 2)
-                exe = 2.0 * 64 * tiles * Cin * Cout
+                nz = int(_L().m3d_conv3d_wino_tile_z())
+                tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // nz)
+                exe = 2.0 * 16 * (nz + 2) * tiles * Cin * Cout
             nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
             _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
         ctx.save_for_backward(x, w, y, z)

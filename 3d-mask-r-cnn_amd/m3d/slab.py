@@ -10,8 +10,8 @@ receives the r = (kd-1)/2 boundary planes of its neighbours (point-to-point
 over RCCL/xGMI) and runs the op on the extended slab with the z padding only
 where the volume really ends; in backward the halo planes' gradients travel
 back to their owners and are added there.  The result is the single-volume
-computation: identical per-voxel arithmetic (slab bounds are even, so the
-Winograd 2x2x2 tiles coincide with the unsharded ones).
+computation: identical per-voxel arithmetic (slab bounds are multiples of 4, so the
+Winograd 2x2x4 tiles coincide with the unsharded ones).
 
 Losses are partial sums over each rank's anchors divided by the global
 counts; weight gradients are all-reduced with SUM; the ProposalLayer merges
@@ -31,15 +31,20 @@ import torch.distributed as dist
 _ACTIVE = None
 
 
+Z_ALIGN = 4   # the Winograd output tile along z (F(2x2x4)): slab starts are multiples of it
+
+
 def slab_bounds(depth, world):
-    """Even-aligned near-equal split of [0, depth) into `world` slabs."""
-    units = (depth + 1) // 2
+    """Near-equal split of [0, depth) into `world` slabs starting at multiples
+    of Z_ALIGN, so every slab's Winograd z tiles coincide with the whole
+    volume's (the sharded forward is then bit-identical)."""
+    units = (depth + Z_ALIGN - 1) // Z_ALIGN
     if units < world:
         raise ValueError(f"depth {depth} too small for {world} slabs")
     per, rem = divmod(units, world)
     out, z = [], 0
     for r in range(world):
-        n = 2 * (per + (1 if r < rem else 0))
+        n = Z_ALIGN * (per + (1 if r < rem else 0))
         out.append((z, min(z + n, depth)))
         z += n
     return out

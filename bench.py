@@ -64,11 +64,14 @@ def _pmc_traffic(kernel_key):
 
 def wino_gemm_shape(S):
     """The step's largest launch of its dominant kernel (conv_gemm_kernel):
-    the 64 batched Winograd point-wise GEMMs of rpn_conv_shared1 (3x3x3,
-    256->512) on P2 [S/4, S/4, S]: M = T = 2x2x2 output tiles, K = 256, N = 512."""
+    the 16*(NZ+2) batched Winograd point-wise GEMMs of rpn_conv_shared1
+    (3x3x3, 256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles,
+    K = 256, N = 512 (NZ = 4 by default: 96 GEMMs)."""
+    from m3d import _lib
+    nz = int(_lib.load().m3d_conv3d_wino_tile_z())
     q = S // 4
-    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + 1) // 2)
-    return 64, T, 256, 512
+    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
+    return 16 * (nz + 2), T, 256, 512
 
 
 def time_dominant_kernel(S, reps=5):
@@ -89,11 +92,11 @@ def time_dominant_kernel(S, reps=5):
     return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
             "traffic": _pmc_traffic(key),
-            "kernel": f"conv_gemm_kernel<128,128> (fp32 MFMA): 64 batched Winograd GEMMs of "
+            "kernel": f"conv_gemm_kernel<128,128> (fp32 MFMA): {nb} batched Winograd GEMMs of "
                       f"rpn_conv_shared1 on P2, M={T} K={K} N={N}",
             "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
             "algorithmic_bytes_per_launch": 4.0 * nb * (T * K + K * N + T * N),
-            "direct_conv_equivalent_tflops": round(2.0 * T * 8 * 27 * K * N / t / 1e12, 2)}
+            "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
 
 
 def time_direct_conv(model, fmaps, reps=5):

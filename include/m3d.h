@@ -198,6 +198,9 @@ int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64
 /* Training variants: the forward keeps its transformed input U = B^T x B
  * ([64][T][Cin], m3d_conv3d_wino_u_bytes) in caller memory (u_keep) and the
  * weight gradient reuses it instead of transforming x again. */
+/* z extent of the Winograd output tile (4: F(2x2x4), default; 2: F(2x2x2)
+ * when M3D_WINO_NZ=2): 16*(NZ+2) batched point GEMMs per conv. */
+int32_t m3d_conv3d_wino_tile_z(void);
 size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin);
 int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
                              const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,

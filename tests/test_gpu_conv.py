@@ -232,11 +232,18 @@ def test_winograd_z_halo_geometry(cuda, D, OD, pz):
     close(dx, xr.grad)
     close(dw, wr.grad)
     # training variants: the forward keeps U = B^T x B, the weight gradient reuses it
-    u = torch.empty(int(L.m3d_conv3d_wino_u_bytes(1, H, W, OD, Ci)) // 4, device=cuda)
+    # (only when the forward and weight-gradient tiles agree; u_bytes == 0 otherwise)
+    ub = int(L.m3d_conv3d_wino_u_bytes(1, H, W, OD, Ci))
+    u = torch.empty(max(ub, 4) // 4, device=cuda)
     y2 = torch.empty_like(y)
-    _lib.check(L.m3d_conv3d_fwd_wino_keep(xd.data_ptr(), 1, H, W, D, Ci, wd.data_ptr(), Co, OD, pz, None,
-                                          None, None, None, 0, None, y2.data_ptr(), u.data_ptr(),
-                                          ws.data_ptr(), nb, _lib.stream()))
+    keep = lambda: _lib.check(L.m3d_conv3d_fwd_wino_keep(  # noqa: E731
+        xd.data_ptr(), 1, H, W, D, Ci, wd.data_ptr(), Co, OD, pz, None, None, None, None, 0, None,
+        y2.data_ptr(), u.data_ptr(), ws.data_ptr(), nb, _lib.stream()))
+    if ub == 0:
+        with pytest.raises(ValueError):
+            keep()
+        return
+    keep()
     dw2 = torch.zeros_like(dw)
     _lib.check(L.m3d_conv3d_bwd_weight_wino_u(u.data_ptr(), dyd.data_ptr(), 1, H, W, D, Ci, Co, OD, pz,
                                               dw2.data_ptr(), ws.data_ptr(), nb, _lib.stream()))

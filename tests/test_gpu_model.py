@@ -54,8 +54,10 @@ def _ref_grads(model, image, match, bbox, dtype):
 
 def test_backward_matches_reference(small, cuda):
     """Gradients vs float64.  Through ~60 layers fp32 itself drifts (relu-mask
-    flips near 0): the bar is the CPU fp32 restatement's own error, x4, and a
-    median below 1e-4."""
+    flips near 0): the bars are the CPU fp32 restatement's own error -- worst
+    tensor within 4x its worst, median tensor below a quarter of its median
+    (measured: GPU 1.2e-4 with the F(2x2x4) Winograd forward, 7.7e-5 with
+    F(2x2x2); CPU fp32 7.8e-4) -- and a median below 2e-4."""
     cfg, model, image, match, bbox, tg = small
     model.store.zero_grad()
     out = model.forward(image.to(cuda), proposals=False)
@@ -74,7 +76,8 @@ def test_backward_matches_reference(small, cuda):
         gpu.append((rel_err(p.grad, g_ref), p.name))
         cpu32.append(rel_err(g32[p.name], g_ref))
     gpu.sort(reverse=True)
-    assert float(np.median([e for e, _ in gpu])) < 1e-4
+    med = float(np.median([e for e, _ in gpu]))
+    assert med < 2e-4 and med <= 0.25 * float(np.median(cpu32)), (med, float(np.median(cpu32)))
     assert gpu[0][0] <= max(1e-3, 4 * max(cpu32)), (gpu[:5], max(cpu32))
 
 

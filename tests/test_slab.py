@@ -81,13 +81,13 @@ def test_slab_collectives():
         assert s == [0.0, 3.0, 6.0, 9.0, 12.0]
 
 
-def test_slab_bounds_even_and_covering():
+def test_slab_bounds_aligned_and_covering():
     from m3d.slab import slab_bounds
     for D, n in [(256, 8), (128, 8), (10, 3), (64, 4), (7, 2)]:
         b = slab_bounds(D, n)
         assert b[0][0] == 0 and b[-1][1] == D
         assert all(b[i][1] == b[i + 1][0] for i in range(n - 1))
-        assert all(z0 % 2 == 0 for z0, _ in b)
+        assert all(z0 % 4 == 0 for z0, _ in b)
     with pytest.raises(ValueError):
         slab_bounds(6, 4)
 
