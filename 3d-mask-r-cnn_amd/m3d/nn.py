@@ -49,14 +49,18 @@ def _L():
 
 # Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
 WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
-WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "128"))
+WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
+# below this channel count the weight gradient runs as a direct implicit GEMM
+# (its F(2x2x2) transforms cost more than they save at 64 channels; measured
+# on res2*_branch2b: Winograd fwd/dgrad 0.23 ms vs direct 0.27, wgrad 0.35 vs 0.33)
+WINO_WGRAD_MIN_C = int(os.environ.get("M3D_WINO_WGRAD_MIN_C", "128"))
 
 
 def use_winograd(geo, cin, cout, in_sp):
     """'same' 3x3x3 stride-1 convs, or their z-halo-extended depth-slab form
     (z pad 0/1, input depth = output depth + halo planes)."""
-    # below 128 channels the (bandwidth-bound) transforms cost more than the
-    # 3.375x MFMA saving (measured: res2*_branch2b 64->64 is no faster)
+    # below 64 channels the (bandwidth-bound) transforms cost more than the
+    # 4.5x MFMA saving of F(2x2x4)
     return (WINOGRAD and geo.k == (3, 3, 3) and geo.stride == (1, 1, 1) and geo.pad[:2] == (1, 1)
             and tuple(geo.out[:2]) == tuple(in_sp[:2]) and geo.pad[2] in (0, 1)
             and 0 <= in_sp[2] - geo.out[2] <= 2
@@ -145,7 +149,8 @@ class _ConvBNAct(torch.autograd.Function):
             # training: keep the transformed input U for the weight gradient when
             # the forward and weight-gradient tiles agree (u_bytes > 0)
             nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4 \
-                if grads is not None and grads.get("kernel") is not None else 0
+                if grads is not None and grads.get("kernel") is not None \
+                and min(Cin, Cout) >= WINO_WGRAD_MIN_C else 0
             if nu > 0:
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32)
                 check(_L().m3d_conv3d_fwd_wino_keep(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
@@ -205,7 +210,12 @@ class _ConvBNAct(torch.autograd.Function):
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
         if ctx.wino:
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
-            if grads.get("kernel") is not None:
+            if grads.get("kernel") is not None and min(Cin, Cout) < WINO_WGRAD_MIN_C:
+                check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
+                                              OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
+                                              stream()), "conv3d_bwd_weight")
+                ctx.u = None
+            elif grads.get("kernel") is not None:
                 if ctx.u is not None:
                     check(L.m3d_conv3d_bwd_weight_wino_u(ptr(ctx.u), ptr(dz), B, H, W, D, Cin, Cout, OD,
                                                          geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
