@@ -160,16 +160,40 @@ class RPN:
     def current_lr(self):
         return self.lr * (1.0 / (1.0 + self.decay * self.iterations))
 
+    def proposals_async(self, out):
+        """Launch the ProposalLayer (top-k, decode, 3-D NMS) of a forward's
+        outputs on a side HIP stream, so it runs concurrently with the backward
+        (nothing in the backward depends on it; its serial NMS reduce occupies
+        one CU).  Returns (rois, join): call join() before using rois on the
+        current stream."""
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        side = self._side
+        side.wait_stream(main)
+        probs, bbox = out["rpn_class"].detach(), out["rpn_bbox"].detach()
+        with torch.cuda.stream(side):
+            rois = self.proposal_layer([probs, bbox, self.anchors])
+        probs.record_stream(side)
+        bbox.record_stream(side)
+
+        def join():
+            main.wait_stream(side)
+            rois.record_stream(main)
+            return rois
+        return rois, join
+
     def train_step(self, image, targets: RPNTargets, proposals=True):
         self.store.zero_grad()
-        out = self.forward(image, proposals=proposals)
+        out = self.forward(image, proposals=False)
+        join = self.proposals_async(out)[1] if proposals else None
         lc, lb = self.losses(out, targets)
         total = lc * self.LOSS_WEIGHTS["rpn_class_loss"] + lb * self.LOSS_WEIGHTS["rpn_bbox_loss"]
         total.backward()
         self.rpn.finish_backward()
         self.sgd_step()
         return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
-                "rpn_rois": out["rpn_rois"]}
+                "rpn_rois": join() if join is not None else None}
 
     def load_weights(self, filepath, by_name=True, skip_mismatch=False, exclude=()):
         """keras_model.load_weights(filepath, by_name=True, ...) on the Keras-H5 format (m3d.weights)."""

@@ -139,7 +139,8 @@ def data_parallel_train_step(model, image, targets, world, proposals=True, overl
         hook.reset()
         mnn.GRAD_HOOK = hook
     try:
-        out = model.forward(image, proposals=proposals)
+        out = model.forward(image, proposals=False)
+        join = model.proposals_async(out)[1] if proposals else None   # overlaps the backward
         lc, lb = model.losses(out, targets)
         total = lc * model.LOSS_WEIGHTS["rpn_class_loss"] + lb * model.LOSS_WEIGHTS["rpn_bbox_loss"]
         total.backward()
@@ -152,7 +153,7 @@ def data_parallel_train_step(model, image, targets, world, proposals=True, overl
         allreduce_mean_(model.store.grad_flat, world)
     model.sgd_step()
     return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
-            "rpn_rois": out["rpn_rois"]}
+            "rpn_rois": join() if join is not None else None}
 
 
 # ---------------------------------------------------------------------------

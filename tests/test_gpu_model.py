@@ -89,3 +89,19 @@ def test_train_step_runs_and_updates(small, cuda):
     assert torch.isfinite(r["loss"]).item()
     assert r["rpn_rois"].shape == (1, cfg.POST_NMS_ROIS_TRAINING, 6)
     assert float((model.store.flat.detach() - before).abs().max()) > 0
+
+
+def test_proposals_on_side_stream_match(small, cuda):
+    """The ProposalLayer launched on the side stream (overlapping the backward
+    in train_step) gives the same proposals as the in-line call."""
+    cfg, model, image, *_ = small
+    with torch.no_grad():
+        out = model.forward(image.to(cuda), proposals=True)
+        rois, join = model.proposals_async(out)
+        # keep the main stream busy meanwhile, as the backward would
+        busy = torch.randn((4096, 4096), device=cuda)
+        for _ in range(4):
+            busy = busy @ busy.T * 1e-3
+        got = join()
+    torch.cuda.synchronize()
+    assert torch.equal(got, out["rpn_rois"])
