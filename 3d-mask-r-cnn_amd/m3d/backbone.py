@@ -154,7 +154,10 @@ class RPNHead:
         return logits, probs, bbox
 
     def finish_backward(self):
-        """Fold the padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
+        """Join the side-stream weight gradients (m3d.nn.join_wgrad) and fold the
+        padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
+        from .nn import join_wgrad
+        join_wgrad()
         if self.w_grad is None:
             return
         apl, cin = self.apl, 256

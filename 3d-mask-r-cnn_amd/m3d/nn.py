@@ -7,6 +7,7 @@ gradients.  Layout is channels-last [B,H,W,D,C] throughout, as the reference.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass
 
@@ -32,10 +33,49 @@ LAYER_LOG = None
 GRAD_HOOK = None
 
 
-def _grad_done(grads):
+# Weight gradients run on a side HIP stream, concurrently with the data-
+# gradient chain of the backward (the next layer's backward needs dx, never
+# dW): the many small, under-filled launches of the deep stages then overlap.
+# The side stream waits for the compute stream before each weight gradient
+# (dz ready), and join_wgrad() -- called by RPNHead.finish_backward, i.e.
+# before anything reads the gradients -- makes the compute stream wait for it.
+# M3D_WGRAD_STREAM=0 runs them in line.
+WGRAD_STREAM = os.environ.get("M3D_WGRAD_STREAM", "1") != "0"
+_SIDE = {}
+_SIDE_USED = set()
+
+
+def _wgrad_stream(dev):
+    if not WGRAD_STREAM:
+        return None
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(dev)
+    _SIDE_USED.add(key)
+    side = _SIDE[key]
+    side.wait_stream(torch.cuda.current_stream(dev))
+    return side
+
+
+def join_wgrad(dev=None):
+    """Make the current stream wait for the weight gradients launched on the side stream."""
+    for key in list(_SIDE_USED):
+        if dev is None or key == (dev.index if dev.index is not None else torch.cuda.current_device()):
+            torch.cuda.current_stream(torch.device("cuda", key)).wait_stream(_SIDE[key])
+            _SIDE_USED.discard(key)
+
+
+def _grad_done(grads, side=None):
     h = grads.get("_hook") if grads else None
     if h is not None:
-        h[0].done(h[1])
+        if side is not None:
+            # the bucket all-reduce must follow this layer's weight gradients
+            # (side) and its BN/bias gradients (compute stream)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                h[0].done(h[1])
+        else:
+            h[0].done(h[1])
 
 
 def _log(kind, direct_flops, exec_flops, nbytes):
@@ -208,37 +248,45 @@ class _ConvBNAct(torch.autograd.Function):
                 mean, rstd, scale = ctx.bn
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
+        side = _wgrad_stream(x.device) if grads.get("kernel") is not None else None
+        if side is not None:
+            dz.record_stream(side)
+            x.record_stream(side)
         if ctx.wino:
-            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
-            if grads.get("kernel") is not None and min(Cin, Cout) < WINO_WGRAD_MIN_C:
-                check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
-                                              OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
-                                              stream()), "conv3d_bwd_weight")
+            if grads.get("kernel") is not None:
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    if min(Cin, Cout) < WINO_WGRAD_MIN_C:
+                        check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
+                                                      OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
+                                                      stream()), "conv3d_bwd_weight")
+                    else:
+                        wsw, wswb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
+                        if ctx.u is not None:
+                            ctx.u.record_stream(torch.cuda.current_stream())
+                            check(L.m3d_conv3d_bwd_weight_wino_u(ptr(ctx.u), ptr(dz), B, H, W, D, Cin, Cout,
+                                                                 OD, geo.pad[2], ptr(grads["kernel"]),
+                                                                 ptr(wsw), wswb, stream()),
+                                  "conv3d_bwd_weight_wino_u")
+                        else:
+                            check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout, OD,
+                                                               geo.pad[2], ptr(grads["kernel"]), ptr(wsw),
+                                                               wswb, stream()),
+                                  "conv3d_bwd_weight_wino")
                 ctx.u = None
-            elif grads.get("kernel") is not None:
-                if ctx.u is not None:
-                    check(L.m3d_conv3d_bwd_weight_wino_u(ptr(ctx.u), ptr(dz), B, H, W, D, Cin, Cout, OD,
-                                                         geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
-                                                         stream()),
-                          "conv3d_bwd_weight_wino_u")
-                    ctx.u = None
-                else:
-                    check(L.m3d_conv3d_bwd_weight_wino(ptr(x), ptr(dz), B, H, W, D, Cin, Cout, OD,
-                                                       geo.pad[2], ptr(grads["kernel"]), ptr(ws), wsb,
-                                                       stream()),
-                          "conv3d_bwd_weight_wino")
+            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
             dx = None
             if ctx.need_dx:
                 dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
                 check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                  geo.pad[2], ptr(dx), 0, ptr(ws), wsb, stream()),
                       "conv3d_bwd_data_wino")
-            _grad_done(grads)
+            _grad_done(grads, side)
             return dx, (dres if need_res else None), None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
-            check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
-                                          OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
-                                          stream()), "conv3d_bwd_weight")
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
+                                              OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
+                                              stream()), "conv3d_bwd_weight")
         dx = None
         if ctx.need_dx:
             strided = any(s != 1 for s in geo.stride)
@@ -253,7 +301,7 @@ class _ConvBNAct(torch.autograd.Function):
             check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
                                         OD, *geo.stride, *geo.pad, ptr(dx), 0, stream()),
                   "conv3d_bwd_data")
-        _grad_done(grads)
+        _grad_done(grads, side)
         dr = None
         if need_res:
             if ctx.res_mode == 1:
