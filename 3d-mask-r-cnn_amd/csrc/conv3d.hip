@@ -847,6 +847,29 @@ __device__ __forceinline__ void gt4(float v0, float v1, float v2, float v3, floa
     o[2] = (v1 + v2) * 0.5f + v3;
 }
 
+// The transformed operands (U, DY: 6-8x the tensor they come from) are
+// written once and read once by the point GEMMs, and M is read once by the
+// output transform: non-temporal, so the streams do not evict the input tile
+// rows that neighbouring tiles re-read (each input element belongs to up to
+// 2x2x2 overlapping 4x4xP windows).  M3D_WINO_NT=0 for A/B.
+#ifndef M3D_WINO_NT
+#define M3D_WINO_NT 1
+#endif
+__device__ __forceinline__ void wino_st(float* p, float v) {
+#if M3D_WINO_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ float wino_ld(const float* p) {
+#if M3D_WINO_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // z-axis transforms of F(NZ,3): P = NZ + 2 points
 template <int NZ> struct ZT;
 template <> struct ZT<2> {
@@ -959,7 +982,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-            for (int k = 0; k < P; ++k) o[(int64_t)((a * 4 + bb) * P + k) * stride] = d[a][bb][k];
+            for (int k = 0; k < P; ++k) wino_st(o + (int64_t)((a * 4 + bb) * P + k) * stride, d[a][bb][k]);
 }
 
 // V[xi][k'][n'] = (G (x) G (x) Gz) w.  fwd: k'=cin, n'=cout; bwd (transpose_flip):
@@ -1031,7 +1054,7 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-            for (int k = 0; k < P; ++k) m[a][bb][k] = src[(int64_t)((a * 4 + bb) * P + k) * stride];
+            for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
     float r1[4][4][NZ];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -1125,7 +1148,7 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
             float o[4];
             a4(t2[0][bb][k], t2[1][bb][k], o);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + bb) * P + k) * stride] = o[a];
+            for (int a = 0; a < 4; ++a) wino_st(out + (int64_t)((a * 4 + bb) * P + k) * stride, o[a]);
         }
 }
 
