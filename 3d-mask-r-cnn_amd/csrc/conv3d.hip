@@ -948,18 +948,24 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     int b, ty, tx, tz;
     tile_coords(t, g, b, ty, tx, tz);
     float d[4][4][P];
+    // branch-free window loads: raw buffer loads whose out-of-range offset
+    // returns 0 (the zero padding), so all 16*P loads issue back to back
+    // (conditional global loads compiled to a branch + wait per element)
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(x, (uint64_t)g.B * g.H * g.W * g.Din * C * 4);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
         const int y = 2 * ty - 1 + a;
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int xx = 2 * tx - 1 + bb;
-            const bool ok = y >= 0 && y < g.H && xx >= 0 && xx < g.W;
-            const float* row = x + ((((int64_t)b * g.H + y) * g.W + xx) * g.Din) * C + c;
+            const bool ok = (unsigned)y < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
+            const uint32_t row = (uint32_t)((((b * g.H + y) * g.W + xx) * g.Din) * C + c);
 #pragma unroll
             for (int k = 0; k < P; ++k) {
                 const int z = NZ * tz - g.pz + k;
-                d[a][bb][k] = (ok && z >= 0 && z < g.Din) ? row[(int64_t)z * C] : 0.0f;
+                const bool in = ok && (unsigned)z < (unsigned)g.Din;
+                d[a][bb][k] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rs, in ? (row + (uint32_t)z * C) * 4u : M3D_OOB, 0, 0));
             }
         }
     }
@@ -1499,6 +1505,9 @@ static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, in
     if (pz < 0 || pz > 1 || D - OD < 0 || D - OD > 2)
         return einval("conv3d winograd: z geometry must be pz in {0,1} and 0 <= D - OD <= 2");
     if (B * H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
+    // the input transform reads x / dz through 32-bit buffer offsets
+    if (B * H * W * (D > OD ? D : OD) * (Cin > Cout ? Cin : Cout) * 4 > 0xFFFFFFF0LL)
+        return einval("conv3d winograd: operand larger than 4 GiB (32-bit buffer offsets)");
     return M3D_OK;
 }
 // Workspace: V [P][Cin][Cout] + U [P][T][C1] + M [P][T][C2] (P = 16*(NZ+2) points) with
