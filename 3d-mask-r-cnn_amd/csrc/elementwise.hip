@@ -207,9 +207,10 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
     }
 }
 
-// out_a[c] += sum_b part[a][b][c].  grid (ceil(C/64), 3); 256 threads =
-// 64 channels x 4 row groups, each with 4 independent accumulators; the
-// partials are folded in a fixed order (deterministic).
+// out_a[c] += sum_b part[a][b][c].  grid (ceil(C/16), 3); 256 threads =
+// 4 channel quads (float4) x 64 row groups, each with 4 independent
+// accumulators, folded by a fixed LDS tree (deterministic).  64 row groups keep
+// the serial chain short for the 2048-block partials of bn_act_bwd_kernel.
 __global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __restrict__ part, int gx,
                                                              int C, float* __restrict__ s0,
                                                              float* __restrict__ s1,
@@ -217,22 +218,45 @@ __global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __rest
     const int a = blockIdx.y;
     float* dst = a == 0 ? s0 : (a == 1 ? s1 : s2);
     if (!dst) return;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + tx;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int tq = threadIdx.x & 3, rg = threadIdx.x >> 2;
+    const int c = blockIdx.x * 16 + tq * 4;
+    float4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < C) {
         const float* p = part + (int64_t)a * gx * C + c;
-        int b = ty;
-        for (; b + 12 < gx; b += 16) {
+        int b = rg;
+        for (; b + 192 < gx; b += 256) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += p[(int64_t)(b + 4 * u) * C];
+            for (int u = 0; u < 4; ++u) {
+                const float4 v = *(const float4*)(p + (int64_t)(b + 64 * u) * C);
+                acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
+            }
         }
-        for (; b < gx; b += 4) acc[0] += p[(int64_t)b * C];
+        for (; b < gx; b += 64) {
+            const float4 v = *(const float4*)(p + (int64_t)b * C);
+            acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+        }
     }
-    __shared__ float red[4][64];
-    red[ty][tx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __shared__ float4 red[64][4];
+    red[rg][tq] = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x),
+                              (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
+                              (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z),
+                              (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w));
     __syncthreads();
-    if (ty == 0 && c < C) dst[c] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    for (int step = 32; step > 0; step >>= 1) {
+        if (rg < step) {
+            const float4 o = red[rg + step][tq];
+            float4 m = red[rg][tq];
+            m.x += o.x; m.y += o.y; m.z += o.z; m.w += o.w;
+            red[rg][tq] = m;
+        }
+        __syncthreads();
+    }
+    if (rg == 0 && c < C) {
+        const float4 r = red[0][tq];
+        dst[c] += r.x; dst[c + 1] += r.y; dst[c + 2] += r.z; dst[c + 3] += r.w;
+    }
 }
 
 // ---- Keras SGD over a flat parameter buffer split into segments padded to
@@ -349,6 +373,12 @@ extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64
     return check_launch("subsample221_kernel(bwd)");
 }
 
+// total bn_act_bwd blocks (M3D_BN_BLOCKS, default 2048 = 8 per CU: enough
+// loads in flight to stream dy/y/z at HBM rate; 512 reached ~2.7 TB/s)
+static int bn_blocks_env() {
+    static int v = [] { const char* e = getenv("M3D_BN_BLOCKS"); return e ? atoi(e) : 2048; }();
+    return v > 0 ? v : 2048;
+}
 static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {
     const int quads = (int)(C / 4);
     T = 1;
@@ -356,7 +386,7 @@ static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {
     groups = (quads + T - 1) / T;
     const int R = 256 / T;
     gx = (M + R - 1) / R;
-    const int64_t cap = 512 / groups > 0 ? 512 / groups : 1;
+    const int64_t cap = bn_blocks_env() / groups > 0 ? bn_blocks_env() / groups : 1;
     if (gx > cap) gx = cap;
     if (gx < 1) gx = 1;
 }
@@ -415,7 +445,7 @@ extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, i
                        sum_dpre_xhat ? 1 : 0, (float*)workspace);
     int rc = check_launch("bn_act_bwd_kernel");
     if (rc || !sums) return rc;
-    hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 63) / 64), 3), dim3(256), 0, st(s),
+    hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 15) / 16), 3), dim3(256), 0, st(s),
                        (const float*)workspace, (int)gx, (int)C, sum_dpre, sum_dpre_xhat, sum_dz);
     return check_launch("bn_sums_reduce_kernel");
 }
