@@ -95,6 +95,40 @@ __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
+// ---- exact 3-way bf16 split of fp32 operands (X3 GEMM mode) ---------------
+// x = hi + mid + lo with hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid):
+// both subtractions are exact (Sterbenz), and 3 x 8 significant bits cover the
+// 24-bit f32 significand, so the split is exact for normal x.  A product a*b
+// is sum_{p+q<=2} a_p b_q (6 bf16 MFMAs, each product exact in the f32
+// accumulator); the dropped terms are below 2^-24 |a b| -- the rounding error
+// of the f32 FMA itself.  v_mfma_f32_32x32x16_bf16 retires 16x the FLOPs per
+// cycle of v_mfma_f32_32x32x2_f32, so 6 of them are 2.7x the f32 MFMA rate.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t bf16_bits(float x) {
+    return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)x);
+}
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+    h = bf16_bits(x);
+    const float r = x - __uint_as_float(h << 16);
+    m = bf16_bits(r);
+    l = bf16_bits(r - __uint_as_float(m << 16));
+}
+// float4 (4 consecutive k) -> three 4 x bf16 packets (element j at bits 16j)
+__device__ __forceinline__ void split3x4(const float4& v, uint2* o) {
+    uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+    split3(v.x, h0, m0, l0); split3(v.y, h1, m1, l1);
+    split3(v.z, h2, m2, l2); split3(v.w, h3, m3, l3);
+    o[0] = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+    o[1] = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
+    o[2] = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+}
+// byte offset of (row, k) in an X3 LDS plane: 32 k x bf16 = 64-B rows, 16-B
+// chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 phase over
+// 16 consecutive rows of one chunk hits 16 distinct 4-bank groups.
+__device__ __forceinline__ int x3_off(int row, int k) {
+    return row * 64 + ((((k >> 3) ^ (row >> 2)) & 3) << 4) + (k & 7) * 2;
+}
+
 // m < 2^31 is guaranteed by the host checks: 32-bit unsigned division only.
 __device__ __forceinline__ void decompose(int64_t m64, int OH, int OW, int OD, int& b, int& oy,
                                           int& ox, int& oz) {
@@ -199,9 +233,11 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false>
+template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false,
+          bool X3 = false>
 __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_gemm_kernel(ConvP p, Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
+    static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
     static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     static_assert(WM * WN == 4, "4 waves");
@@ -221,7 +257,10 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     // stage (two barriers per k-tile) so 3 workgroups fit a CU.  Both keep the
     // next k-tile's global loads in flight in registers during the MFMAs.
     static_assert(NBUF == 1 || NBUF == 2, "NBUF");
-    __shared__ __attribute__((aligned(16))) float smem[NBUF * (A_SZ + B_SZ)];
+    // X3: three bf16 planes per operand, [row][32 k] (64-B rows, swizzled),
+    // B rows = n for both B layouts (the !BT loader transposes while splitting)
+    constexpr int STAGE = X3 ? 3 * (BM + BN) * BK / 2 : A_SZ + B_SZ;   // floats
+    __shared__ __attribute__((aligned(16))) float smem[NBUF * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
@@ -335,7 +374,8 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
 #pragma unroll
             for (int q = 0; q < BQ; ++q) {
                 const int idx = tid + 256 * q;
-                const int kr = idx / C4, c4 = idx % C4;
+                // X3: thread owns k rows BQ*(tid/C4) .. +BQ-1 of one n quad
+                const int kr = X3 ? BQ * (tid / C4) + q : idx / C4, c4 = X3 ? tid % C4 : idx % C4;
                 const int k = k0 + kr, n = n0 + c4 * 4;
                 rb[q] = bload4(rsB, (k < p.K && n < p.N) ? (uint32_t)(k * p.N + n) * 4u : M3D_OOB);
             }
@@ -354,6 +394,60 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     };
 
     auto store_tile = [&](int buf) {
+        if constexpr (X3) {
+            char* Ab = reinterpret_cast<char*>(smem);
+            char* Bb = Ab + 3 * BM * BK * 2;
+#pragma unroll
+            for (int q = 0; q < AQ; ++q) {
+                uint2 o[3];
+                split3x4(ra[q], o);
+                const int off = x3_off(tid / KC4 + RPP * q, a_col4 * 4);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    *reinterpret_cast<uint2*>(Ab + pl * (BM * BK * 2) + off) = o[pl];
+            }
+            if constexpr (BT) {
+#pragma unroll
+                for (int q = 0; q < BQ; ++q) {
+                    uint2 o[3];
+                    split3x4(rb[q], o);
+                    const int off = x3_off(tid / KC4 + RPP * q, a_col4 * 4);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        *reinterpret_cast<uint2*>(Bb + pl * (BN * BK * 2) + off) = o[pl];
+                }
+            } else {
+                // rb[q] = B[k0 + BQ*g + q][n .. n+3]: per n, BQ consecutive k
+                constexpr int C4 = BN / 4;
+                const int g = tid / C4, n4 = (tid % C4) * 4;
+                uint32_t hb[BQ][4], mb[BQ][4], lb[BQ][4];
+#pragma unroll
+                for (int q = 0; q < BQ; ++q) {
+                    split3(rb[q].x, hb[q][0], mb[q][0], lb[q][0]);
+                    split3(rb[q].y, hb[q][1], mb[q][1], lb[q][1]);
+                    split3(rb[q].z, hb[q][2], mb[q][2], lb[q][2]);
+                    split3(rb[q].w, hb[q][3], mb[q][3], lb[q][3]);
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int off = x3_off(n4 + c, BQ * g);
+                    if constexpr (BQ == 4) {
+                        *reinterpret_cast<uint2*>(Bb + off) =
+                            make_uint2(hb[0][c] | (hb[1][c] << 16), hb[2][c] | (hb[3][c] << 16));
+                        *reinterpret_cast<uint2*>(Bb + BN * BK * 2 + off) =
+                            make_uint2(mb[0][c] | (mb[1][c] << 16), mb[2][c] | (mb[3][c] << 16));
+                        *reinterpret_cast<uint2*>(Bb + 2 * BN * BK * 2 + off) =
+                            make_uint2(lb[0][c] | (lb[1][c] << 16), lb[2][c] | (lb[3][c] << 16));
+                    } else {
+                        static_assert(BQ == 2, "X3 B tile");
+                        *reinterpret_cast<uint32_t*>(Bb + off) = hb[0][c] | (hb[1][c] << 16);
+                        *reinterpret_cast<uint32_t*>(Bb + BN * BK * 2 + off) = mb[0][c] | (mb[1][c] << 16);
+                        *reinterpret_cast<uint32_t*>(Bb + 2 * BN * BK * 2 + off) = lb[0][c] | (lb[1][c] << 16);
+                    }
+                }
+            }
+            return;
+        }
         float* As = smem + buf * (A_SZ + B_SZ);
         float* Bs = As + A_SZ;
         if (AVEC) {
@@ -395,6 +489,42 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = NBUF == 2 ? (kt & 1) : 0;
         if (kt + 1 < nk) load_tile(kt + 1);
+        if constexpr (X3) {
+            const char* Ab = reinterpret_cast<const char*>(smem);
+            const char* Bb = Ab + 3 * BM * BK * 2;
+#pragma unroll
+            for (int s16 = 0; s16 < BK / 16; ++s16) {
+                // lane (l32, h): row l32, k = 16 s16 + 8h .. +7 (one 16-B chunk)
+                bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int off = x3_off(wm * TM * 32 + i * 32 + l32, 16 * s16 + 8 * h);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        af[i][pl] = *reinterpret_cast<const bf16x8*>(Ab + pl * (BM * BK * 2) + off);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int off = x3_off(wn * TN * 32 + j * 32 + l32, 16 * s16 + 8 * h);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * (BN * BK * 2) + off);
+                }
+                // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        floatx16 c = acc[i][j];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
+                    }
+            }
+        } else {
         const float* As = smem + buf * (A_SZ + B_SZ);
         const float* Bs = As + A_SZ;
 #pragma unroll
@@ -433,6 +563,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                                                                       acc[i][j], 0, 0, 0);
         }
         }
+        }
         if (NBUF == 2) {
             if (kt + 1 < nk) store_tile(buf ^ 1);
             __syncthreads();
@@ -458,9 +589,9 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     const int64_t Ln = L + Lstep;
     const bool more = PERSIST && Ln < total;
     constexpr int LDT = BN + 8;
-    constexpr int HALVES = (BM * LDT <= NBUF * (A_SZ + B_SZ)) ? 1 : 2;   // staged in row halves
+    constexpr int HALVES = (BM * LDT <= NBUF * STAGE) ? 1 : 2;   // staged in row halves
     constexpr int HR = BM / HALVES;
-    static_assert(HR * LDT <= NBUF * (A_SZ + B_SZ), "epilogue tile must fit the k-loop LDS");
+    static_assert(HR * LDT <= NBUF * STAGE, "epilogue tile must fit the k-loop LDS");
     static_assert(HALVES == 1 || (TM * 32) % HR == 0 || HR % (TM * 32) == 0, "wave rows vs halves");
     float* Ts = smem;
     constexpr int C4T = BN / 4;
@@ -691,11 +822,26 @@ static int gemm_persist_env() {
 static int num_cus() {
     static int v = [] {
         int dev = 0, n = 0;
-        hipGetDevice(&dev);
+        (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
             n = 256;
         return n;
     }();
+    return v;
+}
+
+// M3D_GEMM_X3 (bit mask, default 1): fp32 GEMMs on the exact 3-way bf16 split
+// (6 bf16 MFMAs per product, see split3) instead of v_mfma_f32_32x32x2_f32.
+// bit 0: Winograd fwd / bwd-data point GEMMs on operands pre-split by the
+// transforms (x3_gemm_kernel; measured 39.9 -> 37.9 ms/step at 128^3, GEMM
+// error vs fp64 below the f32 MFMA's: scripts/x3_accuracy.py); bit 1:
+// implicit-GEMM convs splitting in the LDS store (slower: off).
+static int gemm_x3_env() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 1; }();
+    return v & 1;
+}
+static int conv_x3_env() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? (atoi(e) >> 1) & 1 : 0; }();
     return v;
 }
 
@@ -707,6 +853,21 @@ static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch)
         const int64_t resident = (int64_t)num_cus() * (gemm_nbuf_env() == 1 ? 3 : 2);
         const bool plain = e.simple && !e.bias && !e.scale && !e.res_mode && !e.relu && !e.z && !e.split &&
                            !e.accumulate && !e.deconv && (e.ldy & 3) == 0;
+        if constexpr (BT || BN >= 64) {
+            if (conv_x3_env() && gemm_nbuf_env() == 1) {
+                if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
+                    ConvP pp = p;
+                    pp.nbatch = nbatch;
+                    const unsigned g = (unsigned)(resident / 8 * 8);
+                    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, true, true>), dim3(g),
+                                       dim3(256), 0, s, pp, e);
+                } else {
+                    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, false, true>), grid,
+                                       dim3(256), 0, s, p, e);
+                }
+                return;
+            }
+        }
         if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
             ConvP pp = p;
             pp.nbatch = nbatch;
@@ -937,7 +1098,9 @@ __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b
 
 // U[xi][t][c] = (B^T (x) B^T (x) Bz^T) d, d = the 4x4xP input tile at
 // (2ty-1, 2tx-1, NZ*tz-pz); xi = (a*4 + b)*P + k.
-template <int NZ>
+// X3O: U is written as the three bf16 planes of split3 (uint16 [3][points][T][C])
+// for x3_gemm_kernel -- the split is done once here, not per GEMM k-tile.
+template <int NZ, bool X3O = false>
 __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
                                                          int C, float* __restrict__ U) {
     constexpr int P = ZT<NZ>::P;
@@ -982,6 +1145,24 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 #pragma unroll
         for (int k = 0; k < P; ++k) bt4(d[0][bb][k], d[1][bb][k], d[2][bb][k], d[3][bb][k]);
     const int64_t stride = g.T * C;
+    if constexpr (X3O) {
+        unsigned short* o = reinterpret_cast<unsigned short*>(U) + t * C + c;
+        const int64_t pstride = (int64_t)16 * P * stride;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    uint32_t hh, mm, ll;
+                    split3(d[a][bb][k], hh, mm, ll);
+                    unsigned short* q = o + (int64_t)((a * 4 + bb) * P + k) * stride;
+                    __builtin_nontemporal_store((unsigned short)hh, q);
+                    __builtin_nontemporal_store((unsigned short)mm, q + pstride);
+                    __builtin_nontemporal_store((unsigned short)ll, q + 2 * pstride);
+                }
+        return;
+    }
     float* o = U + t * C + c;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -993,7 +1174,24 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 
 // V[xi][k'][n'] = (G (x) G (x) Gz) w.  fwd: k'=cin, n'=cout; bwd (transpose_flip):
 // k'=cout, n'=cin, w taken at the flipped tap.
-template <int NZ>
+// wt[t][n][c] = w[t][c][n] for the 27 taps (32x32 tiles through LDS)
+__global__ __launch_bounds__(256) void x3_wt_kernel(const float* __restrict__ w, int C, int N,
+                                                    float* __restrict__ wt) {
+    __shared__ float tile[32][33];
+    const int t = blockIdx.z, c0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int64_t base = (int64_t)t * C * N;
+#pragma unroll
+    for (int r = ty; r < 32; r += 8)
+        if (c0 + r < C && n0 + tx < N) tile[r][tx] = w[base + (int64_t)(c0 + r) * N + n0 + tx];
+    __syncthreads();
+#pragma unroll
+    for (int r = ty; r < 32; r += 8)
+        if (n0 + r < N && c0 + tx < C) wt[base + (int64_t)(n0 + r) * C + c0 + tx] = tile[tx][r];
+}
+
+// X3O: V is written as split3 planes, transposed: uint16 [3][points][n'][k'].
+template <int NZ, bool X3O = false>
 __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restrict__ w, int Cin,
                                                           int Cout, int transpose_flip,
                                                           float* __restrict__ V) {
@@ -1002,8 +1200,12 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
     const int64_t KN = (int64_t)Cin * Cout;
     if (i >= KN) return;
     int cin, cout, kp, np_, Np;
-    if (!transpose_flip) { cout = (int)(i % Cout); cin = (int)(i / Cout); kp = cin; np_ = cout; Np = Cout; }
-    else { cin = (int)(i % Cin); cout = (int)(i / Cin); kp = cout; np_ = cin; Np = Cin; }
+    // thread order: the output's contiguous axis fastest (X3O writes [n'][k'])
+    const bool cout_fast = X3O ? transpose_flip != 0 : !transpose_flip;
+    if (cout_fast) { cout = (int)(i % Cout); cin = (int)(i / Cout); }
+    else { cin = (int)(i % Cin); cout = (int)(i / Cin); }
+    if (!transpose_flip) { kp = cin; np_ = cout; Np = Cout; }
+    else { kp = cout; np_ = cin; Np = Cin; }
     float gw[3][3][3];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -1012,7 +1214,10 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const int t = transpose_flip ? ((2 - a) * 3 + (2 - b)) * 3 + (2 - k) : (a * 3 + b) * 3 + k;
-                gw[a][b][k] = w[(int64_t)t * KN + (int64_t)cin * Cout + cout];
+                // X3O forward: w arrives transposed ([27][Cout][Cin], x3_wt_kernel) so
+                // the cin-fastest lanes read it coalesced
+                gw[a][b][k] = (X3O && !transpose_flip) ? w[(int64_t)t * KN + (int64_t)cout * Cin + cin]
+                                                       : w[(int64_t)t * KN + (int64_t)cin * Cout + cout];
             }
     float t1[3][3][P];
 #pragma unroll
@@ -1029,6 +1234,27 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
 #pragma unroll
             for (int b = 0; b < 4; ++b) t2[a][b][k] = o[b];
         }
+    if constexpr (X3O) {
+        unsigned short* out = reinterpret_cast<unsigned short*>(V) + (int64_t)np_ * (KN / Np) + kp;
+        const int64_t pstride = (int64_t)16 * P * KN;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                float o[4];
+                g3(t2[0][b][k], t2[1][b][k], t2[2][b][k], o);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    uint32_t hh, mm, ll;
+                    split3(o[a], hh, mm, ll);
+                    unsigned short* q = out + (int64_t)((a * 4 + b) * P + k) * KN;
+                    q[0] = (unsigned short)hh;
+                    q[pstride] = (unsigned short)mm;
+                    q[2 * pstride] = (unsigned short)ll;
+                }
+            }
+        return;
+    }
     float* out = V + (int64_t)kp * Np + np_;
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -1197,6 +1423,189 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
 #pragma unroll
             for (int a = 0; a < 3; ++a) dw[(int64_t)((a * 3 + b) * 3 + k) * CN + i] += o[a];
         }
+}
+
+// ---- batched fp32 GEMM on pre-split operands (Winograd point GEMMs) ------
+// C[b][m][n] = sum_k A[b][m][k] B[b][n][k]; A and B are the three bf16 planes
+// of split3 (uint16 [3][batch][rows][K], k contiguous, written by the X3O
+// transforms), C fp32 [batch][M][N].  128x128 tiles, 32-deep k-tiles staged
+// through one swizzled LDS stage (x3_off) with the next k-tile's 16-byte
+// chunks in flight in registers; 6 bf16 MFMAs per product (see split3).
+// PERSIST: a resident grid loops over all tiles of all batches (XCD-
+// contiguous order, as conv_gemm_kernel).
+struct X3G {
+    const unsigned short* a;
+    const unsigned short* b;
+    float* c;
+    int64_t M;
+    int K, N, nbatch;
+    int64_t psa, psb;          // plane strides (elements)
+    int64_t bsa, bsb, bsc;     // batch strides (elements)
+};
+
+// byte offset of (row, chunk) in a 16-deep X3 plane: 32-B rows of two 16-B
+// chunks, the chunk flipped for rows 8..15 of each 16-row group, so a 16-lane
+// ds_read_b128 phase over 16 consecutive rows covers the 64 banks once
+__device__ __forceinline__ int x3_off16(int row, int kc) {
+    return row * 32 + (((kc ^ (row >> 3)) & 1) << 4);
+}
+
+// BK 16: two LDS stages (one barrier per k-tile), 3 blocks/CU; BK 32: one
+// stage (two barriers per k-tile), 2 blocks/CU.
+template <int BK>
+__device__ __forceinline__ int x3_soff(int row, int kc) {
+    if constexpr (BK == 16) return x3_off16(row, kc);
+    else return x3_off(row, kc * 8);
+}
+
+template <int BK, bool PERSIST, int OCC = (BK == 16 ? 3 : 2)>
+__global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
+    static_assert(BK == 16 || BK == 32, "BK");
+    constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+    constexpr int NBUF = BK == 16 ? 2 : 1;
+    constexpr int KCH = BK / 8, CPT = BM * KCH / 256;   // 16-B chunks per row / per thread and plane
+    constexpr int PLA = BM * BK * 2, PLB = BN * BK * 2;   // bytes per plane
+    constexpr int STAGE = 3 * (PLA + PLB);
+    constexpr int LDT = BN + 8, HR = 64;                  // epilogue staging (2 row halves)
+    static_assert(HR * LDT * 4 <= NBUF * STAGE, "staging fits");
+    __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+    const int64_t nbx = (g.M + BM - 1) / BM, nby = (g.N + BN - 1) / BN;
+    const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
+    int64_t L = PERSIST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+    const int64_t Lstep = PERSIST ? (int64_t)gridDim.x : total;
+    const int nk = g.K / BK;
+    float* const Ts = reinterpret_cast<float*>(smem);
+    int soff[CPT];
+    uint32_t lrow[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = tid + 256 * u;
+        soff[u] = x3_soff<BK>(c / KCH, c % KCH);
+    }
+    for (; L < total; L += Lstep) {
+        const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
+        const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+        const int64_t bz = T / per_batch, Tt = T - bz * per_batch;
+        const int64_t m0 = (Tt / nby) * BM;
+        const int n0 = (int)(Tt % nby) * BN;
+        __amdgpu_buffer_rsrc_t ra[3], rb[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            ra[pl] = make_rsrc(g.a + pl * g.psa + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 2);
+            rb[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + (int64_t)n0 * g.K, (uint64_t)(g.N - n0) * g.K * 2);
+        }
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int c = tid + 256 * u;
+            lrow[u] = (uint32_t)((c / KCH) * g.K + (c % KCH) * 8) * 2u;
+        }
+        uint4 va[3][CPT], vb[3][CPT];
+        auto load = [&](int kt) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+                for (int u = 0; u < CPT; ++u) {
+                    const int off = (int)(lrow[u] + (uint32_t)kt * (BK * 2));
+                    va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
+                    vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
+                }
+        };
+        auto store = [&](int buf) {
+            char* As = smem + buf * STAGE;
+            char* Bs = As + 3 * PLA;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+                for (int u = 0; u < CPT; ++u) {
+                    *reinterpret_cast<uint4*>(As + q * PLA + soff[u]) = va[q][u];
+                    *reinterpret_cast<uint4*>(Bs + q * PLB + soff[u]) = vb[q][u];
+                }
+        };
+        floatx16 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+        load(0);
+        store(0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) load(kt + 1);
+            const char* As = smem + (NBUF == 2 ? (kt & 1) : 0) * STAGE;
+            const char* Bs = As + 3 * PLA;
+#pragma unroll
+            for (int s16 = 0; s16 < BK / 16; ++s16) {
+                // lane (l32, h): row l32 of its 32-row blocks, k = 16 s16 + 8h .. +7
+                bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int off = x3_soff<BK>(wm * TM * 32 + i * 32 + l32, 2 * s16 + h);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * PLA + off);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int off = x3_soff<BK>(wn * TN * 32 + j * 32 + l32, 2 * s16 + h);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PLB + off);
+                }
+                // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        floatx16 c = acc[i][j];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
+                    }
+            }
+            if constexpr (NBUF == 2) {
+                // the other stage was last read in iteration kt-1, before its closing barrier
+                if (kt + 1 < nk) store((kt + 1) & 1);
+                __syncthreads();
+            } else {
+                __syncthreads();
+                if (kt + 1 < nk) {
+                    store(0);
+                    __syncthreads();
+                }
+            }
+        }
+        // epilogue: two 64-row halves staged through LDS, float4 row stores
+        float* const cb = g.c + bz * g.bsc;
+        for (int hf = 0; hf < 2; ++hf) {
+            if (hf) __syncthreads();
+            if (wm == hf) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            Ts[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * TN * 32 + j * 32 + l32] =
+                                acc[i][j][r];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < HR * (BN / 4) / 256; ++q) {
+                const int idx = tid + 256 * q;
+                const int row = idx / (BN / 4), c4 = idx % (BN / 4);
+                const int64_t m = m0 + hf * HR + row;
+                const int n = n0 + c4 * 4;
+                if (m < g.M && n < g.N)
+                    st4(cb + m * g.N + n, *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4));
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // M3D_WINO_NZ = 2 selects the F(2x2x2) tiles (A/B testing; default 4: F(2x2x4))
@@ -1530,27 +1939,81 @@ extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t 
     for (int nz : {wino_nz(), wino_wgrad_nz(), wino_dgrad_nz()}) {
         const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz);
         const size_t P = (size_t)wino_points(nz);
-        const size_t b = al(sizeof(float) * P * (size_t)Cin * Cout) + al(sizeof(float) * P * (size_t)g.T * Cin) +
-                         al(sizeof(float) * P * (size_t)g.T * Cout);
+        const size_t eb = gemm_x3_env() ? 6 : 4;      // X3: V and U hold three bf16 planes
+        const size_t wt = gemm_x3_env() ? al(sizeof(float) * 27 * (size_t)Cin * Cout) : 0;
+        const size_t b = wt + al(eb * P * (size_t)Cin * Cout) + al(eb * P * (size_t)g.T * Cin) +
+                         al(eb * P * (size_t)g.T * Cout);
         best = b > best ? b : best;
     }
     return best;
 }
 
-struct WinoWs { float *V, *U, *M; };
+struct WinoWs { float *V, *U, *M, *WT; };
+// [WT: X3 only, the transposed kernel][V][U][M]
 static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, int nz = -1) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t P = (size_t)wino_points(nz < 0 ? wino_nz() : nz);
     char* p = (char*)ws;
     WinoWs w;
-    w.V = (float*)p; p += al(sizeof(float) * P * (size_t)Cin * Cout);
-    w.U = (float*)p; p += al(sizeof(float) * P * (size_t)g.T * Cin);
+    w.WT = (float*)p;
+    if (gemm_x3_env()) p += al(sizeof(float) * 27 * (size_t)Cin * Cout);
+    const size_t eb = gemm_x3_env() ? 6 : 4;
+    w.V = (float*)p; p += al(eb * P * (size_t)Cin * Cout);
+    w.U = (float*)p; p += al(eb * P * (size_t)g.T * Cin);
     w.M = (float*)p;
     return w;
 }
 
+#define WINO_LAUNCH_NZ_X3(nz, kern, ...)                                         \
+    do {                                                                         \
+        if ((nz) == 4) hipLaunchKernelGGL((kern<4, true>), __VA_ARGS__);         \
+        else hipLaunchKernelGGL((kern<2, true>), __VA_ARGS__);                   \
+    } while (0)
+
+// M3D_X3_BK (16 | 32) and M3D_X3_PERSIST (0 | 1): x3_gemm_kernel variant (A/B)
+static int x3_bk_env() {
+    static int v = [] { const char* e = getenv("M3D_X3_BK"); return e && atoi(e) == 16 ? 16 : 32; }();
+    return v;
+}
+static int x3_occ3_env() {
+    static int v = [] { const char* e = getenv("M3D_X3_OCC3"); return e ? atoi(e) : 1; }();
+    return v;
+}
+static int x3_persist_env() {
+    static int v = [] { const char* e = getenv("M3D_X3_PERSIST"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
+// the P point GEMMs M[xi] = U[xi] V[xi] on split planes (U: T x K, V: N x K)
+static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipStream_t s) {
+    X3G q;
+    q.a = reinterpret_cast<const unsigned short*>(ws.U);
+    q.b = reinterpret_cast<const unsigned short*>(ws.V);
+    q.c = ws.M;
+    q.M = T; q.K = K; q.N = N; q.nbatch = P;
+    q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
+    q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
+    const int64_t tiles = ((T + 127) / 128) * ((N + 127) / 128) * P;
+    const bool bk16 = x3_bk_env() == 16;
+    const bool occ3 = !bk16 && x3_occ3_env();
+    const int64_t resident = (int64_t)num_cus() * (bk16 || occ3 ? 3 : 2);
+    const bool persist = x3_persist_env() && tiles > 2 * resident;
+    const dim3 grid(persist ? (unsigned)(resident / 8 * 8) : (unsigned)tiles);
+    if (bk16) {
+        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<16, true>), grid, dim3(256), 0, s, q);
+        else hipLaunchKernelGGL((x3_gemm_kernel<16, false>), grid, dim3(256), 0, s, q);
+    } else if (occ3) {
+        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<32, true, 3>), grid, dim3(256), 0, s, q);
+        else hipLaunchKernelGGL((x3_gemm_kernel<32, false, 3>), grid, dim3(256), 0, s, q);
+    } else {
+        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<32, true>), grid, dim3(256), 0, s, q);
+        else hipLaunchKernelGGL((x3_gemm_kernel<32, false>), grid, dim3(256), 0, s, q);
+    }
+}
+
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
     if (wino_nz() != wino_wgrad_nz()) return 0;       // forward tiles differ from the wgrad's: nothing to keep
+    if (gemm_x3_env()) return 0;                        // the forward's U is in bf16 planes
     return sizeof(float) * wino_points() * (size_t)wino_geom(B, H, W, OD, OD, 1).T * (size_t)Cin;
 }
 
@@ -1565,6 +2028,22 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
         return einval("conv3d winograd: workspace too small");
     const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
+    if (gemm_x3_env() && !u_keep) {
+        float* wt = ws.WT;
+        hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
+                           dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
+        WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
+                          (int)Cin, (int)Cout, 0, ws.V);
+        WINO_LAUNCH_NZ_X3(wino_nz(), wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
+                          (int)Cin, ws.U);
+        wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s);
+        Epi o{};
+        o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
+        o.res_mode = residual ? 1 : 0; o.relu = relu; o.z = z_out; o.y = y; o.ldy = Cout;
+        WINO_LAUNCH(wino_output_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, s, ws.M,
+                    g, (int)Cout, o);
+        return check_launch("conv3d winograd fwd (x3)");
+    }
     if (u_keep) ws.U = u_keep;
     WINO_LAUNCH(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
                        (int)Cin, (int)Cout, 0, ws.V);
@@ -1621,6 +2100,18 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
     WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz);
+    if (gemm_x3_env()) {
+        WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+                          (int)Cin, (int)Cout, 1, ws.V);
+        WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+                          (int)Cout, ws.U);
+        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), st(s));
+        Epi o{};
+        o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
+        WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
+                       g, (int)Cin, o);
+        return check_launch("conv3d winograd bwd-data (x3)");
+    }
     WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
                        (int)Cin, (int)Cout, 1, ws.V);
     WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,

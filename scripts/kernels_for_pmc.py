@@ -19,6 +19,21 @@ S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 NR = 128 if S == 128 else 512          # configs[2] / configs[3] ROI counts (bench.py)
 if leg == "gemm":
     print(bench.time_dominant_kernel(S, reps=3))
+elif leg == "winofwd":
+    # rpn_conv_shared1 on P2 as a Winograd conv through the C-ABI (M3D_GEMM_X3 picks the GEMM)
+    from m3d import _lib
+    L = _lib.load()
+    B, H, W, D, Cin, Cout = 1, S // 4, S // 4, S, 256, 512
+    x = torch.randn((B, H, W, D, Cin), device="cuda")
+    w = torch.randn((3, 3, 3, Cin, Cout), device="cuda") / (27 * Cin) ** 0.5
+    y = torch.empty((B, H, W, D, Cout), device="cuda")
+    nb = L.m3d_conv3d_wino_workspace_bytes(B, H, W, D, D, Cin, Cout)
+    ws = torch.empty(nb // 4 + 64, device="cuda")
+    for _ in range(3):
+        _lib.check(L.m3d_conv3d_fwd_wino(x.data_ptr(), B, H, W, D, Cin, w.data_ptr(), Cout, D, 1, None, None,
+                                         None, None, 0, None, y.data_ptr(), ws.data_ptr(), nb, _lib.stream()),
+                   "wino")
+    torch.cuda.synchronize()
 elif leg == "infer":
     print(bench.mrcnn_inference_leg(S, 3, 1, torch.device("cuda")))
 else:
