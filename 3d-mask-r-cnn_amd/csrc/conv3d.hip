@@ -1678,6 +1678,21 @@ extern "C" int m3d_gemm_f32(const float* A, const float* Bm, float* C, int64_t b
     return check_launch("m3d_gemm_f32");
 }
 
+extern "C" int m3d_gemm_wgrad_f32(const float* A, const float* Bm, float* C, int64_t batch, int64_t M,
+                                  int64_t K, int64_t N, m3d_stream_t s) {
+    if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm_wgrad: dimensions must be positive");
+    if (K % 4 || N % 4) return einval("gemm_wgrad: K and N must be multiples of 4");
+    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
+    if (M >= 0x7FFFFFFF || M * K >= lim || M * N >= lim || K * N >= lim)
+        return einval("gemm_wgrad: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p = wino_gemm_p(A, M, (int)K, nullptr, (int)N);
+    p.bsw = M * N;                      // B batch stride
+    p.bsy = K * N;                      // C batch stride
+    if (N <= 64) launch_wgrad<128, 64, 2, 2, true>(p, Bm, C, st(s), (int)batch);
+    else launch_wgrad<128, 128, 2, 2, true>(p, Bm, C, st(s), (int)batch);
+    return check_launch("m3d_gemm_wgrad_f32");
+}
+
 static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, int32_t kh,
                       int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
                       int32_t sy, int32_t sx, int32_t sz) {

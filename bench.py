@@ -62,13 +62,13 @@ def _pmc_traffic(kernel_key):
         return None
 
 
-def wino_gemm_shape(S):
-    """The step's largest launch of its dominant kernel (conv_gemm_kernel):
-    the 16*(NZ+2) batched Winograd point-wise GEMMs of rpn_conv_shared1
-    (3x3x3, 256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles,
-    K = 256, N = 512 (NZ = 4 by default: 96 GEMMs)."""
-    from m3d import _lib
-    nz = int(_lib.load().m3d_conv3d_wino_tile_z())
+def wgrad_gemm_shape(S):
+    """The step's largest launch of its dominant kernel (conv_wgrad_kernel, 28 %
+    of the step's kernel time, profiles/r01p_bench_kernels_128.txt): the 64
+    batched Winograd weight-gradient GEMMs of rpn_conv_shared1 (3x3x3, 256->512)
+    on P2 [S/4, S/4, S] -- F(2x2x2) tiles (the weight gradient keeps NZ = 2,
+    conv3d.hip wino_wgrad_nz), reduction over M = T tiles, K = 256, N = 512."""
+    nz = 4 if os.environ.get("M3D_WINO_WGRAD_NZ") == "4" else 2
     q = S // 4
     T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
     return 16 * (nz + 2), T, 256, 512
@@ -77,26 +77,52 @@ def wino_gemm_shape(S):
 def time_dominant_kernel(S, reps=5):
     from m3d import _lib
     L = _lib.load()
-    nb, T, K, N = wino_gemm_shape(S)
+    nb, T, K, N = wgrad_gemm_shape(S)
     g = torch.Generator(device="cuda").manual_seed(5)
     A = torch.randn((nb, T, K), device="cuda", generator=g)
-    Bm = torch.randn((nb, K, N), device="cuda", generator=g) * 0.05
-    C = torch.empty((nb, T, N), device="cuda")
+    Bm = torch.randn((nb, T, N), device="cuda", generator=g) * 0.05
+    C = torch.zeros((nb, K, N), device="cuda")
 
     def launch():
-        _lib.check(L.m3d_gemm_f32(A.data_ptr(), Bm.data_ptr(), C.data_ptr(), nb, T, K, N, None, 0, 0,
-                                  _lib.stream()), "gemm")
+        _lib.check(L.m3d_gemm_wgrad_f32(A.data_ptr(), Bm.data_ptr(), C.data_ptr(), nb, T, K, N,
+                                        _lib.stream()), "gemm_wgrad")
     t = _event_time(launch, reps)
     flops = 2.0 * nb * T * K * N
-    key = f"wino_gemm_rpn_shared1_S{S}"
+    key = f"wino_wgrad_gemm_rpn_shared1_S{S}"
     return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
             "traffic": _pmc_traffic(key),
-            "kernel": f"conv_gemm_kernel<128,128> (fp32 MFMA): {nb} batched Winograd GEMMs of "
-                      f"rpn_conv_shared1 on P2, M={T} K={K} N={N}",
+            "kernel": f"conv_wgrad_kernel<128,128> (fp32 MFMA): {nb} batched Winograd weight-gradient "
+                      f"GEMMs of rpn_conv_shared1 on P2, reduction M={T}, K={K}, N={N}",
             "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
-            "algorithmic_bytes_per_launch": 4.0 * nb * (T * K + K * N + T * N),
+            "algorithmic_bytes_per_launch": 4.0 * nb * (T * K + T * N + K * N),
             "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
+
+
+def time_wino_fwd(S, reps=5):
+    """rpn_conv_shared1 (3x3x3, 256->512) on P2 as the whole F(2x2x4) Winograd
+    forward (weight + input transforms, 96 point GEMMs on the exact bf16 split
+    (x3_gemm_kernel), output transform): time and direct-conv-equivalent rate."""
+    from m3d import _lib
+    L = _lib.load()
+    B, H, W, D, Cin, Cout = 1, S // 4, S // 4, S, 256, 512
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.randn((B, H, W, D, Cin), device="cuda", generator=g)
+    w = torch.randn((3, 3, 3, Cin, Cout), device="cuda", generator=g) / (27 * Cin) ** 0.5
+    y = torch.empty((B, H, W, D, Cout), device="cuda")
+    nb = L.m3d_conv3d_wino_workspace_bytes(B, H, W, D, D, Cin, Cout)
+    ws = torch.empty(nb // 4 + 64, device="cuda")
+
+    def launch():
+        _lib.check(L.m3d_conv3d_fwd_wino(x.data_ptr(), B, H, W, D, Cin, w.data_ptr(), Cout, D, 1, None, None,
+                                         None, None, 0, None, y.data_ptr(), ws.data_ptr(), nb, _lib.stream()),
+                   "wino fwd")
+    t = _event_time(launch, reps)
+    nz = int(L.m3d_conv3d_wino_tile_z())
+    T = ((H + 1) // 2) * ((W + 1) // 2) * ((D + nz - 1) // nz)
+    return {"ms": round(t * 1e3, 4),
+            "gemm_tflops": round(2.0 * 16 * (nz + 2) * T * Cin * Cout / t / 1e12, 2),
+            "direct_conv_equivalent_tflops": round(2.0 * H * W * D * 27 * Cin * Cout / t / 1e12, 2)}
 
 
 def time_direct_conv(model, fmaps, reps=5):
@@ -509,6 +535,7 @@ def main():
         try:
             out["roofline"] = time_dominant_kernel(S)
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
+            out["roofline"]["wino_fwd_conv"] = time_wino_fwd(S)
         except Exception as e:  # report, never hide
             out["roofline"] = {"error": repr(e)}
         try:

@@ -214,10 +214,20 @@ int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int
 /* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
  * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],
  * C [M][N] row-major, batches contiguous; N multiple of 4.  The Winograd
- * point-wise products above are exactly this call with batch = 64 (bench.py
- * prices the RPN head's largest one). */
+ * point-wise products above run this f32-MFMA kernel with M3D_GEMM_X3=0 (by
+ * default they run x3_gemm_kernel on the exact bf16 split, conv3d.hip). */
 int m3d_gemm_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
                  int64_t N, const float* bias, int32_t relu, int32_t accumulate, m3d_stream_t s);
+
+/* Batched weight-gradient GEMM on the conv weight-gradient kernel
+ * (conv_wgrad_kernel, fp32 MFMA, M split over workgroups, fp32 atomics):
+ * for b < batch, C[b] [K][N] += A[b]^T B[b] with A [M][K], B [M][N], batches
+ * contiguous; K, N multiples of 4.  The Winograd weight gradient (Conv3D's
+ * kernel gradient, TF Conv3DBackpropFilterV2 in the reference graph) is this
+ * call with batch = 64 on the transformed input and output gradient; bench.py
+ * prices the RPN head's largest one. */
+int m3d_gemm_wgrad_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
+                       int64_t N, m3d_stream_t s);
 
 /* Strided batched GEMM: for b < batch, C + b*bsc [M][N] (+)= act(A[b] B[b] + bias)
  * with A[b] = A + b*bsa (rows of stride lda >= K), B[b] = B + b*bsb [K][N]; act

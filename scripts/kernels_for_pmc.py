@@ -1,6 +1,6 @@
 """Runs ONE priced launch of bench.py a few times for the rocprofv3 --pmc
 passes of scripts/gpu_prof.sh:  kernels_for_pmc.py LEG [S]
-  gemm    the dominant kernel's largest launch (batched Winograd GEMM of rpn_conv_shared1)
+  gemm    the dominant kernel's largest launch (batched Winograd weight-gradient GEMM of rpn_conv_shared1)
   direct  rpn_conv_shared1 as a direct implicit-GEMM conv on P2
   roi7 / roi14  PyramidROIAlign 7^3 / 14^3 at configs[2] shapes
   infer   MaskRCNN inference (configs[3]) x3 after one warm-up

@@ -249,3 +249,20 @@ def test_winograd_z_halo_geometry(cuda, D, OD, pz):
                                               dw2.data_ptr(), ws.data_ptr(), nb, _lib.stream()))
     assert torch.equal(y2, y)
     close(dw2, wr.grad)
+
+
+@pytest.mark.parametrize("nb,M,K,N", [(3, 200, 64, 96), (2, 1000, 128, 36), (64, 512, 256, 512)])
+def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
+    """m3d_gemm_wgrad_f32 (the Winograd weight-gradient GEMM launch bench.py
+    prices): C[b] += A[b]^T B[b] against a float64 torch bmm, ragged M/K/N tiles."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn((nb, M, K), generator=g)
+    Bm = torch.randn((nb, M, N), generator=g)
+    C0 = torch.randn((nb, K, N), generator=g)
+    ref = torch.bmm(A.double().transpose(1, 2), Bm.double()) + C0.double()
+    Ad, Bd, Cd = (t.to(cuda).contiguous() for t in (A, Bm, C0))
+    _lib.check(L.m3d_gemm_wgrad_f32(Ad.data_ptr(), Bd.data_ptr(), Cd.data_ptr(), nb, M, K, N, _lib.stream()),
+               "gemm_wgrad")
+    close(Cd, ref)
