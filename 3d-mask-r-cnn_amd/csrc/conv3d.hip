@@ -660,16 +660,27 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wi = wave / WJ, wj = wave % WJ;
-    const int k0 = blockIdx.x * BI;
-    const int n0 = blockIdx.y * BJ;
+    // XCD-aware order: the dispatcher deals consecutive workgroups round-robin
+    // to the 8 XCDs; remap so each XCD runs a contiguous range, i.e. the (K,N)
+    // tiles of one m-range share their A / dZ rows through one L2 (without it
+    // every tile of an m-range sat on a different XCD and re-read the rows
+    // from HBM: 2.7x the algorithmic bytes)
+    const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
+    const int64_t total = gxy * gridDim.z;
+    const int64_t Lb = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int bz_ = (int)(Lt / gxy), rem = (int)(Lt % gxy);
+    const int k0 = (rem % gridDim.x) * BI;
+    const int n0 = (rem / gridDim.x) * BJ;
     const int64_t nsplit = (p.M + m_per_split - 1) / m_per_split;
-    const int64_t batch = blockIdx.z / nsplit;
+    const int64_t batch = bz_ / nsplit;
     if (batch) {
         p.a += batch * p.bsa;
         dz += batch * p.bsw;
         dw += batch * p.bsy;
     }
-    const int64_t ms = (int64_t)(blockIdx.z % nsplit) * m_per_split;
+    const int64_t ms = (int64_t)(bz_ % nsplit) * m_per_split;
     int64_t me = ms + m_per_split;
     if (me > p.M) me = p.M;
     if (ms >= me) return;
