@@ -841,20 +841,19 @@ static int num_cus() {
     return v;
 }
 
-// M3D_GEMM_X3 (bit mask, default 1): fp32 GEMMs on the exact 3-way bf16 split
+// M3D_GEMM_X3 (bit mask, default 5): fp32 GEMMs on the exact 3-way bf16 split
 // (6 bf16 MFMAs per product, see split3) instead of v_mfma_f32_32x32x2_f32.
 // bit 0: Winograd fwd / bwd-data point GEMMs on operands pre-split by the
 // transforms (x3_gemm_kernel; measured 39.9 -> 37.9 ms/step at 128^3, GEMM
 // error vs fp64 below the f32 MFMA's: scripts/x3_accuracy.py); bit 1:
-// implicit-GEMM convs splitting in the LDS store (slower: off).
-static int gemm_x3_env() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 1; }();
-    return v & 1;
-}
-static int conv_x3_env() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? (atoi(e) >> 1) & 1 : 0; }();
+// implicit-GEMM convs splitting in the LDS store (slower: off); bit 2: the
+// Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step).
+static int x3_mask() {
+    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 5; }();
     return v;
 }
+static int gemm_x3_env() { return x3_mask() & 1; }
+static int conv_x3_env() { return (x3_mask() >> 1) & 1; }
 
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
 static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
@@ -961,6 +960,159 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
                        mper);
 }
 
+
+// ---- weight-gradient GEMM on the exact bf16 split (plain batched rows) ----
+// C[b][k][n] += sum_m A[b][m][k] B[b][m][n] (the Winograd weight gradient:
+// A = transformed input, B = transformed output gradient), split3 of both
+// operands in the LDS store.  The reduction index m is the slow axis of both
+// operands, so each loader thread takes 8 consecutive m rows of one float4
+// column and writes, per column, the 8 m values as one 16-byte k-chunk of the
+// [row = k or n][32 m] planes (same swizzled image as x3_gemm_kernel).
+// Threads 0-127 load A, 128-255 load B.  grid (K/128, N/128, splits * batch)
+// with the XCD-contiguous order of conv_wgrad_kernel; fp32 atomics out.
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restrict__ A,
+                                                            const float* __restrict__ Bm,
+                                                            float* __restrict__ C, int64_t M, int K, int N,
+                                                            int64_t m_per_split, int64_t bsa, int64_t bsb,
+                                                            int64_t bsc) {
+    constexpr int BI = 128, BJ = 128, TI = 2, TJ = 2, BKM = 32;
+    constexpr int PL = 128 * BKM * 2;                    // bytes per plane (128 rows x 64 B)
+    __shared__ __attribute__((aligned(16))) char smem[6 * PL];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave >> 1, wj = wave & 1, h = lane >> 5, l32 = lane & 31;
+    const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
+    const int64_t total = gxy * gridDim.z;
+    const int64_t Lb = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int bz = (int)(Lt / gxy), rem = (int)(Lt % gxy);
+    const int k0 = (rem % gridDim.x) * BI;
+    const int n0 = (rem / gridDim.x) * BJ;
+    const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
+    const int64_t batch = bz / nsplit;
+    A += batch * bsa;
+    Bm += batch * bsb;
+    C += batch * bsc;
+    const int64_t ms = (int64_t)(bz % nsplit) * m_per_split;
+    const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
+    if (ms >= me) return;
+    // loader role: operand, float4 column, 8-row group
+    const bool isB = tid >= 128;
+    const int lt = tid & 127, c4 = lt & 31, grp = lt >> 5;
+    const int ld = isB ? N : K;
+    const int col = (isB ? n0 : k0) + c4 * 4;
+    const bool colok = col < ld;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(isB ? (const void*)Bm : (const void*)A, (uint64_t)M * ld * 4);
+    char* const Pb = smem + (isB ? 3 * PL : 0);
+    float4 v[8];
+    auto load = [&](int64_t mb) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int64_t m = mb + grp * 8 + r;
+            v[r] = bload4(rs, (colok && m < me) ? (uint32_t)(m * ld + col) * 4u : M3D_OOB);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t hh[8], mm[8], ll[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) split3(f4get(v[r], c), hh[r], mm[r], ll[r]);
+            const int off = x3_off(c4 * 4 + c, grp * 8);
+            *reinterpret_cast<uint4*>(Pb + off) =
+                make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+            *reinterpret_cast<uint4*>(Pb + PL + off) =
+                make_uint4(mm[0] | (mm[1] << 16), mm[2] | (mm[3] << 16), mm[4] | (mm[5] << 16), mm[6] | (mm[7] << 16));
+            *reinterpret_cast<uint4*>(Pb + 2 * PL + off) =
+                make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+        }
+    };
+    floatx16 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const char* const As = smem;
+    const char* const Bs = smem + 3 * PL;
+    const int nchunks = (int)((me - ms + BKM - 1) / BKM);
+    load(ms);
+    store();
+    __syncthreads();
+    for (int t = 0; t < nchunks; ++t) {
+        if (t + 1 < nchunks) load(ms + (int64_t)(t + 1) * BKM);
+#pragma unroll
+        for (int s16 = 0; s16 < 2; ++s16) {
+            bf16x8 af[TI][3], bfr[TJ][3];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) {
+                const int off = x3_off(wi * TI * 32 + i * 32 + l32, 16 * s16 + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * PL + off);
+            }
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                const int off = x3_off(wj * TJ * 32 + j * 32 + l32, 16 * s16 + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PL + off);
+            }
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) {
+                    floatx16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
+                }
+        }
+        __syncthreads();
+        if (t + 1 < nchunks) {
+            store();
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int n = n0 + wj * TJ * 32 + j * 32 + l32;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = k0 + wi * TI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (k < K) unsafeAtomicAdd(C + (int64_t)k * N + n, acc[i][j][r]);
+            }
+        }
+}
+
+// M3D_GEMM_X3 bit 2: the batched Winograd weight-gradient GEMMs on x3_wgrad_kernel
+static int wgrad_x3_env() { return (x3_mask() >> 2) & 1; }
+
+// C[b] += A[b]^T B[b]: A [M][K], B [M][N], C [K][N], batch strides bsa/bsb/bsc
+static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M, int K, int N, int nbatch,
+                            int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
+    const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
+    int64_t splits = (1024 + tiles - 1) / tiles;
+    const int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
+    const int64_t max_splits = (M + minm - 1) / minm;
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int64_t mper = (M + splits - 1) / splits;
+    mper = (mper + 31) / 32 * 32;
+    splits = (M + mper - 1) / mper;
+    dim3 grid((unsigned)((K + 127) / 128), (unsigned)((N + 127) / 128), (unsigned)(splits * nbatch));
+    static const int occ = [] { const char* e = getenv("M3D_X3W_OCC"); return e && atoi(e) == 3 ? 3 : 2; }();
+    if (occ == 2)
+        hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+    else
+        hipLaunchKernelGGL((x3_wgrad_kernel<3>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+}
 
 // =========================================================================
 // Winograd F(2x2xNZ, 3x3x3) for stride-1 'same' 3x3x3 convs: F(2,3) along y
@@ -1696,6 +1848,10 @@ extern "C" int m3d_gemm_wgrad_f32(const float* A, const float* Bm, float* C, int
     const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
     if (M >= 0x7FFFFFFF || M * K >= lim || M * N >= lim || K * N >= lim)
         return einval("gemm_wgrad: operand larger than 4 GiB (32-bit buffer offsets)");
+    if (wgrad_x3_env() && N > 64) {
+        launch_wgrad_x3(A, Bm, C, M, (int)K, (int)N, (int)batch, M * K, M * N, K * N, st(s));
+        return check_launch("m3d_gemm_wgrad_f32 (x3)");
+    }
     ConvP p = wino_gemm_p(A, M, (int)K, nullptr, (int)N);
     p.bsw = M * N;                      // B batch stride
     p.bsy = K * N;                      // C batch stride
@@ -2037,6 +2193,41 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     }
 }
 
+// x -> three bf16 planes of split3 (planes at x3 + p * n), one element per thread
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, int64_t n,
+                                                     unsigned short* __restrict__ x3) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t h, m, l;
+    split3(x[i], h, m, l);
+    x3[i] = (unsigned short)h;
+    x3[n + i] = (unsigned short)m;
+    x3[2 * n + i] = (unsigned short)l;
+}
+
+extern "C" int m3d_split3_f32(const float* x, int64_t n, uint16_t* x3, m3d_stream_t s) {
+    if (n <= 0) return einval("split3: n must be positive");
+    hipLaunchKernelGGL(split3_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st(s), x, n,
+                       reinterpret_cast<unsigned short*>(x3));
+    return check_launch("split3_kernel");
+}
+
+extern "C" int m3d_gemm_x3(const uint16_t* A3, const uint16_t* B3, float* C, int64_t batch, int64_t M,
+                           int64_t K, int64_t N, m3d_stream_t s) {
+    if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm_x3: dimensions must be positive");
+    if (K % 32 || N % 4) return einval("gemm_x3: K must be a multiple of 32 and N of 4");
+    if (M > 0x7FFFFFFF || M * K * 2 >= 0xFFFFFFF0LL || N * K * 2 >= 0xFFFFFFF0LL || M * N * 4 >= 0xFFFFFFF0LL)
+        return einval("gemm_x3: operand larger than 4 GiB (32-bit buffer offsets)");
+    WinoWs ws;
+    ws.U = (float*)const_cast<uint16_t*>(A3);
+    ws.V = (float*)const_cast<uint16_t*>(B3);
+    ws.M = C;
+    ws.WT = nullptr;
+    wino_gemm_x3(ws, M, (int)K, (int)N, (int)batch, st(s));
+    return check_launch("m3d_gemm_x3");
+}
+
+
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
     if (wino_nz() != wino_wgrad_nz()) return 0;       // forward tiles differ from the wgrad's: nothing to keep
     if (gemm_x3_env()) return 0;                        // the forward's U is in bf16 planes
@@ -2173,11 +2364,16 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
                            (int)Cin, ws.U);
     WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
-    ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, nullptr, (int)Cout);
-    p.bsw = g.T * Cout;                 // dz (DY) batch stride
-    p.bsy = (int64_t)Cin * Cout;        // dW_hat batch stride
-    if (Cout <= 64) launch_wgrad<128, 64, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
-    else launch_wgrad<128, 128, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
+    if (wgrad_x3_env() && Cout > 64) {
+        launch_wgrad_x3(ws.U, ws.M, ws.V, g.T, (int)Cin, (int)Cout, wino_points(nz), g.T * Cin, g.T * Cout,
+                        (int64_t)Cin * Cout, st(s));
+    } else {
+        ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, nullptr, (int)Cout);
+        p.bsw = g.T * Cout;                 // dz (DY) batch stride
+        p.bsy = (int64_t)Cin * Cout;        // dW_hat batch stride
+        if (Cout <= 64) launch_wgrad<128, 64, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
+        else launch_wgrad<128, 128, 2, 2, true>(p, ws.M, ws.V, st(s), wino_points(nz));
+    }
     WINO_LAUNCH_NZ(nz, wino_wgrad_out_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s),
                        ws.V, (int)Cin, (int)Cout, dw);
     return check_launch("conv3d winograd bwd-weight");

@@ -29,6 +29,11 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "volumes/sec fwd+bwd @128³ & 256³, 1/2/4/8 MI355X; 3D ROIAlign GB/s vs HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TFLOPS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICROARCH.md)
+# bf16 MFMA dense peak: 256 CUs x 4 SIMDs x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16,
+# 32 cycles) x 2.4 GHz; the X3 kernels run 6 of them per fp32 product, so their
+# fp32-FLOP ceiling is a sixth of it
+BF16_MFMA_PEAK_TFLOPS = 2516.6
+X3_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
 
 
 def log(*a):
@@ -63,8 +68,7 @@ def _pmc_traffic(kernel_key):
 
 
 def wgrad_gemm_shape(S):
-    """The step's largest launch of its dominant kernel (conv_wgrad_kernel, 28 %
-    of the step's kernel time, profiles/r01p_bench_kernels_128.txt): the 64
+    """The largest weight-gradient launch of the step: the 64
     batched Winograd weight-gradient GEMMs of rpn_conv_shared1 (3x3x3, 256->512)
     on P2 [S/4, S/4, S] -- F(2x2x2) tiles (the weight gradient keeps NZ = 2,
     conv3d.hip wino_wgrad_nz), reduction over M = T tiles, K = 256, N = 512."""
@@ -74,7 +78,56 @@ def wgrad_gemm_shape(S):
     return 16 * (nz + 2), T, 256, 512
 
 
+def wino_gemm_shape(S):
+    """The step's largest launch of its dominant kernel (x3_gemm_kernel, 19 % of
+    the step's kernel time, profiles/r01r_bench_kernels_128.txt): the
+    16*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
+    256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles, K = 256,
+    N = 512 (NZ = 4 by default: 96 GEMMs)."""
+    from m3d import _lib
+    nz = int(_lib.load().m3d_conv3d_wino_tile_z())
+    q = S // 4
+    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
+    return 16 * (nz + 2), T, 256, 512
+
+
 def time_dominant_kernel(S, reps=5):
+    """x3_gemm_kernel on the priced shape through m3d_gemm_x3 (operands split
+    once, untimed, as the Winograd transforms do in the step)."""
+    from m3d import _lib
+    L = _lib.load()
+    nb, T, K, N = wino_gemm_shape(S)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn((nb, T, K), device="cuda", generator=g)
+    Bt = torch.randn((nb, N, K), device="cuda", generator=g) * 0.05
+    A3 = torch.empty(3 * A.numel(), dtype=torch.int16, device="cuda")
+    B3 = torch.empty(3 * Bt.numel(), dtype=torch.int16, device="cuda")
+    _lib.check(L.m3d_split3_f32(A.data_ptr(), A.numel(), A3.data_ptr(), _lib.stream()), "split3")
+    _lib.check(L.m3d_split3_f32(Bt.data_ptr(), Bt.numel(), B3.data_ptr(), _lib.stream()), "split3")
+    del A, Bt
+    C = torch.empty((nb, T, N), device="cuda")
+
+    def launch():
+        _lib.check(L.m3d_gemm_x3(A3.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, T, K, N, _lib.stream()),
+                   "gemm_x3")
+    t = _event_time(launch, reps)
+    flops = 2.0 * nb * T * K * N
+    key = f"wino_gemm_x3_rpn_shared1_S{S}"
+    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": X3_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4),
+            "traffic": _pmc_traffic(key),
+            "kernel": f"x3_gemm_kernel (fp32 GEMM as 6 bf16 MFMAs per product on the exact 3-way split): "
+                      f"{nb} batched Winograd point GEMMs of rpn_conv_shared1 on P2, M={T} K={K} N={N}",
+            "peak_note": "bf16 MFMA dense peak 2516.6 TFLOP/s / 6; achieved counts fp32 FLOPs 2*M*K*N",
+            "f32_mfma_peak_frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
+            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
+            "algorithmic_bytes_per_launch": nb * (6.0 * (T * K + N * K) + 4.0 * T * N),
+            "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
+
+
+def time_wgrad_gemm(S, reps=5):
+    """The Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2 through
+    m3d_gemm_wgrad_f32 (x3_wgrad_kernel by default)."""
     from m3d import _lib
     L = _lib.load()
     nb, T, K, N = wgrad_gemm_shape(S)
@@ -88,15 +141,11 @@ def time_dominant_kernel(S, reps=5):
                                         _lib.stream()), "gemm_wgrad")
     t = _event_time(launch, reps)
     flops = 2.0 * nb * T * K * N
-    key = f"wino_wgrad_gemm_rpn_shared1_S{S}"
-    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": _pmc_traffic(key),
-            "kernel": f"conv_wgrad_kernel<128,128> (fp32 MFMA): {nb} batched Winograd weight-gradient "
-                      f"GEMMs of rpn_conv_shared1 on P2, reduction M={T}, K={K}, N={N}",
-            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
-            "algorithmic_bytes_per_launch": 4.0 * nb * (T * K + T * N + K * N),
-            "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
+    return {"achieved": round(flops / t / 1e12, 2), "unit": "TFLOP/s",
+            "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4), "peak": X3_PEAK_TFLOPS,
+            "f32_mfma_peak_frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
+            "avg_launch_ms": round(t * 1e3, 4), "shape": f"{nb} x (M={T}) K={K} N={N}",
+            "traffic": _pmc_traffic(f"wino_wgrad_gemm_rpn_shared1_S{S}")}
 
 
 def time_wino_fwd(S, reps=5):
@@ -536,6 +585,7 @@ def main():
             out["roofline"] = time_dominant_kernel(S)
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
             out["roofline"]["wino_fwd_conv"] = time_wino_fwd(S)
+            out["roofline"]["wgrad_gemm"] = time_wgrad_gemm(S)
         except Exception as e:  # report, never hide
             out["roofline"] = {"error": repr(e)}
         try:

@@ -229,6 +229,18 @@ int m3d_gemm_f32(const float* A, const float* B, float* C, int64_t batch, int64_
 int m3d_gemm_wgrad_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
                        int64_t N, m3d_stream_t s);
 
+/* The exact 3-way bf16 split of fp32 data (x = hi + mid + lo, each bf16; exact
+ * for normal x): x3 receives the three uint16 planes, plane p at x3 + p*n. */
+int m3d_split3_f32(const float* x, int64_t n, uint16_t* x3, m3d_stream_t s);
+
+/* Batched fp32 GEMM on split operands (x3_gemm_kernel: 6 bf16 MFMAs per
+ * product, the default for the Winograd point GEMMs above): for b < batch,
+ * C[b] [M][N] = A[b] B[b]^T with A3 the m3d_split3_f32 planes of A
+ * [batch][M][K] and B3 those of B^T [batch][N][K]; K multiple of 32, N of 4.
+ * bench.py prices the RPN head's largest launch with it. */
+int m3d_gemm_x3(const uint16_t* A3, const uint16_t* B3, float* C, int64_t batch, int64_t M, int64_t K,
+                int64_t N, m3d_stream_t s);
+
 /* Strided batched GEMM: for b < batch, C + b*bsc [M][N] (+)= act(A[b] B[b] + bias)
  * with A[b] = A + b*bsa (rows of stride lda >= K), B[b] = B + b*bsb [K][N]; act
  * 0 none / 1 ReLU / 2 sigmoid.  Split-K: batch = #K-slices of width kc (bsa =

@@ -266,3 +266,25 @@ def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
     _lib.check(L.m3d_gemm_wgrad_f32(Ad.data_ptr(), Bd.data_ptr(), Cd.data_ptr(), nb, M, K, N, _lib.stream()),
                "gemm_wgrad")
     close(Cd, ref)
+
+
+def test_split3_exact_and_gemm_x3(cuda):
+    """m3d_split3_f32: hi + mid + lo == x exactly (float64 sum of the bf16
+    planes); m3d_gemm_x3 (the Winograd point-GEMM kernel) against float64."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator().manual_seed(13)
+    nb, M, K, N = 3, 300, 96, 160
+    A = torch.randn((nb, M, K), generator=g) * torch.exp(torch.randn((nb, M, K), generator=g) * 4)
+    Bt = torch.randn((nb, N, K), generator=g)
+    Ad, Bd = A.to(cuda), Bt.to(cuda)
+    A3 = torch.empty(3 * A.numel(), dtype=torch.int16, device=cuda)
+    B3 = torch.empty(3 * Bt.numel(), dtype=torch.int16, device=cuda)
+    _lib.check(L.m3d_split3_f32(Ad.data_ptr(), A.numel(), A3.data_ptr(), _lib.stream()), "split3")
+    _lib.check(L.m3d_split3_f32(Bd.data_ptr(), Bt.numel(), B3.data_ptr(), _lib.stream()), "split3")
+    planes = (A3.cpu().view(3, -1).to(torch.int32) & 0xFFFF) << 16
+    parts = planes.view(torch.float32).double()
+    assert torch.equal(parts.sum(0), A.reshape(-1).double())
+    C = torch.empty((nb, M, N), device=cuda)
+    _lib.check(L.m3d_gemm_x3(A3.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, M, K, N, _lib.stream()), "gemm_x3")
+    close(C, torch.bmm(A.double(), Bt.double().transpose(1, 2)))
