@@ -841,15 +841,16 @@ static int num_cus() {
     return v;
 }
 
-// M3D_GEMM_X3 (bit mask, default 5): fp32 GEMMs on the exact 3-way bf16 split
+// M3D_GEMM_X3 (bit mask, default 13): fp32 GEMMs on the exact 3-way bf16 split
 // (6 bf16 MFMAs per product, see split3) instead of v_mfma_f32_32x32x2_f32.
 // bit 0: Winograd fwd / bwd-data point GEMMs on operands pre-split by the
 // transforms (x3_gemm_kernel; measured 39.9 -> 37.9 ms/step at 128^3, GEMM
 // error vs fp64 below the f32 MFMA's: scripts/x3_accuracy.py); bit 1:
 // implicit-GEMM convs splitting in the LDS store (slower: off); bit 2: the
-// Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step).
+// Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step);
+// bit 3: the weight gradients of 1x1x1 stride-1 convs on the same kernel.
 static int x3_mask() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 5; }();
+    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 13; }();
     return v;
 }
 static int gemm_x3_env() { return x3_mask() & 1; }
@@ -2072,6 +2073,13 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
     const bool vec = (Cin % 4) == 0;
+    // 1x1x1 stride-1 convs: im2col is x itself, the plain weight-gradient GEMM
+    // dW += x^T dz -- on the exact bf16 split like the Winograd ones
+    if (vec && ((x3_mask() >> 3) & 1) && kh == 1 && kw == 1 && kd == 1 && sy == 1 && sx == 1 && sz == 1 &&
+        py == 0 && px == 0 && pz == 0 && OH == H && OW == W && OD == D && Cout > 64) {
+        launch_wgrad_x3(x, dz, dw, p.M, (int)Cin, (int)Cout, 1, 0, 0, 0, st(s));
+        return check_launch("x3_wgrad_kernel (1x1x1)");
+    }
     if (vec && p.K <= 64 && wgrad_k64_env()) {        // e.g. the 64 -> 256 1x1 convs of stage 2
         if (Cout <= 64) launch_wgrad<64, 64, 2, 2, true>(p, dz, dw, st(s));
         else launch_wgrad<64, 128, 2, 2, true>(p, dz, dw, st(s));
@@ -2123,8 +2131,11 @@ extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t 
         const size_t P = (size_t)wino_points(nz);
         const size_t eb = gemm_x3_env() ? 6 : 4;      // X3: V and U hold three bf16 planes
         const size_t wt = gemm_x3_env() ? al(sizeof(float) * 27 * (size_t)Cin * Cout) : 0;
-        const size_t b = wt + al(eb * P * (size_t)Cin * Cout) + al(eb * P * (size_t)g.T * Cin) +
-                         al(eb * P * (size_t)g.T * Cout);
+        // U (eb bytes / element) then M (fp32), in either role order (fwd: U over
+        // Cin, M over Cout; bwd-data: the reverse)
+        const size_t um1 = al(eb * P * (size_t)g.T * Cin) + al(4 * P * (size_t)g.T * Cout);
+        const size_t um2 = al(eb * P * (size_t)g.T * Cout) + al(4 * P * (size_t)g.T * Cin);
+        const size_t b = wt + al(eb * P * (size_t)Cin * Cout) + (um1 > um2 ? um1 : um2);
         best = b > best ? b : best;
     }
     return best;

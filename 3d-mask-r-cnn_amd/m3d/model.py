@@ -87,6 +87,18 @@ def rpn_class_loss(t: RPNTargets, rpn_class_logits, alpha=0.90, gamma=1.5):
     return (alpha_t * ce).sum() / t.cls_denom
 
 
+_MASKS = {}
+
+
+def _xy_z_masks(dev):
+    """The (y,x,-,y,x,-) / (-,-,z,-,-,z) coordinate masks, made once per device
+    (no host-to-device copy inside a captured step)."""
+    if dev not in _MASKS:
+        _MASKS[dev] = (torch.tensor([1., 1., 0., 1., 1., 0.], device=dev),
+                       torch.tensor([0., 0., 1., 0., 0., 1.], device=dev))
+    return _MASKS[dev]
+
+
 def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     """core/models.py:1629-1673."""
     if t.n_pos == 0:
@@ -94,8 +106,7 @@ def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     pred = rpn_bbox.reshape(-1, 6).index_select(0, t.pos_idx).clamp(-5.0, 5.0)
     diff = (t.gt_bbox - pred).clamp(-2.0, 2.0)
     ad = diff.abs()
-    xy = torch.tensor([1., 1., 0., 1., 1., 0.], device=diff.device)
-    zm = torch.tensor([0., 0., 1., 0., 0., 1.], device=diff.device)
+    xy, zm = _xy_z_masks(diff.device)
     h_xy = torch.where(ad < 1.0, 0.5 * diff * diff, ad - 0.5) * xy
     h_z = torch.where(ad < 0.5, 0.5 * diff * diff, 0.5 * ad - 0.25) * zm
     return (h_xy + h_z).sum() / (6 * t.pos_denom)
@@ -183,7 +194,9 @@ class RPN:
             return rois
         return rois, join
 
-    def train_step(self, image, targets: RPNTargets, proposals=True):
+    def forward_backward(self, image, targets: RPNTargets, proposals=True):
+        """One step up to (not including) the optimizer: gradients in
+        store.grad_flat, the ProposalLayer overlapped on its side stream."""
         self.store.zero_grad()
         out = self.forward(image, proposals=False)
         join = self.proposals_async(out)[1] if proposals else None
@@ -191,9 +204,42 @@ class RPN:
         total = lc * self.LOSS_WEIGHTS["rpn_class_loss"] + lb * self.LOSS_WEIGHTS["rpn_bbox_loss"]
         total.backward()
         self.rpn.finish_backward()
-        self.sgd_step()
         return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
                 "rpn_rois": join() if join is not None else None}
+
+    def train_step(self, image, targets: RPNTargets, proposals=True):
+        r = self.forward_backward(image, targets, proposals)
+        self.sgd_step()
+        return r
+
+    def graphed_train_step(self, image, targets: RPNTargets, proposals=True, warmup=2):
+        """The training step with its forward + backward (+ ProposalLayer on
+        the side stream) captured once into a HIP graph: ~870 launches replay
+        without the host's per-launch overhead (the stage-4/5 layers are
+        launch-bound eagerly; measured on the 128^3 step the replayed kernels
+        run longer than eager ones, so bench.py uses it only with --graph).
+        The optimizer runs eagerly after each replay
+        (its learning rate decays per iteration).  ``image`` and ``targets``
+        are the graph's static inputs: copy new data into them in place.
+        Returns step() -> the result dict of the captured step (same tensors
+        every call, refreshed by each replay)."""
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):                 # lazy streams / caches, allocator warm-up
+            for _ in range(warmup):
+                self.train_step(image, targets, proposals)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            res = self.forward_backward(image, targets, proposals)
+        self._graph = graph                           # keep the graph (and its pool) alive
+
+        def step():
+            graph.replay()
+            self.sgd_step()
+            return res
+        return step
 
     def load_weights(self, filepath, by_name=True, skip_mismatch=False, exclude=()):
         """keras_model.load_weights(filepath, by_name=True, ...) on the Keras-H5 format (m3d.weights)."""

@@ -509,6 +509,7 @@ def main():
     ap.add_argument("--roi-size", type=int, default=256, help="large-volume ROIAlign leg (0: off)")
     ap.add_argument("--infer-size", type=int, default=256, help="MaskRCNN inference leg size (0: off)")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
+    ap.add_argument("--graph", action="store_true", help="HIP-graph capture of the N=1 step")
     args = ap.parse_args()
 
     from m3d.config import synthetic_rpn_config
@@ -528,8 +529,15 @@ def main():
     targets = RPNTargets(match, bbox, dev)
     props = not args.no_proposals
 
-    def step():
-        return data_parallel_train_step(model, image, targets, world, proposals=props)
+    if world == 1 and args.graph:
+        # the whole forward + backward as one HIP graph (m3d.model.RPN.graphed_train_step):
+        # measured slower (37.6 vs 35.4 ms/step at 128^3: the replayed kernels run
+        # longer, 37.2 vs 36.5 ms busy, while the ~1 ms of launch gaps it removes
+        # is less than that), so eager launches are the default
+        step = model.graphed_train_step(image, targets, proposals=props)
+    else:
+        def step():
+            return data_parallel_train_step(model, image, targets, world, proposals=props)
 
     log(f"[bench] rank {rank}/{world} size {S}^3, warmup {args.warmup}")
     for _ in range(args.warmup):
@@ -562,7 +570,8 @@ def main():
                                   f"{' + ProposalLayer(3D NMS 15000->6000)' if props else ''}, "
                                   f"{S}^3 x1 volume per GPU",
                       "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
-                      "anchors": int(model.anchors.shape[1])}}
+                      "anchors": int(model.anchors.shape[1]),
+                      "hip_graph": bool(world == 1 and args.graph)}}
     if world > 1 and not args.no_extras:
         try:
             ar = time_allreduce(model.store.grad_flat, world)
