@@ -1614,6 +1614,9 @@ __device__ __forceinline__ int x3_off16(int row, int kc) {
     return row * 32 + (((kc ^ (row >> 3)) & 1) << 4);
 }
 
+#ifndef M3D_X3_DBG
+#define M3D_X3_DBG 0   // timing probes of x3_gemm_kernel (debug builds only): 1 no MFMA, 2 no loads
+#endif
 // BK 16: two LDS stages (one barrier per k-tile), 3 blocks/CU; BK 32: one
 // stage (two barriers per k-tile), 2 blocks/CU.
 template <int BK>
@@ -1672,8 +1675,12 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
 #pragma unroll
                 for (int u = 0; u < CPT; ++u) {
                     const int off = (int)(lrow[u] + (uint32_t)kt * (BK * 2));
+#if M3D_X3_DBG == 2   // timing probe: no global loads
+                    va[q][u] = make_uint4(off, q, u, kt); vb[q][u] = make_uint4(kt, u, q, off);
+#else
                     va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
                     vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
+#endif
                 }
         };
         auto store = [&](int buf) {
@@ -1722,6 +1729,9 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
+#if M3D_X3_DBG == 1   // timing probe: no MFMA (fragments still consumed)
+                        acc[i][j][0] += (float)(af[i][0][0] ^ af[i][1][1] ^ af[i][2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
+#else
                         floatx16 c = acc[i][j];
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
@@ -1729,6 +1739,7 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
+#endif
                     }
             }
             if constexpr (NBUF == 2) {
