@@ -999,7 +999,9 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
     const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
     if (ms >= me) return;
     // loader role: operand, float4 column, 8-row group
-    const bool isB = tid >= 128;
+    // wave-uniform role (readfirstlane): a lane-divergent select of the buffer
+    // resource wraps every load in a readfirstlane waterfall loop
+    const bool isB = __builtin_amdgcn_readfirstlane(tid) >= 128;
     const int lt = tid & 127, c4 = lt & 31, grp = lt >> 5;
     const int ld = isB ? N : K;
     const int col = (isB ? n0 : k0) + c4 * 4;

@@ -68,7 +68,8 @@ def _pmc_traffic(kernel_key):
 
 
 def wgrad_gemm_shape(S):
-    """The largest weight-gradient launch of the step: the 64
+    """The largest launch of the step's dominant kernel (x3_wgrad_kernel, 21 %
+    of the step's kernel time, profiles/r01s_bench_kernels_128.txt): the 64
     batched Winograd weight-gradient GEMMs of rpn_conv_shared1 (3x3x3, 256->512)
     on P2 [S/4, S/4, S] -- F(2x2x2) tiles (the weight gradient keeps NZ = 2,
     conv3d.hip wino_wgrad_nz), reduction over M = T tiles, K = 256, N = 512."""
@@ -79,8 +80,8 @@ def wgrad_gemm_shape(S):
 
 
 def wino_gemm_shape(S):
-    """The step's largest launch of its dominant kernel (x3_gemm_kernel, 19 % of
-    the step's kernel time, profiles/r01r_bench_kernels_128.txt): the
+    """The step's largest launch of x3_gemm_kernel (19 % of the step's kernel
+    time, profiles/r01s_bench_kernels_128.txt): the
     16*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
     256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles, K = 256,
     N = 512 (NZ = 4 by default: 96 GEMMs)."""
@@ -91,9 +92,10 @@ def wino_gemm_shape(S):
     return 16 * (nz + 2), T, 256, 512
 
 
-def time_dominant_kernel(S, reps=5):
-    """x3_gemm_kernel on the priced shape through m3d_gemm_x3 (operands split
-    once, untimed, as the Winograd transforms do in the step)."""
+def time_wino_gemm(S, reps=5):
+    """x3_gemm_kernel (the step's second kernel) on its largest launch through
+    m3d_gemm_x3 (operands split once, untimed, as the Winograd transforms do in
+    the step)."""
     from m3d import _lib
     L = _lib.load()
     nb, T, K, N = wino_gemm_shape(S)
@@ -141,11 +143,17 @@ def time_wgrad_gemm(S, reps=5):
                                         _lib.stream()), "gemm_wgrad")
     t = _event_time(launch, reps)
     flops = 2.0 * nb * T * K * N
-    return {"achieved": round(flops / t / 1e12, 2), "unit": "TFLOP/s",
-            "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4), "peak": X3_PEAK_TFLOPS,
+    return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": X3_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4),
+            "traffic": _pmc_traffic(f"wino_wgrad_gemm_rpn_shared1_S{S}"),
+            "kernel": f"x3_wgrad_kernel (fp32 GEMM as 6 bf16 MFMAs per product, operands split in the "
+                      f"LDS store): {nb} batched Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2, "
+                      f"C[K][N] += A[M][K]^T B[M][N], M={T} K={K} N={N}",
+            "peak_note": "bf16 MFMA dense peak 2516.6 TFLOP/s / 6; achieved counts fp32 FLOPs 2*M*K*N",
             "f32_mfma_peak_frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
-            "avg_launch_ms": round(t * 1e3, 4), "shape": f"{nb} x (M={T}) K={K} N={N}",
-            "traffic": _pmc_traffic(f"wino_wgrad_gemm_rpn_shared1_S{S}")}
+            "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
+            "algorithmic_bytes_per_launch": nb * (4.0 * T * (K + N) + 4.0 * K * N),
+            "shape": f"{nb} x (M={T}) K={K} N={N}"}
 
 
 def time_wino_fwd(S, reps=5):
@@ -591,10 +599,12 @@ def main():
         with torch.no_grad():
             fmaps = model.features(image)
         try:
-            out["roofline"] = time_dominant_kernel(S)
+            # dominant kernel of the step: x3_wgrad_kernel (21 % of the step's kernel
+            # time, profiles/r01s_bench_kernels_128.txt), then x3_gemm_kernel (19 %)
+            out["roofline"] = time_wgrad_gemm(S)
+            out["roofline"]["wino_gemm"] = time_wino_gemm(S)
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
             out["roofline"]["wino_fwd_conv"] = time_wino_fwd(S)
-            out["roofline"]["wgrad_gemm"] = time_wgrad_gemm(S)
         except Exception as e:  # report, never hide
             out["roofline"] = {"error": repr(e)}
         try:

@@ -7,7 +7,7 @@ cp $O/bench.json $P/${TAG}_bench_128.json
 cp $O/pytest_gpu.log $P/${TAG}_pytest_gpu.log
 cp $O/bench_kernels.txt $P/${TAG}_bench_kernels_128.txt
 cp $O/prof/run_kernel_stats.csv $P/${TAG}_bench_128_kernel_stats.csv
-for leg in gemm direct roi7 roi14; do
+for leg in gemm wgrad direct roi7 roi14; do
   [ -f $O/k_$leg.txt ] && cp $O/k_$leg.txt $P/${TAG}_k_${leg}_128.txt && cp $O/k_$leg/run_kernel_stats.csv $P/${TAG}_k_${leg}_128_kernel_stats.csv
 done
 [ -f $O/k_infer.txt ] && cp $O/k_infer.txt $P/${TAG}_k_infer_256.txt && cp $O/k_infer/run_kernel_stats.csv $P/${TAG}_k_infer_256_kernel_stats.csv

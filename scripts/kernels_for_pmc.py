@@ -1,7 +1,7 @@
 """Runs ONE priced launch of bench.py a few times for the rocprofv3 --pmc
 passes of scripts/gpu_prof.sh:  kernels_for_pmc.py LEG [S]
-  gemm    the dominant kernel's largest launch (x3_gemm_kernel: batched Winograd GEMM of rpn_conv_shared1)
-  wgrad   the batched Winograd weight-gradient GEMM of rpn_conv_shared1 (x3_wgrad_kernel)
+  gemm    x3_gemm_kernel's largest launch (batched Winograd GEMM of rpn_conv_shared1)
+  wgrad   the dominant kernel's largest launch: batched Winograd weight-gradient GEMM of rpn_conv_shared1 (x3_wgrad_kernel)
   direct  rpn_conv_shared1 as a direct implicit-GEMM conv on P2
   roi7 / roi14  PyramidROIAlign 7^3 / 14^3 at configs[2] shapes
   infer   MaskRCNN inference (configs[3]) x3 after one warm-up
@@ -19,7 +19,7 @@ leg = sys.argv[1]
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 NR = 128 if S == 128 else 512          # configs[2] / configs[3] ROI counts (bench.py)
 if leg == "gemm":
-    print(bench.time_dominant_kernel(S, reps=20))      # 20: the cold first launch moves the average < 2 %
+    print(bench.time_wino_gemm(S, reps=20))      # 20: the cold first launch moves the average < 2 %
 elif leg == "wgrad":
     print(bench.time_wgrad_gemm(S, reps=20))
 elif leg == "winofwd":
