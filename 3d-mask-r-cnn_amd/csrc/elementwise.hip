@@ -83,6 +83,95 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const uint8_t* 
     }
 }
 
+// C % 4 == 0 and < 2^31 float4s per tensor: one float4 of channels per
+// thread and 32-bit index math (the generic kernels above pay a 64-bit
+// division chain per element: the stem pool ran at 0.8 TB/s).  Per channel
+// the window order, the first-valid initialisation and the strict '>' (so the
+// argmax byte and NaN behaviour) and the backward summation order are the
+// scalar kernels' own, so results are bit-identical.
+__global__ __launch_bounds__(256) void maxpool_fwd4_kernel(const float4* __restrict__ x, int H, int W, int D,
+                                                           int C4, int kh, int kw, int kd, int sy, int sx,
+                                                           int sz, int py, int px, int pz, int OH, int OW,
+                                                           int OD, uint32_t total, float4* __restrict__ y,
+                                                           uchar4* __restrict__ am) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int oz = (int)(t % (uint32_t)OD); t /= (uint32_t)OD;
+        const int ox = (int)(t % (uint32_t)OW); t /= (uint32_t)OW;
+        const int oy = (int)(t % (uint32_t)OH);
+        const uint32_t b = t / (uint32_t)OH;
+        float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int bi[4] = {0, 0, 0, 0};
+        bool any = false;
+        for (int ky = 0; ky < kh; ++ky) {
+            const int iy = oy * sy - py + ky;
+            if (iy < 0 || iy >= H) continue;
+            for (int kx = 0; kx < kw; ++kx) {
+                const int ix = ox * sx - px + kx;
+                if (ix < 0 || ix >= W) continue;
+                const uint32_t row = ((b * (uint32_t)H + iy) * (uint32_t)W + ix) * (uint32_t)D;
+                for (int kz = 0; kz < kd; ++kz) {
+                    const int iz = oz * sz - pz + kz;
+                    if (iz < 0 || iz >= D) continue;
+                    const float4 v = x[(row + iz) * (uint32_t)C4 + c];
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+                    const int id = (ky * kw + kx) * kd + kz;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (!any || vv[q] > best[q]) { best[q] = vv[q]; bi[q] = id; }
+                    any = true;
+                }
+            }
+        }
+        y[i] = make_float4(best[0], best[1], best[2], best[3]);
+        if (am) am[i] = make_uchar4((unsigned char)bi[0], (unsigned char)bi[1], (unsigned char)bi[2],
+                                    (unsigned char)bi[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float4* __restrict__ dy,
+                                                           const uchar4* __restrict__ am, int H, int W,
+                                                           int D, int C4, int kh, int kw, int kd, int sy,
+                                                           int sx, int sz, int py, int px, int pz, int OH,
+                                                           int OW, int OD, uint32_t total,
+                                                           float4* __restrict__ dx) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int iz = (int)(t % (uint32_t)D); t /= (uint32_t)D;
+        const int ix = (int)(t % (uint32_t)W); t /= (uint32_t)W;
+        const int iy = (int)(t % (uint32_t)H);
+        const uint32_t b = t / (uint32_t)H;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const int oy_lo = max(0, (iy + py - kh + 1 + sy - 1) / sy), oy_hi = min(OH - 1, (iy + py) / sy);
+        const int ox_lo = max(0, (ix + px - kw + 1 + sx - 1) / sx), ox_hi = min(OW - 1, (ix + px) / sx);
+        const int oz_lo = max(0, (iz + pz - kd + 1 + sz - 1) / sz), oz_hi = min(OD - 1, (iz + pz) / sz);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const int ky = iy - (oy * sy - py);
+            if (ky < 0 || ky >= kh) continue;
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int kx = ix - (ox * sx - px);
+                if (kx < 0 || kx >= kw) continue;
+                const uint32_t row = ((b * (uint32_t)OH + oy) * (uint32_t)OW + ox) * (uint32_t)OD;
+                for (int oz = oz_lo; oz <= oz_hi; ++oz) {
+                    const int kz = iz - (oz * sz - pz);
+                    if (kz < 0 || kz >= kd) continue;
+                    const uint32_t o = (row + oz) * (uint32_t)C4 + c;
+                    const uchar4 a = am[o];
+                    const float4 g = dy[o];
+                    const unsigned char id = (unsigned char)((ky * kw + kx) * kd + kz);
+                    if (a.x == id) acc[0] += g.x;
+                    if (a.y == id) acc[1] += g.y;
+                    if (a.z == id) acc[2] += g.z;
+                    if (a.w == id) acc[3] += g.w;
+                }
+            }
+        }
+        dx[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+}
+
 __global__ void upsample221_bwd_kernel(const float4* __restrict__ dup, int B, int H, int W, int D,
                                        int C4, float4* __restrict__ dsrc, int accumulate) {
     const int64_t total = (int64_t)B * H * W * D * C4;
@@ -261,23 +350,42 @@ __global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __rest
 
 // ---- Keras SGD over a flat parameter buffer split into segments padded to
 // multiples of 1024 floats; chunk c (1024 floats) belongs to seg_of_chunk[c].
+// Each block folds SGD_NORM_CHUNKS consecutive chunks and issues one atomic
+// per segment it touches (was one per 1024-float chunk: ~57k atomics onto
+// ~160 addresses per step).  The segment of a chunk is block-uniform.
+constexpr int SGD_NORM_CHUNKS = 16;
 __global__ __launch_bounds__(256) void sgd_norm_kernel(const float* __restrict__ w,
                                                        const float* __restrict__ g,
                                                        const int32_t* __restrict__ seg_of_chunk,
-                                                       const float* __restrict__ l2,
+                                                       const float* __restrict__ l2, int64_t n_chunks,
                                                        float* __restrict__ norms) {
-    const int64_t ch = blockIdx.x;
-    const int seg = seg_of_chunk[ch];
-    const float lc = l2[seg];
-    const int64_t off = ch * 1024 + threadIdx.x * 4;
-    const float4 wv = *(const float4*)(w + off), gv = *(const float4*)(g + off);
-    const float a = gv.x + lc * wv.x, b = gv.y + lc * wv.y, c = gv.z + lc * wv.z, d = gv.w + lc * wv.w;
-    float s = a * a + b * b + c * c + d * d;
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     __shared__ float red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) unsafeAtomicAdd(norms + seg, red[0] + red[1] + red[2] + red[3]);
+    const int64_t ch0 = (int64_t)blockIdx.x * SGD_NORM_CHUNKS;
+    const int64_t ch1 = ch0 + SGD_NORM_CHUNKS < n_chunks ? ch0 + SGD_NORM_CHUNKS : n_chunks;
+    int cur = seg_of_chunk[ch0];
+    float s = 0.0f;
+    auto flush = [&]() {
+        float r = s;
+        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
+        __syncthreads();
+        if (threadIdx.x == 0) unsafeAtomicAdd(norms + cur, red[0] + red[1] + red[2] + red[3]);
+        __syncthreads();
+        s = 0.0f;
+    };
+    for (int64_t ch = ch0; ch < ch1; ++ch) {
+        const int seg = seg_of_chunk[ch];
+        if (seg != cur) {
+            flush();
+            cur = seg;
+        }
+        const float lc = l2[seg];
+        const int64_t off = ch * 1024 + threadIdx.x * 4;
+        const float4 wv = *(const float4*)(w + off), gv = *(const float4*)(g + off);
+        const float a = gv.x + lc * wv.x, b = gv.y + lc * wv.y, c = gv.z + lc * wv.z, d = gv.w + lc * wv.w;
+        s += a * a + b * b + c * c + d * d;
+    }
+    flush();
 }
 
 __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ w,
@@ -323,6 +431,14 @@ extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W
     if (kh * kw * kd > 255) return einval("maxpool3d: window larger than 255");
     const int64_t total = B * OH * OW * OD * C;
     if (total == 0) return M3D_OK;
+    if (C % 4 == 0 && B * H * W * D * C / 4 < 0x7FFFFFFF && total / 4 < 0x7FFFFFFF &&
+        ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+                           (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, sz,
+                           py, px, pz, (int)OH, (int)OW, (int)OD, (uint32_t)(total / 4), (float4*)y,
+                           (uchar4*)argmax);
+        return check_launch("maxpool_fwd4_kernel");
+    }
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), x, (int)B,
                        (int)H, (int)W, (int)D, (int)C, kh, kw, kd, sy, sx, sz, py, px, pz, (int)OH,
                        (int)OW, (int)OD, y, argmax);
@@ -336,6 +452,14 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
                                  float* dx, m3d_stream_t s) {
     const int64_t total = B * H * W * D * C;
     if (total == 0) return M3D_OK;
+    if (C % 4 == 0 && total / 4 < 0x7FFFFFFF && B * OH * OW * OD * C / 4 < 0x7FFFFFFF &&
+        ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+                           (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
+                           kh, kw, kd, sy, sx, sz, py, px, pz, (int)OH, (int)OW, (int)OD,
+                           (uint32_t)(total / 4), (float4*)dx);
+        return check_launch("maxpool_bwd4_kernel");
+    }
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), dy, argmax,
                        (int)B, (int)H, (int)W, (int)D, (int)C, kh, kw, kd, sy, sx, sz, py, px, pz,
                        (int)OH, (int)OW, (int)OD, dx);
@@ -458,8 +582,8 @@ extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, 
     if (clipnorm > 0.f) {
         if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
             return check_launch("memset norms");
-        hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params,
-                           grads, seg_of_chunk, l2_coef, norms);
+        hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)((n_chunks + SGD_NORM_CHUNKS - 1) / SGD_NORM_CHUNKS)),
+                           dim3(256), 0, st(s), params, grads, seg_of_chunk, l2_coef, (int64_t)n_chunks, norms);
         int rc = check_launch("sgd_norm_kernel");
         if (rc) return rc;
     }
