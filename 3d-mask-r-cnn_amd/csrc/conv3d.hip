@@ -848,7 +848,9 @@ static int num_cus() {
 // error vs fp64 below the f32 MFMA's: scripts/x3_accuracy.py); bit 1:
 // implicit-GEMM convs splitting in the LDS store (slower: off); bit 2: the
 // Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step);
-// bit 3: the weight gradients of 1x1x1 stride-1 convs on the same kernel.
+// bit 3: the weight gradients of 1x1x1 stride-1 convs on the same kernel;
+// bit 4: the Winograd input transform writes U as fp32 (4 B per point
+// instead of 3 x 2 B) and x3_gemm_kernel splits it in its LDS store.
 static int x3_mask() {
     static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 13; }();
     return v;
@@ -1601,6 +1603,7 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
 // contiguous order, as conv_gemm_kernel).
 struct X3G {
     const unsigned short* a;
+    const float* af;           // AF32: A as fp32 [batch][M][K], split in the LDS store
     const unsigned short* b;
     float* c;
     int64_t M;
@@ -1627,7 +1630,7 @@ __device__ __forceinline__ int x3_soff(int row, int kc) {
     else return x3_off(row, kc * 8);
 }
 
-template <int BK, bool PERSIST, int OCC = (BK == 16 ? 3 : 2)>
+template <int BK, bool PERSIST, int OCC = (BK == 16 ? 3 : 2), bool AF32 = false>
 __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
     static_assert(BK == 16 || BK == 32, "BK");
     constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
@@ -1662,7 +1665,11 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
         __amdgpu_buffer_rsrc_t ra[3], rb[3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) {
-            ra[pl] = make_rsrc(g.a + pl * g.psa + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 2);
+            if constexpr (AF32) {
+                if (pl == 0) ra[0] = make_rsrc(g.af + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 4);
+            } else {
+                ra[pl] = make_rsrc(g.a + pl * g.psa + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 2);
+            }
             rb[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + (int64_t)n0 * g.K, (uint64_t)(g.N - n0) * g.K * 2);
         }
 #pragma unroll
@@ -1670,7 +1677,8 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
             const int c = tid + 256 * u;
             lrow[u] = (uint32_t)((c / KCH) * g.K + (c % KCH) * 8) * 2u;
         }
-        uint4 va[3][CPT], vb[3][CPT];
+        uint4 va[AF32 ? 1 : 3][CPT], vb[3][CPT];
+        float4 fa[AF32 ? CPT : 1][2];   // AF32: the 8 fp32 k of each A chunk
         auto load = [&](int kt) {
 #pragma unroll
             for (int q = 0; q < 3; ++q)
@@ -1678,9 +1686,17 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                 for (int u = 0; u < CPT; ++u) {
                     const int off = (int)(lrow[u] + (uint32_t)kt * (BK * 2));
 #if M3D_X3_DBG == 2   // timing probe: no global loads
-                    va[q][u] = make_uint4(off, q, u, kt); vb[q][u] = make_uint4(kt, u, q, off);
+                    if constexpr (!AF32) va[q][u] = make_uint4(off, q, u, kt);
+                    vb[q][u] = make_uint4(kt, u, q, off);
 #else
-                    va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
+                    if constexpr (AF32) {
+                        if (q == 0) {   // element offset of the chunk = byte offset of its bf16 image / 2
+                            fa[u][0] = bload4(ra[0], (uint32_t)off * 2u);
+                            fa[u][1] = bload4(ra[0], (uint32_t)off * 2u + 16u);
+                        }
+                    } else {
+                        va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
+                    }
                     vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
 #endif
                 }
@@ -1689,12 +1705,22 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
             char* As = smem + buf * STAGE;
             char* Bs = As + 3 * PLA;
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
+            for (int u = 0; u < CPT; ++u) {
+                if constexpr (AF32) {
+                    uint2 lo4[3], hi4[3];
+                    split3x4(fa[u][0], lo4);
+                    split3x4(fa[u][1], hi4);
 #pragma unroll
-                for (int u = 0; u < CPT; ++u) {
-                    *reinterpret_cast<uint4*>(As + q * PLA + soff[u]) = va[q][u];
-                    *reinterpret_cast<uint4*>(Bs + q * PLB + soff[u]) = vb[q][u];
+                    for (int q = 0; q < 3; ++q)
+                        *reinterpret_cast<uint4*>(As + q * PLA + soff[u]) =
+                            make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint4*>(As + q * PLA + soff[u]) = va[q][u];
                 }
+#pragma unroll
+                for (int q = 0; q < 3; ++q) *reinterpret_cast<uint4*>(Bs + q * PLB + soff[u]) = vb[q][u];
+            }
         };
         floatx16 acc[TM][TN];
 #pragma unroll
@@ -2190,10 +2216,15 @@ static int x3_persist_env() {
     return v;
 }
 
-// the P point GEMMs M[xi] = U[xi] V[xi] on split planes (U: T x K, V: N x K)
-static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipStream_t s) {
+static int x3_af32_env() { return (x3_mask() >> 4) & 1; }
+
+// the P point GEMMs M[xi] = U[xi] V[xi] on split planes (U: T x K, V: N x K);
+// af32: U is fp32 [P][T][K] (split in the GEMM's LDS store)
+static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipStream_t s,
+                         bool af32 = false) {
     X3G q;
     q.a = reinterpret_cast<const unsigned short*>(ws.U);
+    q.af = ws.U;
     q.b = reinterpret_cast<const unsigned short*>(ws.V);
     q.c = ws.M;
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
@@ -2205,7 +2236,9 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     const int64_t resident = (int64_t)num_cus() * (bk16 || occ3 ? 3 : 2);
     const bool persist = x3_persist_env() && tiles > 2 * resident;
     const dim3 grid(persist ? (unsigned)(resident / 8 * 8) : (unsigned)tiles);
-    if (bk16) {
+    if (af32) {
+        hipLaunchKernelGGL((x3_gemm_kernel<32, false, 2, true>), dim3((unsigned)tiles), dim3(256), 0, s, q);
+    } else if (bk16) {
         if (persist) hipLaunchKernelGGL((x3_gemm_kernel<16, true>), grid, dim3(256), 0, s, q);
         else hipLaunchKernelGGL((x3_gemm_kernel<16, false>), grid, dim3(256), 0, s, q);
     } else if (occ3) {
@@ -2275,9 +2308,13 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
                            dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
         WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
                           (int)Cin, (int)Cout, 0, ws.V);
-        WINO_LAUNCH_NZ_X3(wino_nz(), wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
-                          (int)Cin, ws.U);
-        wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s);
+        const bool af32 = x3_af32_env();
+        if (af32)
+            WINO_LAUNCH(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g, (int)Cin, ws.U);
+        else
+            WINO_LAUNCH_NZ_X3(wino_nz(), wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
+                              (int)Cin, ws.U);
+        wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s, af32);
         Epi o{};
         o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
         o.res_mode = residual ? 1 : 0; o.relu = relu; o.z = z_out; o.y = y; o.ldy = Cout;
@@ -2344,9 +2381,14 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     if (gemm_x3_env()) {
         WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
                           (int)Cin, (int)Cout, 1, ws.V);
-        WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
-                          (int)Cout, ws.U);
-        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), st(s));
+        const bool af32 = x3_af32_env();
+        if (af32)
+            WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+                           (int)Cout, ws.U);
+        else
+            WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+                              (int)Cout, ws.U);
+        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), st(s), af32);
         Epi o{};
         o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
         WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
