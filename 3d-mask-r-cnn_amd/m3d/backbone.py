@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from .nn import _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
+from .nn import GradLink, _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
 from .params import BNLayer, ConvLayer
 
 
@@ -23,10 +23,11 @@ class _Unit:
         self.bn = BNLayer(store, bn_name, cout)
         self.stride, self.padding = tuple(stride), padding
 
-    def __call__(self, x, relu, residual=None, need_dx=True):
+    def __call__(self, x, relu, residual=None, need_dx=True, link=None):
         geo = conv_geom(tuple(x.shape[1:4]), self.conv.k, self.stride, self.padding)
         return conv_bn_act(x, self.conv, geo, relu, residual=residual,
-                           res_mode=1 if residual is not None else 0, bn=self.bn, need_dx=need_dx)
+                           res_mode=1 if residual is not None else 0, bn=self.bn, need_dx=need_dx,
+                           link=link)
 
 
 class _Block:
@@ -41,10 +42,13 @@ class _Block:
         self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
 
     def __call__(self, x):
+        # identity block: 2c's residual gradient is accumulated into 2a's data
+        # gradient by the bwd-data kernel (GradLink) instead of an autograd add
+        link = GradLink() if self.sc is None and torch.is_grad_enabled() and x.requires_grad else None
         short = self.sc(x, relu=False) if self.sc is not None else x
-        y = self.a(x, relu=True)
+        y = self.a(x, relu=True, link=link)
         y = self.b(y, relu=True)
-        return self.c(y, relu=True, residual=short)
+        return self.c(y, relu=True, residual=short, link=link)
 
 
 class ResNet3D:

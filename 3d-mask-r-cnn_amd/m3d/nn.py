@@ -156,6 +156,19 @@ def conv_geom(in_sp, k, stride, padding):
                     tuple(valid_out(n + 2 * p, kk, s) for n, kk, s in zip(in_sp, k, stride)))
 
 
+class GradLink:
+    """Hands one conv's residual gradient to the conv that reads the same tensor
+    as its input, so the input conv's data gradient is accumulated into it by
+    the kernel (accumulate=1) instead of autograd adding two full tensors.
+    identity_block (core/models.py:157-189): x is both conv 2a's input and
+    conv 2c's residual, and 2c's backward always runs before 2a's (2a -> 2b
+    -> 2c), so 2c parks dres in ``buf`` and returns no residual gradient."""
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
 class _ConvBNAct(torch.autograd.Function):
     """y = act(BN_frozen(conv(x, w) + b) [+ residual]).
 
@@ -163,7 +176,7 @@ class _ConvBNAct(torch.autograd.Function):
     source of y (FPN top-down add, core/models.py:3193-3204)."""
 
     @staticmethod
-    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx):
+    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None):
         B, H, W, D, Cin = x.shape
         kh, kw, kd = geo.k
         Cout = w.shape[-1]
@@ -218,6 +231,7 @@ class _ConvBNAct(torch.autograd.Function):
             _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
         ctx.save_for_backward(x, w, y, z)
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
+        ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
         return y
 
@@ -276,21 +290,30 @@ class _ConvBNAct(torch.autograd.Function):
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
             dx = None
             if ctx.need_dx:
-                dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+                acc = 0
+                if ctx.link is not None and ctx.link.buf is not None and ctx.link.buf.shape == x.shape:
+                    dx, acc, ctx.link.buf = ctx.link.buf, 1, None
+                else:
+                    dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
                 check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
-                                                 geo.pad[2], ptr(dx), 0, ptr(ws), wsb, stream()),
+                                                 geo.pad[2], ptr(dx), acc, ptr(ws), wsb, stream()),
                       "conv3d_bwd_data_wino")
             _grad_done(grads, side)
-            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None
+            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                               OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
                                               stream()), "conv3d_bwd_weight")
         dx = None
+        link = ctx.link
+        acc = 0
         if ctx.need_dx:
             strided = any(s != 1 for s in geo.stride)
-            dx = (torch.zeros if strided else torch.empty)(x.shape, device=x.device, dtype=torch.float32)
+            if link is not None and link.buf is not None and link.buf.shape == x.shape:
+                dx, acc, link.buf = link.buf, 1, None     # dx = dres (parked by the residual conv) + conv^T dz
+            else:
+                dx = (torch.zeros if strided else torch.empty)(x.shape, device=x.device, dtype=torch.float32)
             wd, dzd, cpad = w, dz, Cout
             if Cout % 32:   # bwd-data stages 32-channel slices of dz: zero-pad the channel dim
                 cpad = -(-Cout // 32) * 32
@@ -299,19 +322,21 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
                 dzd[..., :Cout] = dz
             check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
-                                        OD, *geo.stride, *geo.pad, ptr(dx), 0, stream()),
+                                        OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
                   "conv3d_bwd_data")
         _grad_done(grads, side)
         dr = None
         if need_res:
-            if ctx.res_mode == 1:
+            if ctx.res_mode == 1 and link is not None and not trivial:
+                link.buf = dres                               # consumed by the input conv's backward
+            elif ctx.res_mode == 1:
                 dr = dres
             else:
                 rb, rh, rw, rd, rc = ctx.res_shape
                 dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
-        return dx, dr, None, None, None, None, None, None, None, None
+        return dx, dr, None, None, None, None, None, None, None, None, None
 
 
 def _slab_extend(x, geo):
@@ -326,8 +351,10 @@ def _slab_extend(x, geo):
     return xe, ConvGeom(geo.k, geo.stride, (geo.pad[0], geo.pad[1], r - nlo), geo.out)
 
 
-def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True):
-    """Functional entry: ``layer`` is a Conv3D parameter group from params.py."""
+def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None):
+    """Functional entry: ``layer`` is a Conv3D parameter group from params.py.
+    ``link``: a GradLink shared by the residual conv and the input conv of an
+    identity block (see GradLink)."""
     w = layer.kernel.data
     b = layer.bias.data if layer.bias is not None else None
     grads = layer.grad_dict(bn) if torch.is_grad_enabled() else None   # inference: no z / grads
@@ -343,7 +370,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                            need_dx and x.requires_grad)
+                            need_dx and x.requires_grad, link)
 
 
 class _MaxPool(torch.autograd.Function):
