@@ -42,13 +42,20 @@ class _Block:
         self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
 
     def __call__(self, x):
-        # identity block: 2c's residual gradient is accumulated into 2a's data
-        # gradient by the bwd-data kernel (GradLink) instead of an autograd add
-        link = GradLink() if self.sc is None and torch.is_grad_enabled() and x.requires_grad else None
-        short = self.sc(x, relu=False) if self.sc is not None else x
+        # the two gradients of x are summed by the bwd-data kernel (GradLink)
+        # instead of an autograd add: identity block 2c's residual gradient
+        # into 2a's data gradient; conv block shortcut's and 2a's data gradients
+        train = torch.is_grad_enabled() and x.requires_grad
+        if self.sc is None:
+            link = GradLink("res") if train else None
+            y = self.a(x, relu=True, link=link)
+            y = self.b(y, relu=True)
+            return self.c(y, relu=True, residual=x, link=link)
+        link = GradLink("dx2") if train else None
+        short = self.sc(x, relu=False, link=link)
         y = self.a(x, relu=True, link=link)
         y = self.b(y, relu=True)
-        return self.c(y, relu=True, residual=short, link=link)
+        return self.c(y, relu=True, residual=short)
 
 
 class ResNet3D:

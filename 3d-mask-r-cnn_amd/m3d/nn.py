@@ -157,16 +157,37 @@ def conv_geom(in_sp, k, stride, padding):
 
 
 class GradLink:
-    """Hands one conv's residual gradient to the conv that reads the same tensor
-    as its input, so the input conv's data gradient is accumulated into it by
-    the kernel (accumulate=1) instead of autograd adding two full tensors.
-    identity_block (core/models.py:157-189): x is both conv 2a's input and
-    conv 2c's residual, and 2c's backward always runs before 2a's (2a -> 2b
-    -> 2c), so 2c parks dres in ``buf`` and returns no residual gradient."""
-    __slots__ = ("buf",)
+    """Lets the bwd-data kernel accumulate one consumer's gradient of a tensor
+    into another's (accumulate=1) instead of autograd adding two full tensors.
 
-    def __init__(self):
+    mode "res" -- identity_block (core/models.py:157-189): x is both conv 2a's
+    input and conv 2c's residual; 2c's backward always runs before 2a's (2a ->
+    2b -> 2c), so 2c parks dres in ``buf`` and returns no residual gradient.
+    mode "dx2" -- conv_block (core/models.py:192-232): x is the input of both
+    the shortcut conv and conv 2a, whose backward order is not fixed: the
+    first to run parks its dx and returns none, the second accumulates into
+    the parked buffer and returns the sum."""
+    __slots__ = ("buf", "mode")
+
+    def __init__(self, mode="res"):
         self.buf = None
+        self.mode = mode
+
+
+def _link_take(link, x):
+    """(parked gradient of x, 1) if the link holds one, else (None, 0)."""
+    if link is not None and link.buf is not None and link.buf.shape == x.shape:
+        buf, link.buf = link.buf, None
+        return buf, 1
+    return None, 0
+
+
+def _link_park(link, dx, acc):
+    """mode dx2, first consumer: park dx and return no gradient."""
+    if link is not None and link.mode == "dx2" and not acc and dx is not None:
+        link.buf = dx
+        return None
+    return dx
 
 
 class _ConvBNAct(torch.autograd.Function):
@@ -290,14 +311,13 @@ class _ConvBNAct(torch.autograd.Function):
             ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
             dx = None
             if ctx.need_dx:
-                acc = 0
-                if ctx.link is not None and ctx.link.buf is not None and ctx.link.buf.shape == x.shape:
-                    dx, acc, ctx.link.buf = ctx.link.buf, 1, None
-                else:
+                dx, acc = _link_take(ctx.link, x)
+                if dx is None:
                     dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
                 check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                  geo.pad[2], ptr(dx), acc, ptr(ws), wsb, stream()),
                       "conv3d_bwd_data_wino")
+                dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
@@ -310,9 +330,8 @@ class _ConvBNAct(torch.autograd.Function):
         acc = 0
         if ctx.need_dx:
             strided = any(s != 1 for s in geo.stride)
-            if link is not None and link.buf is not None and link.buf.shape == x.shape:
-                dx, acc, link.buf = link.buf, 1, None     # dx = dres (parked by the residual conv) + conv^T dz
-            else:
+            dx, acc = _link_take(link, x)                     # dx = parked gradient + conv^T dz
+            if dx is None:
                 dx = (torch.zeros if strided else torch.empty)(x.shape, device=x.device, dtype=torch.float32)
             wd, dzd, cpad = w, dz, Cout
             if Cout % 32:   # bwd-data stages 32-channel slices of dz: zero-pad the channel dim
@@ -324,10 +343,11 @@ class _ConvBNAct(torch.autograd.Function):
             check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
                                         OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
                   "conv3d_bwd_data")
+            dx = _link_park(link, dx, acc)
         _grad_done(grads, side)
         dr = None
         if need_res:
-            if ctx.res_mode == 1 and link is not None and not trivial:
+            if ctx.res_mode == 1 and link is not None and link.mode == "res" and not trivial:
                 link.buf = dres                               # consumed by the input conv's backward
             elif ctx.res_mode == 1:
                 dr = dres
