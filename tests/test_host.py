@@ -61,3 +61,39 @@ def test_tf_same_padding_is_asymmetric():
     assert same_out_pad(128, 3, 1) == (128, 1)
     g = conv_geom((128, 128, 128), (7, 7, 7), (2, 2, 1), 3)  # ZeroPadding3D(3) + valid
     assert g.out == (64, 64, 128) and g.pad == (3, 3, 3)
+
+
+@pytest.mark.parametrize("order", ["sc_first", "a_first"])
+def test_gradlink_dx2_protocol_sums_once(order):
+    """GradLink 'dx2' (conv block: shortcut and conv 2a read the same x): the
+    first backward parks its gradient and returns none, the second takes the
+    parked buffer with accumulate=1 and returns it -- in either order."""
+    import torch
+    from m3d.nn import GradLink, _link_park, _link_take
+    x = torch.zeros(2, 3)
+    link = GradLink("dx2")
+    g_first, g_second = torch.full((2, 3), 1.0), torch.full((2, 3), 2.0)
+    buf, acc = _link_take(link, x)
+    assert buf is None and acc == 0
+    assert _link_park(link, g_first, acc) is None and link.buf is g_first
+    buf, acc = _link_take(link, x)
+    assert buf is g_first and acc == 1 and link.buf is None
+    buf += g_second                       # what the bwd-data kernel does with accumulate=1
+    out = _link_park(link, buf, acc)
+    assert out is g_first and torch.equal(out, torch.full((2, 3), 3.0)) and link.buf is None
+
+
+def test_gradlink_res_mode_never_parks_data_gradients():
+    """GradLink 'res' (identity block): only the residual conv parks (dres);
+    data gradients pass through, the input conv consumes the parked dres."""
+    import torch
+    from m3d.nn import GradLink, _link_park, _link_take
+    x = torch.zeros(4)
+    link = GradLink("res")
+    dx = torch.ones(4)
+    assert _link_park(link, dx, 0) is dx and link.buf is None
+    link.buf = torch.full((4,), 5.0)      # conv 2c's backward parks dres
+    buf, acc = _link_take(link, torch.zeros(3))
+    assert buf is None and acc == 0       # shape mismatch: not this tensor's gradient
+    buf, acc = _link_take(link, x)
+    assert acc == 1 and torch.equal(buf, torch.full((4,), 5.0)) and link.buf is None
