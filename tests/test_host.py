@@ -97,3 +97,25 @@ def test_gradlink_res_mode_never_parks_data_gradients():
     assert buf is None and acc == 0       # shape mismatch: not this tensor's gradient
     buf, acc = _link_take(link, x)
     assert acc == 1 and torch.equal(buf, torch.full((4,), 5.0)) and link.buf is None
+
+
+@pytest.mark.parametrize("shape,stride", [((1, 12, 10, 9, 1), (2, 2, 1)), ((2, 9, 8, 16, 1), (1, 1, 1))])
+def test_stem_zwindow_form_is_the_same_conv(shape, stride):
+    """The stem's window form (x64 = the 8x8 (x, z) windows of x as channels,
+    w64 = the kw x kd taps zero-padded to 8 x 8, a (kh, 1, 1) conv) equals the
+    7^3 conv (float64)."""
+    import torch
+    from m3d.nn import _stem_zwindow, conv_geom
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(shape, generator=g)
+    w = torch.randn((7, 7, 7, 1, 5), generator=g)
+    geo = conv_geom(shape[1:4], (7, 7, 7), stride, 3)
+    x8, w8, g8 = _stem_zwindow(x, w, geo)
+    assert x8.shape[-1] == 64 and g8.k == (7, 1, 1) and g8.out == geo.out
+
+    def conv(xc, wc, gg):   # channels-last [B,H,W,D,C] with pad-before; crop to gg.out
+        xt = torch.nn.functional.pad(xc.permute(0, 4, 1, 2, 3).double(),
+                                     (gg.pad[2], 16, gg.pad[1], 16, gg.pad[0], 16))
+        y = torch.nn.functional.conv3d(xt, wc.permute(4, 3, 0, 1, 2).double(), stride=gg.stride)
+        return y[:, :, :gg.out[0], :gg.out[1], :gg.out[2]]
+    torch.testing.assert_close(conv(x8, w8, g8), conv(x, w, geo), rtol=0, atol=1e-12)
