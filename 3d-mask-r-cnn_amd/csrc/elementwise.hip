@@ -417,6 +417,65 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ w,
     *(float4*)(v + off) = vv;
 }
 
+// ---- Keras 2.3.1 Adam / Adadelta over the same flat, chunked buffers
+// (core/models.py:3349-3357 picks them by OPTIMIZER.name).  Per element, in
+// the op order of keras/optimizers.py (compiled -ffp-contract=off):
+//   Adam:     m = b1*m + (1-b1)*g;  v = b2*v + (1-b2)*(g*g);
+//             [amsgrad: vh = max(vh, v), v' = vh]   p -= (lr_t*m) / (sqrt(v') + eps)
+//             (lr_t = lr*sqrt(1-b2^t)/(1-b1^t) is a host scalar)
+//   Adadelta: a = rho*a + (1-rho)*(g*g);  u = (g*sqrt(d+eps)) / sqrt(a+eps);
+//             p -= lr*u;  d = rho*d + (1-rho)*(u*u)
+// where g is the tf.clip_by_norm'd gradient plus the L2 term, as for SGD.
+template <int MODE>
+__global__ __launch_bounds__(256) void adaptive_update_kernel(
+        float* __restrict__ w, const float* __restrict__ g, float* __restrict__ s1,
+        float* __restrict__ s2, float* __restrict__ s3, const int32_t* __restrict__ seg_of_chunk,
+        const float* __restrict__ l2, const float* __restrict__ norms, float lr, float c1,
+        float c1m, float c2, float c2m, float eps, float clipnorm) {
+    const int64_t ch = blockIdx.x;
+    const int seg = seg_of_chunk[ch];
+    const float lc = l2[seg];
+    const float nrm = clipnorm > 0.f ? sqrtf(norms[seg]) : 0.0f;
+    const float den = clipnorm > 0.f ? (nrm > clipnorm ? nrm : clipnorm) : 1.0f;
+    const float num = clipnorm > 0.f ? clipnorm : 1.0f;
+    const int64_t off = ch * 1024 + threadIdx.x * 4;
+    float4 wv = *(float4*)(w + off), av = *(float4*)(s1 + off), bv = *(float4*)(s2 + off);
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == 1) hv = *(float4*)(s3 + off);
+    const float4 gv = *(const float4*)(g + off);
+    const float gg[4] = {gv.x + lc * wv.x, gv.y + lc * wv.y, gv.z + lc * wv.z, gv.w + lc * wv.w};
+    float* wp = &wv.x;
+    float* ap = &av.x;
+    float* bp = &bv.x;
+    float* hp = &hv.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float gc = (gg[q] * num) / den;                  // tf.clip_by_norm
+        if (MODE <= 1) {                                       // Adam (1: amsgrad)
+            const float m = c1 * ap[q] + c1m * gc;
+            const float v = c2 * bp[q] + c2m * (gc * gc);
+            float vd = v;
+            if (MODE == 1) {
+                hp[q] = hp[q] > v ? hp[q] : v;
+                vd = hp[q];
+            }
+            wp[q] = wp[q] - (lr * m) / (sqrtf(vd) + eps);
+            ap[q] = m;
+            bp[q] = v;
+        } else {                                               // Adadelta
+            const float a = c1 * ap[q] + c1m * (gc * gc);
+            const float u = (gc * sqrtf(bp[q] + eps)) / sqrtf(a + eps);
+            wp[q] = wp[q] - lr * u;
+            ap[q] = a;
+            bp[q] = c1 * bp[q] + c1m * (u * u);
+        }
+    }
+    *(float4*)(w + off) = wv;
+    *(float4*)(s1 + off) = av;
+    *(float4*)(s2 + off) = bv;
+    if (MODE == 1) *(float4*)(s3 + off) = hv;
+}
+
 }  // namespace m3d
 
 using namespace m3d;
@@ -590,4 +649,52 @@ extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, 
     hipLaunchKernelGGL(sgd_update_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params,
                        grads, moments, seg_of_chunk, l2_coef, norms, lr, momentum, clipnorm);
     return check_launch("sgd_update_kernel");
+}
+
+static int clip_norms(const float* params, const float* grads, int64_t n_chunks,
+                      const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
+                      float clipnorm, float* norms, m3d_stream_t s) {
+    if (!(clipnorm > 0.f)) return M3D_OK;
+    if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
+        return check_launch("memset norms");
+    hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)((n_chunks + SGD_NORM_CHUNKS - 1) / SGD_NORM_CHUNKS)),
+                       dim3(256), 0, st(s), params, grads, seg_of_chunk, l2_coef, (int64_t)n_chunks, norms);
+    return check_launch("sgd_norm_kernel");
+}
+
+extern "C" int m3d_adam_keras(float* params, const float* grads, float* m, float* v, float* vhat,
+                              int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
+                              int32_t n_segments, float lr_t, float beta_1, float beta_2,
+                              float epsilon, float clipnorm, float* norms, m3d_stream_t s) {
+    if (n_chunks <= 0) return M3D_OK;
+    if (!params || !grads || !m || !v || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
+        return einval("adam: null pointer");
+    int rc = clip_norms(params, grads, n_chunks, seg_of_chunk, l2_coef, n_segments, clipnorm, norms, s);
+    if (rc) return rc;
+    const float c1m = 1.0f - beta_1, c2m = 1.0f - beta_2;
+    if (vhat)
+        hipLaunchKernelGGL(adaptive_update_kernel<1>, dim3((unsigned)n_chunks), dim3(256), 0, st(s),
+                           params, grads, m, v, vhat, seg_of_chunk, l2_coef, norms, lr_t, beta_1, c1m,
+                           beta_2, c2m, epsilon, clipnorm);
+    else
+        hipLaunchKernelGGL(adaptive_update_kernel<0>, dim3((unsigned)n_chunks), dim3(256), 0, st(s),
+                           params, grads, m, v, (float*)nullptr, seg_of_chunk, l2_coef, norms, lr_t,
+                           beta_1, c1m, beta_2, c2m, epsilon, clipnorm);
+    return check_launch("adaptive_update_kernel<adam>");
+}
+
+extern "C" int m3d_adadelta_keras(float* params, const float* grads, float* accum, float* delta_accum,
+                                  int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
+                                  int32_t n_segments, float lr, float rho, float epsilon,
+                                  float clipnorm, float* norms, m3d_stream_t s) {
+    if (n_chunks <= 0) return M3D_OK;
+    if (!params || !grads || !accum || !delta_accum || !seg_of_chunk || !l2_coef ||
+        (clipnorm > 0.f && !norms))
+        return einval("adadelta: null pointer");
+    int rc = clip_norms(params, grads, n_chunks, seg_of_chunk, l2_coef, n_segments, clipnorm, norms, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(adaptive_update_kernel<2>, dim3((unsigned)n_chunks), dim3(256), 0, st(s),
+                       params, grads, accum, delta_accum, (float*)nullptr, seg_of_chunk, l2_coef, norms,
+                       lr, rho, 1.0f - rho, 0.f, 0.f, epsilon, clipnorm);
+    return check_launch("adaptive_update_kernel<adadelta>");
 }

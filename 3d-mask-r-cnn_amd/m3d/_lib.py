@@ -100,6 +100,9 @@ _SIGS = {
     "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
                        c_p, c_p, c_p, c_sz, c_p],
     "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p],
+    "m3d_adam_keras": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_f, c_p,
+                       c_p],
+    "m3d_adadelta_keras": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_p, c_p],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,

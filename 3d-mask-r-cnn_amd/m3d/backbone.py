@@ -41,17 +41,18 @@ class _Block:
         self.c = _Unit(store, c + "2c", b + "2c", (1, 1, 1), f2, f3, (1, 1, 1), "valid")
         self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
 
-    def __call__(self, x):
+    def __call__(self, x, links=None):
         # the two gradients of x are summed by the bwd-data kernel (GradLink)
         # instead of an autograd add: identity block 2c's residual gradient
         # into 2a's data gradient; conv block shortcut's and 2a's data gradients
+        x = x.contiguous()
         train = torch.is_grad_enabled() and x.requires_grad
         if self.sc is None:
-            link = GradLink("res") if train else None
+            link = GradLink("res", x, links) if train else None
             y = self.a(x, relu=True, link=link)
             y = self.b(y, relu=True)
             return self.c(y, relu=True, residual=x, link=link)
-        link = GradLink("dx2") if train else None
+        link = GradLink("dx2", x, links) if train else None
         short = self.sc(x, relu=False, link=link)
         y = self.a(x, relu=True, link=link)
         y = self.b(y, relu=True)
@@ -80,14 +81,16 @@ class ResNet3D:
             cin = filters[2]
             self.stages.append(blocks)
         self.stage5 = stage5
+        self.links = []
 
     def __call__(self, image):
+        self.links = []                 # GradLinks of this forward (checked by check_links)
         x = self.stem(image, relu=True, need_dx=False)
         c1 = x = max_pool3d(x, (3, 3, 3), (2, 2, 1), "same")
         outs = [c1]
         for blocks in self.stages:
             for blk in blocks:
-                x = blk(x)
+                x = blk(x, self.links)
             outs.append(x)
         if not self.stage5:
             outs.append(None)
@@ -132,7 +135,7 @@ class RPNHead:
     """build_rpn_model(anchor_stride, anchors_per_location, channel): one shared
     head applied to every pyramid level (core/models.py:512-584)."""
 
-    def __init__(self, store, anchor_stride, anchors_per_location, channel):
+    def __init__(self, store, anchor_stride, anchors_per_location, channel, backbone=None):
         if anchor_stride != 1:
             raise NotImplementedError("RPN_ANCHOR_STRIDE != 1")
         self.apl = anchors_per_location
@@ -143,6 +146,7 @@ class RPNHead:
                               kernel_init=("normal", 0.001))
         self.w_grad = None
         self.b_grad = None
+        self.backbone = backbone        # its GradLinks are checked in finish_backward
 
     def __call__(self, feature_maps):
         shared = []
@@ -156,19 +160,24 @@ class RPNHead:
         w24 = torch.cat([self.cls.kernel.data.reshape(cin, 2 * apl),
                          self.bbox.kernel.data.reshape(cin, 6 * apl)], dim=1).contiguous()
         b24 = torch.cat([self.cls.bias.data, self.bbox.bias.data]).contiguous()
-        npad = -(-8 * apl // 32) * 32
-        self.w_grad = torch.zeros((cin, npad), device=w24.device, dtype=torch.float32)
-        self.b_grad = torch.zeros((npad,), device=w24.device, dtype=torch.float32)
-        logits, bbox = _RPNOut.apply(w24, b24, {"kernel": self.w_grad, "bias": self.b_grad}, apl,
-                                     *shared)
+        grads = None
+        self.w_grad = self.b_grad = None           # a new forward drops any unfinished head gradient
+        if torch.is_grad_enabled():
+            npad = -(-8 * apl // 32) * 32
+            self.w_grad = torch.zeros((cin, npad), device=w24.device, dtype=torch.float32)
+            self.b_grad = torch.zeros((npad,), device=w24.device, dtype=torch.float32)
+            grads = {"kernel": self.w_grad, "bias": self.b_grad}
+        logits, bbox = _RPNOut.apply(w24, b24, grads, apl, *shared)
         probs = torch.softmax(logits, dim=-1)
         return logits, probs, bbox
 
     def finish_backward(self):
         """Join the side-stream weight gradients (m3d.nn.join_wgrad) and fold the
         padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
-        from .nn import join_wgrad
+        from .nn import check_links, join_wgrad
         join_wgrad()
+        if self.backbone is not None:
+            check_links(self.backbone.links)
         if self.w_grad is None:
             return
         apl, cin = self.apl, 256

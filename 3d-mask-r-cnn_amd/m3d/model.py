@@ -6,7 +6,8 @@ Mirrors core/models.py:3162-3387:
   (POST_NMS_ROIS_TRAINING) -> rpn_class_loss (focal CE, 1589-1625) and
   rpn_bbox_loss (XY/Z Huber, 1629-1673), weighted 1.0 / 1.5 (3366-3376), plus
   the L2 term WEIGHT_DECAY*0.5*||w||^2/size(w) on every non-gamma/beta weight
-  (3378-3384), optimised by Keras SGD (momentum, clipnorm, decay).
+  (3378-3384), optimised by the compiled Keras optimizer (m3d.optim: SGD,
+  Adam or Adadelta with clipnorm and decay, 3349-3357).
 The two losses are tiny gathers over <= RPN_TRAIN_ANCHORS_PER_IMAGE anchors and
 run as torch ops on the GPU; all convolution / pooling / NMS work is libm3d.
 """
@@ -19,6 +20,7 @@ from . import _lib
 from .anchors import get_anchors
 from .backbone import FPN, ResNet3D, RPNHead
 from .layers import ProposalLayer
+from .optim import KerasOptimizer
 from .params import ParamStore
 
 
@@ -131,22 +133,14 @@ class RPN:
         self.backbone = ResNet3D(self.store, config.BACKBONE, stage5=True, train_bn=config.TRAIN_BN)
         self.fpn = FPN(self.store, config.TOP_DOWN_PYRAMID_SIZE)
         self.rpn = RPNHead(self.store, config.RPN_ANCHOR_STRIDE, len(config.RPN_ANCHOR_RATIOS),
-                           config.TOP_DOWN_PYRAMID_SIZE)
+                           config.TOP_DOWN_PYRAMID_SIZE, backbone=self.backbone)
         self.store.finalize(self.device, seed=seed, weight_decay=float(config.WEIGHT_DECAY))
         self.anchors = torch.from_numpy(get_anchors(config)).to(self.device)[None]
         self.proposal_layer = ProposalLayer(
             proposal_count=config.POST_NMS_ROIS_TRAINING, nms_threshold=config.RPN_NMS_THRESHOLD,
             pre_nms_limit=config.PRE_NMS_LIMIT, images_per_gpu=config.IMAGES_PER_GPU,
             rpn_bbox_std_dev=config.RPN_BBOX_STD_DEV, image_depth=config.IMAGE_DEPTH, name="ROI")
-        opt = dict(config.OPTIMIZER.get("parameters", {}))
-        self.lr = float(opt.get("learning_rate", opt.get("lr", 0.01)))
-        self.momentum = float(opt.get("momentum", 0.0))
-        self.clipnorm = float(opt.get("clipnorm", 0.0))
-        self.decay = float(opt.get("decay", 0.0))
-        self.iterations = 0
-        name = str(config.OPTIMIZER.get("name", "SGD")).upper()
-        if name != "SGD":
-            raise NotImplementedError(f"optimizer {name}: only the SGD path is implemented")
+        self.optimizer = KerasOptimizer(config.OPTIMIZER)      # RPN.compile, core/models.py:3349-3357
 
     # -- forward ----------------------------------------------------------
     def features(self, image):
@@ -168,8 +162,12 @@ class RPN:
         return lc, lb
 
     # -- one fit step -----------------------------------------------------
+    @property
+    def iterations(self):
+        return self.optimizer.iterations
+
     def current_lr(self):
-        return self.lr * (1.0 / (1.0 + self.decay * self.iterations))
+        return self.optimizer.current_lr()
 
     def proposals_async(self, out):
         """Launch the ProposalLayer (top-k, decode, 3-D NMS) of a forward's
@@ -251,14 +249,11 @@ class RPN:
         from .weights import save_weights
         save_weights(self.store, filepath)
 
-    def sgd_step(self):
-        s = self.store
-        L = _lib.load()
-        _lib.check(L.m3d_sgd_keras(s.flat.data_ptr(), s.grad_flat.data_ptr(), s.moments.data_ptr(),
-                                   s.n_chunks, s.seg_of_chunk.data_ptr(), s.l2_coef.data_ptr(),
-                                   len(s.params), float(self.current_lr()), self.momentum,
-                                   self.clipnorm, s.norms.data_ptr(), _lib.stream()), "sgd")
-        self.iterations += 1
+    def optimizer_step(self):
+        """Apply the compiled Keras optimizer (SGD / Adam / Adadelta) to store.grad_flat."""
+        self.optimizer.step(self.store)
+
+    sgd_step = optimizer_step          # name kept for callers written against the SGD-only path
 
     def l2_loss(self):
         with torch.no_grad():

@@ -94,8 +94,6 @@ WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
 # (its F(2x2x2) transforms cost more than they save at 64 channels; measured
 # on res2*_branch2b: Winograd fwd/dgrad 0.23 ms vs direct 0.27, wgrad 0.35 vs 0.33)
 WINO_WGRAD_MIN_C = int(os.environ.get("M3D_WINO_WGRAD_MIN_C", "128"))
-# single-channel stem conv in its (x, z)-window form (_stem_zwindow); measured no step gain: off
-STEM_ZWINDOW = os.environ.get("M3D_STEM_ZWINDOW", "0") == "1"
 
 
 def use_winograd(geo, cin, cout, in_sp):
@@ -168,17 +166,36 @@ class GradLink:
     mode "dx2" -- conv_block (core/models.py:192-232): x is the input of both
     the shortcut conv and conv 2a, whose backward order is not fixed: the
     first to run parks its dx and returns none, the second accumulates into
-    the parked buffer and returns the sum."""
-    __slots__ = ("buf", "mode")
+    the parked buffer and returns the sum.
 
-    def __init__(self, mode="res"):
+    A link is bound to the tensor x it carries the gradient of (its storage
+    pointer and shape): a parked buffer is only handed to that tensor's
+    consumer.  ``registry`` (a list owned by the model's forward) collects the
+    links; check_links() after the backward raises if a parked gradient was
+    never consumed (a partner backward that did not run, e.g. autograd.grad on
+    an intermediate), instead of silently dropping it."""
+    __slots__ = ("buf", "mode", "key")
+
+    def __init__(self, mode="res", x=None, registry=None):
         self.buf = None
         self.mode = mode
+        self.key = None if x is None else (x.data_ptr(), tuple(x.shape))
+        if registry is not None:
+            registry.append(self)
+
+
+def check_links(links):
+    """Raise if any GradLink still holds a parked gradient (see GradLink)."""
+    bad = [l for l in links if l.buf is not None]
+    if bad:
+        raise RuntimeError(f"{len(bad)} parked residual/shortcut gradient(s) were never consumed: "
+                           "both consumers of a linked tensor must run their backward in the same pass")
 
 
 def _link_take(link, x):
-    """(parked gradient of x, 1) if the link holds one, else (None, 0)."""
-    if link is not None and link.buf is not None and link.buf.shape == x.shape:
+    """(parked gradient of x, 1) if the link holds one for x, else (None, 0)."""
+    if link is not None and link.buf is not None and link.buf.shape == x.shape and (
+            link.key is None or link.key == (x.data_ptr(), tuple(x.shape))):
         buf, link.buf = link.buf, None
         return buf, 1
     return None, 0
@@ -199,7 +216,7 @@ class _ConvBNAct(torch.autograd.Function):
     source of y (FPN top-down add, core/models.py:3193-3204)."""
 
     @staticmethod
-    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, alt=None):
+    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None):
         B, H, W, D, Cin = x.shape
         kh, kw, kd = geo.k
         Cout = w.shape[-1]
@@ -239,9 +256,8 @@ class _ConvBNAct(torch.autograd.Function):
                                                ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
                                                ptr(ws), wsb, stream()), "conv3d_fwd_wino")
         else:
-            cx, cw, cg = (x, w, geo) if alt is None else alt     # alt: the z-window stem form
-            check(_L().m3d_conv3d_fwd(ptr(cx), *cx.shape, ptr(cw), *cg.k, Cout, OH, OW, OD,
-                                      *cg.stride, *cg.pad, ptr(b), ptr(scale), ptr(shift),
+            check(_L().m3d_conv3d_fwd(ptr(x), *x.shape, ptr(w), *geo.k, Cout, OH, OW, OD,
+                                      *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
                                       ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
                                       None, 0, 0, stream()), "conv3d_fwd")
         if LAYER_LOG is not None:
@@ -253,13 +269,9 @@ class _ConvBNAct(torch.autograd.Function):
                 exe = 2.0 * 16 * (nz + 2) * tiles * Cin * Cout
             nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
             _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
-        ctx.alt_geo = None
-        if alt is not None:          # the weight gradient runs on the z-window form too
-            x, ctx.alt_geo = alt[0], alt[2]
         ctx.save_for_backward(x, w, y, z)
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.link = link
-        ctx.alt = alt is not None
         ctx.res_shape = None if residual is None else tuple(residual.shape)
         return y
 
@@ -326,16 +338,8 @@ class _ConvBNAct(torch.autograd.Function):
                       "conv3d_bwd_data_wino")
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
-            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None
-        if grads.get("kernel") is not None and ctx.alt:
-            # window form of the stem: dW64 [kh,1,1,64,Cout] from x64, folded into dW [kh,kw,kd,1,Cout]
-            ga = ctx.alt_geo
-            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                dwa = torch.zeros(tuple(ga.k) + (Cin, Cout), device=x.device, dtype=torch.float32)
-                check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, *ga.k, Cout, OH, OW, OD,
-                                              *ga.stride, *ga.pad, ptr(dwa), stream()), "conv3d_bwd_weight")
-                grads["kernel"].view(kh, kw, kd, Cout).add_(dwa.view(kh, 8, 8, Cout)[:, :kw, :kd])
-        elif grads.get("kernel") is not None:
+            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None
+        if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                               OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
@@ -371,31 +375,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
-        return dx, dr, None, None, None, None, None, None, None, None, None, None
-
-
-def _stem_zwindow(x, w, geo):
-    """Single-channel k^3 conv with z-stride 1 (the 7^3 stem, core/models.py:243)
-    as a (kh, 1, 1) conv over 64 channels: x64[b, y, ox, oz, 8*kx + k] =
-    x[b, y, sx*ox - px + kx, oz - pz + k] (zero for kx >= kw or k >= kd, and
-    outside the volume), w64[ky, 0, 0, 8*kx + k, :] = w[ky, kx, k, 0, :].  64
-    channels put the implicit GEMM on its float4 A loader (a scalar gather per
-    tap for Cin = 1).  The same products with exact zeros for the padding taps
-    (the MFMA k-grouping shifts, so sums agree to fp32 rounding)."""
-    B, H, W, D, _ = x.shape
-    kh, kw, kd = geo.k
-    py, px, pz = geo.pad
-    OH, OW, OD = geo.out
-    sx = geo.stride[1]
-    hw = max(0, (OW - 1) * sx - px + kw - 1 - (W - 1))
-    hd = max(0, OD - 1 - pz + kd - 1 - (D - 1))
-    xp = torch.nn.functional.pad(x[..., 0], (pz, hd, px, hw))
-    win = xp.unfold(2, kw, sx)[:, :, :OW].unfold(3, kd, 1)[:, :, :, :OD]        # [B,H,OW,OD,kw,kd]
-    x64 = torch.nn.functional.pad(win, (0, 8 - kd, 0, 8 - kw)).reshape(B, H, OW, OD, 64)
-    w64 = torch.zeros((kh, 1, 1, 8, 8, w.shape[-1]), device=w.device, dtype=torch.float32)
-    w64[:, 0, 0, :kw, :kd, :] = w[:, :, :, 0, :]
-    g64 = ConvGeom((kh, 1, 1), (geo.stride[0], 1, 1), (py, 0, 0), geo.out)
-    return x64, w64.reshape(kh, 1, 1, 64, -1), g64
+        return dx, dr, None, None, None, None, None, None, None, None, None
 
 
 def _slab_extend(x, geo):
@@ -427,13 +407,9 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     if residual is not None:
         residual = residual.contiguous()
     x, geo = _slab_extend(x, geo)
-    alt = None
-    if STEM_ZWINDOW and x.shape[-1] == 1 and geo.k[1] <= 8 and 1 < geo.k[2] <= 8 and geo.stride[2] == 1 and not (
-            need_dx and x.requires_grad) and residual is None:
-        alt = _stem_zwindow(x, w, geo)
     # the function must see at least one tensor requiring grad to be recorded
     return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                            need_dx and x.requires_grad, link, alt)
+                            need_dx and x.requires_grad, link)
 
 
 class _MaxPool(torch.autograd.Function):
@@ -532,7 +508,7 @@ class _RPNOut(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits, dbbox):
         w24, *shared = ctx.saved_tensors
-        apl, rows, grads = ctx.apl, ctx.rows, ctx.grads
+        apl, rows, grads = ctx.apl, ctx.rows, ctx.grads or {}
         B = shared[0].shape[0]
         Cin = shared[0].shape[-1]
         n_out = 8 * apl

@@ -391,6 +391,21 @@ int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, i
 int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
                   const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
                   float lr, float momentum, float clipnorm, float* norms, m3d_stream_t s);
+/* Keras 2.3.1 Adam (keras.optimizers.Adam, the `else` branch of RPN.compile,
+ * core/models.py:3356-3357) on the same flat buffers: m, v (and vhat when
+ * amsgrad; NULL otherwise) are [n_chunks*1024] moment buffers, lr_t =
+ * lr_decayed*sqrt(1-beta_2^t)/(1-beta_1^t) (t = iterations+1) is computed by
+ * the caller, epsilon defaults to K.epsilon() = 1e-7 in Keras. */
+int m3d_adam_keras(float* params, const float* grads, float* m, float* v, float* vhat,
+                   int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
+                   int32_t n_segments, float lr_t, float beta_1, float beta_2, float epsilon,
+                   float clipnorm, float* norms, m3d_stream_t s);
+/* Keras 2.3.1 Adadelta (core/models.py:3354-3355): accum / delta_accum are the
+ * accumulators of keras.optimizers.Adadelta, lr the decayed learning rate. */
+int m3d_adadelta_keras(float* params, const float* grads, float* accum, float* delta_accum,
+                       int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
+                       int32_t n_segments, float lr, float rho, float epsilon, float clipnorm,
+                       float* norms, m3d_stream_t s);
 
 #ifdef __cplusplus
 }

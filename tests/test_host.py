@@ -99,23 +99,69 @@ def test_gradlink_res_mode_never_parks_data_gradients():
     assert acc == 1 and torch.equal(buf, torch.full((4,), 5.0)) and link.buf is None
 
 
-@pytest.mark.parametrize("shape,stride", [((1, 12, 10, 9, 1), (2, 2, 1)), ((2, 9, 8, 16, 1), (1, 1, 1))])
-def test_stem_zwindow_form_is_the_same_conv(shape, stride):
-    """The stem's window form (x64 = the 8x8 (x, z) windows of x as channels,
-    w64 = the kw x kd taps zero-padded to 8 x 8, a (kh, 1, 1) conv) equals the
-    7^3 conv (float64)."""
-    import torch
-    from m3d.nn import _stem_zwindow, conv_geom
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(shape, generator=g)
-    w = torch.randn((7, 7, 7, 1, 5), generator=g)
-    geo = conv_geom(shape[1:4], (7, 7, 7), stride, 3)
-    x8, w8, g8 = _stem_zwindow(x, w, geo)
-    assert x8.shape[-1] == 64 and g8.k == (7, 1, 1) and g8.out == geo.out
+def test_keras_optimizer_selection_and_params():
+    """RPN.compile's optimizer switch (core/models.py:3349-3357) and
+    _keras_opt_params renaming (core/models.py:117-125)."""
+    from m3d.optim import KerasOptimizer
+    assert KerasOptimizer({"name": "sgd", "parameters": {"learning_rate": 0.1}}).kind == "SGD"
+    assert KerasOptimizer({"name": "Adadelta"}).kind == "ADADELTA"
+    for other in ("ADAM", "RMSprop", "nadam"):
+        assert KerasOptimizer({"name": other}).kind == "ADAM"
+    o = KerasOptimizer({"name": "ADAM", "parameters": {"learning_rate": 0.01, "beta1": 0.8, "beta2": 0.9}})
+    assert o.lr == 0.01 and o.params["beta_1"] == 0.8 and o.params["beta_2"] == 0.9
+    assert o.params["epsilon"] == 1e-7 and o.params["amsgrad"] is False
+    assert KerasOptimizer({"name": "ADADELTA"}).params == {"lr": 1.0, "rho": 0.95, "epsilon": 1e-7}
+    with pytest.raises(TypeError):
+        KerasOptimizer({"name": "SGD", "parameters": {"beta_1": 0.9}})
 
-    def conv(xc, wc, gg):   # channels-last [B,H,W,D,C] with pad-before; crop to gg.out
-        xt = torch.nn.functional.pad(xc.permute(0, 4, 1, 2, 3).double(),
-                                     (gg.pad[2], 16, gg.pad[1], 16, gg.pad[0], 16))
-        y = torch.nn.functional.conv3d(xt, wc.permute(4, 3, 0, 1, 2).double(), stride=gg.stride)
-        return y[:, :, :gg.out[0], :gg.out[1], :gg.out[2]]
-    torch.testing.assert_close(conv(x8, w8, g8), conv(x, w, geo), rtol=0, atol=1e-12)
+
+def test_keras_optimizer_schedule_float32():
+    """lr/(1+decay*it) and Adam's lr*sqrt(1-b2^t)/(1-b1^t), evaluated in float32."""
+    from m3d.optim import KerasOptimizer
+    o = KerasOptimizer({"name": "ADAM", "parameters": {"lr": 0.001, "decay": 0.5}})
+    assert o.adam_lr_t() == pytest.approx(0.001 * np.sqrt(1 - 0.999) / (1 - 0.9), rel=1e-4)   # 1-b2 cancels in float32, as in TF
+    o.iterations = 2
+    assert o.current_lr() == pytest.approx(0.001 / 2.0, rel=1e-7)
+    assert o.adam_lr_t() == pytest.approx(0.0005 * np.sqrt(1 - 0.999 ** 3) / (1 - 0.9 ** 3), rel=1e-4)
+    assert isinstance(o.current_lr(), float) and np.float32(o.current_lr()) == o.current_lr()
+
+
+def test_optim_oracle_known_answers():
+    """Single-step known answers of oracle/optim_ref.py, worked by hand."""
+    from oracle import optim_ref as O
+    p = np.array([1.0, -2.0], np.float32)
+    g = np.array([0.5, 0.0], np.float32)
+    # Adam step 1: m=(1-b1)g, v=(1-b2)g^2, lr_t = lr*sqrt(1-b2)/(1-b1)  ->  p - lr*g/(|g|+eps*...) ~ p - lr*sign(g)
+    out = O.step("ADAM", p, g, {}, 0, 0.1)
+    assert out[0] == pytest.approx(1.0 - 0.1, abs=1e-5) and out[1] == -2.0
+    # Adadelta step 1 with rho=0.5, eps=1e-7: a = 0.5 g^2, u = g*sqrt(eps)/sqrt(a+eps)
+    st = {}
+    out = O.step("ADADELTA", p, g, st, 0, 1.0, rho=0.5)
+    u = 0.5 * np.sqrt(1e-7) / np.sqrt(0.125 + 1e-7)
+    assert out[0] == pytest.approx(1.0 - u, rel=1e-6)
+    assert st["d"][0] == pytest.approx(0.5 * u * u, rel=1e-5)
+    # SGD with momentum 0.5, two steps: v1 = -lr g, v2 = 0.5 v1 - lr g
+    st = {}
+    p1 = O.step("SGD", p, g, st, 0, 0.1, momentum=0.5)
+    p2 = O.step("SGD", p1, g, st, 1, 0.1, momentum=0.5)
+    assert p2[0] == pytest.approx(1.0 - 0.05 - 0.075, abs=1e-7)
+    # clip_by_norm: ||(3,4)|| = 5 clipped to 1
+    np.testing.assert_allclose(O.clip_by_norm(np.array([3.0, 4.0], np.float32), 1.0), [0.6, 0.8], rtol=1e-6)
+
+
+def test_gradlink_is_bound_and_checked():
+    """A parked gradient goes only to the tensor the link was made for, and an
+    unconsumed one is reported by check_links (no silent drop)."""
+    import torch
+    from m3d.nn import GradLink, _link_take, check_links
+    reg = []
+    x, other = torch.zeros(4), torch.zeros(4)
+    link = GradLink("res", x, reg)
+    assert reg == [link]
+    link.buf = torch.ones(4)
+    assert _link_take(link, other) == (None, 0)          # same shape, different tensor
+    with pytest.raises(RuntimeError, match="never consumed"):
+        check_links(reg)
+    buf, acc = _link_take(link, x)
+    assert acc == 1 and link.buf is None
+    check_links(reg)
