@@ -59,8 +59,9 @@ class OverlappedAllReduce:
     finish_backward) keep their buckets until ``finish``, which launches the
     rest, waits for all, and averages."""
 
-    def __init__(self, store, world, bucket=BUCKET_FLOATS):
+    def __init__(self, store, world, bucket=BUCKET_FLOATS, average=True, group=None):
         self.store, self.world = store, world
+        self.average, self.group = average, group
         flat = store.grad_flat
         self.base = flat.data_ptr()
         self.esize = flat.element_size()
@@ -114,7 +115,7 @@ class OverlappedAllReduce:
         if self.launched[b] is None:
             s, e = self.bounds[b]
             self.launched[b] = dist.all_reduce(self.store.grad_flat[s:e], op=dist.ReduceOp.SUM,
-                                               async_op=True)
+                                               group=self.group, async_op=True)
             self.order.append(b)
 
     def finish(self):
@@ -123,7 +124,8 @@ class OverlappedAllReduce:
             self._launch(b)
         for w in self.launched:
             w.wait()
-        self.store.grad_flat.mul_(1.0 / self.world)
+        if self.average:
+            self.store.grad_flat.mul_(1.0 / self.world)
 
 
 def data_parallel_train_step(model, image, targets, world, proposals=True, overlap=True):
@@ -151,7 +153,7 @@ def data_parallel_train_step(model, image, targets, world, proposals=True, overl
         hook.finish()
     else:
         allreduce_mean_(model.store.grad_flat, world)
-    model.sgd_step()
+    model.optimizer_step()
     return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
             "rpn_rois": join() if join is not None else None}
 
@@ -200,22 +202,42 @@ class SlabRPN:
         return {"rpn_class_logits": logits, "rpn_class": probs, "rpn_bbox": bbox, "rpn_rois": rois,
                 "feature_maps": fmaps}
 
-    def train_step(self, image_slab, proposals=True):
+    def train_step(self, image_slab, proposals=True, apply=True, overlap=True):
+        """One sharded step.  The weight gradients (partial sums of one
+        gradient) are SUM-all-reduced in buckets DURING the backward
+        (OverlappedAllReduce, as the data-parallel path) -- the halo exchanges
+        and the bucket all-reduces then share the backward.  apply=False stops
+        before the optimizer (tests compare the reduced gradient)."""
+        from . import nn as mnn
         from . import slab
         m = self.model
         m.store.zero_grad()
-        out = self.forward(image_slab, proposals=False)
-        lc, lb = m.losses(out, self.targets)
-        total = lc * m.LOSS_WEIGHTS["rpn_class_loss"] + lb * m.LOSS_WEIGHTS["rpn_bbox_loss"]
-        with slab.active(self.sg):          # halo gradients flow during backward
-            total.backward()
+        hook = None
+        if self.sg.world > 1 and overlap:
+            hook = getattr(self, "_hook", None)
+            if hook is None:
+                hook = self._hook = OverlappedAllReduce(m.store, self.sg.world, average=False)
+            hook.reset()
+            mnn.GRAD_HOOK = hook
+        try:
+            out = self.forward(image_slab, proposals=False)
+            lc, lb = m.losses(out, self.targets)
+            total = lc * m.LOSS_WEIGHTS["rpn_class_loss"] + lb * m.LOSS_WEIGHTS["rpn_bbox_loss"]
+            with slab.active(self.sg):          # halo gradients flow during backward
+                total.backward()
+        finally:
+            mnn.GRAD_HOOK = None
         m.rpn.finish_backward()
-        self.sg.all_reduce_sum_(m.store.grad_flat)
-        m.sgd_step()
+        if hook is not None:
+            hook.finish()
+        else:
+            self.sg.all_reduce_sum_(m.store.grad_flat)
         if proposals:
             out["rpn_rois"] = m.proposal_layer.call_slab([out["rpn_class"], out["rpn_bbox"], m.anchors],
                                                          self.sg, self.local_index)
+        if apply:
+            m.optimizer_step()
         parts = torch.stack([total.detach(), lc.detach(), lb.detach()])
         self.sg.all_reduce_sum_(parts)
         return {"loss": parts[0], "rpn_class_loss": parts[1], "rpn_bbox_loss": parts[2],
-                "rpn_rois": out["rpn_rois"]}
+                "rpn_rois": out["rpn_rois"], "outputs": out}

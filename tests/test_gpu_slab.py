@@ -1,4 +1,4 @@
-"""Depth-slab sharded RPN on the GPU (m3d.parallel.SlabRPN), 2 and 3 ranks
+"""Depth-slab sharded RPN on the GPU (m3d.parallel.SlabRPN), 2, 3 and 8 ranks
 sharing the box's one GPU over gloo: the sharded forward (feature maps, RPN
 logits / deltas, merged proposals) is bit-identical to the single-volume
 forward, the loss equal and the SUM-all-reduced gradient equal up to fp32
@@ -34,5 +34,32 @@ def test_slab_rpn_matches_single_volume(cuda, tmp_path, world, D):
     for x in res:
         assert x["p2_bitexact"] and x["logits_bitexact"] and x["bbox_bitexact"], x
         assert x["rois_bitexact"], x
+        assert abs(x["loss_slab"] - x["loss_full"]) <= 1e-5 * abs(x["loss_full"]), x
+        assert x["grad_rel_err"] < 1e-4, x
+
+
+def test_slab_rpn_256_eight_ranks(cuda, tmp_path):
+    """BASELINE configs[4] geometry: ONE 256^3 volume in 8 depth slabs of 32
+    planes (8 ranks sharing the box's GPU over gloo), against the unsharded
+    256^3 step run beforehand in its own process and saved: P2..P6, RPN
+    logits / deltas and the merged proposals (15000 -> 6000) bit-exact, the
+    loss to 1e-5 and the SUM-all-reduced (overlapped) gradient to 1e-4 of its scale."""
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "slab_worker.py"), "ref", str(ref), "256", "256"],
+                       cwd=ROOT, timeout=600)          # output streams into the (-s) log
+    assert r.returncode == 0, r.returncode
+    world = 8
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "tests", "slab_worker.py"), "cmp", str(tmp_path), "256", "256", str(ref)]
+    r = subprocess.run(cmd, cwd=ROOT, timeout=900)
+    assert r.returncode == 0, r.returncode
+    res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
+    for x in res:
+        print(x)
+        assert x["z1"] - x["z0"] == 32, x
+        for k in ("p2", "p3", "p4", "p5", "p6", "logits", "bbox", "rois"):
+            assert x[f"{k}_bitexact"], (k, x)
         assert abs(x["loss_slab"] - x["loss_full"]) <= 1e-5 * abs(x["loss_full"]), x
         assert x["grad_rel_err"] < 1e-4, x
