@@ -15,8 +15,9 @@ for st in $STAGES; do
     all)  ARGS="tests -m gpu"; LIM=1200;;
     *)    ARGS="$st"; LIM=900;;
   esac
+  LOG=$OUT/pytest_$(echo $st | tr "/." "__").log
   echo "== $st"
-  timeout -k 10 $LIM $PT $ARGS > $OUT/pytest_$st.log 2>&1 || { echo "stage $st failed"; tail -80 $OUT/pytest_$st.log; exit 1; }
-  tail -3 $OUT/pytest_$st.log
+  timeout -k 10 $LIM $PT $ARGS > $LOG 2>&1 || { echo "stage $st failed"; tail -80 $LOG; exit 1; }
+  tail -3 $LOG
 done
 echo DONE

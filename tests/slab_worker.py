@@ -43,7 +43,7 @@ def full_step(model, image, match, bbox, dev):
     lc, lb = model.losses(full, RPNTargets(match, bbox, dev))
     (lc * 1.0 + lb * 1.5).backward()
     model.rpn.finish_backward()
-    return full, float(lc * 1.0 + lb * 1.5), model.store.grad_flat.detach().clone()
+    return full, float((lc * 1.0 + lb * 1.5).detach()), model.store.grad_flat.detach().clone()
 
 
 def slab_step(model, image, match, bbox, D):
@@ -85,9 +85,9 @@ def mode_ref(out_dir, S, D):
     full, loss, g = full_step(model, image, match, bbox, dev)
     torch.cuda.synchronize()
     for i, p in enumerate(full["feature_maps"]):
-        np.save(os.path.join(out_dir, f"p{i + 2}.npy"), p.cpu().numpy())
+        np.save(os.path.join(out_dir, f"p{i + 2}.npy"), p.detach().cpu().numpy())
     for k in ("rpn_class_logits", "rpn_bbox", "rpn_rois"):
-        np.save(os.path.join(out_dir, f"{k}.npy"), full[k].cpu().numpy())
+        np.save(os.path.join(out_dir, f"{k}.npy"), full[k].detach().cpu().numpy())
     np.save(os.path.join(out_dir, "grad.npy"), g.cpu().numpy())
     with open(os.path.join(out_dir, "ref.json"), "w") as f:
         json.dump({"loss": loss, "peak_gb": torch.cuda.max_memory_allocated() / 1e9}, f)
@@ -105,10 +105,10 @@ def mode_cmp(out_dir, S, D, ref_dir):
     gi = srpn.local_index.cpu().numpy()
     res = {"rank": rank, "world": world, "z0": sg.z0, "z1": sg.z1}
     for i, p in enumerate(out["feature_maps"]):
-        res[f"p{i + 2}_bitexact"] = bool(np.array_equal(p.cpu().numpy(), ld(f"p{i + 2}")[:, :, :, sg.z0:sg.z1]))
-    res["logits_bitexact"] = bool(np.array_equal(out["rpn_class_logits"].cpu().numpy(),
+        res[f"p{i + 2}_bitexact"] = bool(np.array_equal(p.detach().cpu().numpy(), ld(f"p{i + 2}")[:, :, :, sg.z0:sg.z1]))
+    res["logits_bitexact"] = bool(np.array_equal(out["rpn_class_logits"].detach().cpu().numpy(),
                                                  ld("rpn_class_logits")[:, gi]))
-    res["bbox_bitexact"] = bool(np.array_equal(out["rpn_bbox"].cpu().numpy(), ld("rpn_bbox")[:, gi]))
+    res["bbox_bitexact"] = bool(np.array_equal(out["rpn_bbox"].detach().cpu().numpy(), ld("rpn_bbox")[:, gi]))
     res["rois_bitexact"] = bool(np.array_equal(r["rpn_rois"].cpu().numpy(), ld("rpn_rois")))
     g = model.store.grad_flat.detach().cpu().numpy().astype(np.float64)
     gref = np.asarray(ld("grad"), np.float64)

@@ -127,7 +127,8 @@ def e2e128(fwd128, cuda):
     rng = np.random.default_rng(3)
     G = 8
     src = rois[rng.choice(np.nonzero(np.abs(rois).sum(1) > 0)[0][:200], G, replace=False)]
-    gt = np.clip(src + rng.normal(0, 0.01, src.shape), 0, 1).astype(np.float32)
+    ext = np.tile(src[:, 3:] - src[:, :3], 2)                 # jitter 3 % of each box's own extent
+    gt = np.clip(src + rng.normal(0, 0.03, src.shape) * ext, 0, 1).astype(np.float32)
     gt = np.concatenate([np.minimum(gt[:, :3], gt[:, 3:]), np.maximum(gt[:, :3], gt[:, 3:])], 1)
     cls = np.ones(G, np.int32)
     masks = np.zeros((S, S, S, G), bool)

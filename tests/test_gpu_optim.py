@@ -34,7 +34,7 @@ def test_keras_optimizer_steps(cuda, name, params):
     st.finalize(cuda, seed=3, weight_decay=wd)
     opt = KerasOptimizer({"name": name, "parameters": params})
     hp = keras_opt_params(params)
-    clip, decay, lr = hp.pop("clipnorm", 0.0), hp.pop("decay", 0.0), hp.pop("lr")
+    clip, decay, lr = hp.pop("clipnorm", 0.0), hp.pop("decay", 0.0), hp.pop("lr", opt.lr)
     kind = opt.kind
     ref = {p.name: p.data.detach().cpu().numpy().copy() for p in ps}
     states = {p.name: {} for p in ps}
