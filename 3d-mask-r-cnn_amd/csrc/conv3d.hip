@@ -1096,12 +1096,190 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
         }
 }
 
+// ---- weight-gradient GEMM, 256x256 tiles, transposed LDS reads -------------
+// Same product as x3_wgrad_kernel (C[b][k][n] += sum_m A[b][m][k] B[b][m][n],
+// fp32 operands with the reduction index m as their rows, exact bf16 split).
+// 512 threads = 8 waves (2 x 4; 128 x 64 outputs = 4 x 2 32x32 MFMA blocks per
+// wave), one workgroup per CU.  A k-step is 16 rows of m: every thread loads
+// two float4 of each operand (each wave one row-contiguous 1 KB access),
+// splits them and writes each plane's four bf16 with one ds_write_b64 into a
+// row-major [16 m][256 col] image (no register transpose).  The MFMA operand
+// wants 8 consecutive m of one column per lane: two ds_read_b64_tr_b16 (4 rows
+// x 16 columns per 16-lane group, gfx950's transposing LDS read) deliver it.
+// 16-B chunks are XOR-swizzled by 4*(m & 3) so the transposed reads (4 rows x
+// 4 chunks per 32-lane half) and the row writes are bank-conflict-free.  Two
+// LDS stages (2 x 48 KB); the loads of step t+2 are issued behind the MFMAs of
+// step t, their split + LDS writes follow the MFMAs of step t+1; one barrier
+// per step.  fp32 atomics out (the m range is split over workgroups).
+typedef short v4s __attribute__((ext_vector_type(4)));
+constexpr int W2_BK = 16;
+constexpr int W2_PL = W2_BK * 256 * 2;          // one plane: 16 rows x 512 B
+constexpr int W2_STAGE = 6 * W2_PL;             // 3 planes of A + 3 of B = 48 KB
+
+__device__ __forceinline__ int w2_off(int row, int col) {
+    return row * 512 + ((((col >> 3) ^ ((row & 3) << 2)) & 31) << 4) + (col & 7) * 2;
+}
+__device__ __forceinline__ bf16x8 w2_frag(const char* plane, int o1, int o2) {
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const v4s r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + o1));
+    const v4s r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + o2));
+    return __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __restrict__ A,
+                                                             const float* __restrict__ Bm,
+                                                             float* __restrict__ C, int64_t M, int K,
+                                                             int N, int64_t m_per_split, int64_t bsa,
+                                                             int64_t bsb, int64_t bsc) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * W2_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wk = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
+    const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
+    const int64_t total = gxy * gridDim.z;
+    const int64_t Lb = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int bz = (int)(Lt / gxy), rem = (int)(Lt % gxy);
+    const int k0 = (rem % gridDim.x) * 256;
+    const int n0 = (rem / gridDim.x) * 256;
+    const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
+    const int64_t batch = bz / nsplit;
+    A += batch * bsa;
+    Bm += batch * bsb;
+    C += batch * bsc;
+    const int64_t ms = (int64_t)(bz % nsplit) * m_per_split;
+    const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
+    if (ms >= me) return;
+    // loader: rows lr and lr + 8 of the step, columns lc..lc+3 of both operands
+    const int lr = tid >> 6, lc = (tid & 63) * 4;
+    const bool aok = k0 + lc < K, bok = n0 + lc < N;
+    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (uint64_t)M * K * 4);
+    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(Bm, (uint64_t)M * N * 4);
+    float4 va[2], vb[2];
+    auto load = [&](int kt) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t m = ms + (int64_t)kt * W2_BK + lr + 8 * u;
+            va[u] = bload4(rsa, (aok && m < me) ? (uint32_t)(m * K + k0 + lc) * 4u : M3D_OOB);
+            vb[u] = bload4(rsb, (bok && m < me) ? (uint32_t)(m * N + n0 + lc) * 4u : M3D_OOB);
+        }
+    };
+    auto store = [&](int buf) {
+        char* S = smem + buf * W2_STAGE;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int off = w2_off(lr + 8 * u, lc);
+            uint2 pa[3], pb[3];
+            split3x4(va[u], pa);
+            split3x4(vb[u], pb);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                *reinterpret_cast<uint2*>(S + q * W2_PL + off) = pa[q];
+                *reinterpret_cast<uint2*>(S + (3 + q) * W2_PL + off) = pb[q];
+            }
+        }
+    };
+    // transposed-read offsets: lane 4q+p of 16-lane group g reads row 8(g>>1)+q
+    // (and +4), columns base + 16(g&1) + 4p .. +3
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int trow = 8 * (g >> 1) + q, tcol = 16 * (g & 1) + 4 * p;
+    int aoff[4][2], boff[2][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        aoff[i][0] = w2_off(trow, wk * 128 + i * 32 + tcol);
+        aoff[i][1] = w2_off(trow + 4, wk * 128 + i * 32 + tcol);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        boff[j][0] = w2_off(trow, wn * 64 + j * 32 + tcol);
+        boff[j][1] = w2_off(trow + 4, wn * 64 + j * 32 + tcol);
+    }
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const int nk = (int)((me - ms + W2_BK - 1) / W2_BK);
+    load(0);
+    store(0);
+    if (nk > 1) load(1);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* S = smem + (kt & 1) * W2_STAGE;
+        bf16x8 bfr[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = w2_frag(S + (3 + pl) * W2_PL, boff[j][0], boff[j][1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[pl] = w2_frag(S + pl * W2_PL, aoff[i][0], aoff[i][1]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                floatx16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+            }
+        }
+        // the other stage was last read in step kt-1, before its closing barrier
+        if (kt + 1 < nk) store((kt + 1) & 1);
+        if (kt + 2 < nk) load(kt + 2);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wn * 64 + j * 32 + l32;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = k0 + wk * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (k < K) unsafeAtomicAdd(C + (int64_t)k * N + n, acc[i][j][r]);
+            }
+        }
+}
+
+// M3D_X3W_TR (default 1): the 256x256 transposed-read weight-gradient kernel
+// for GEMMs with K, N >= 192; 0 keeps the 128x128 x3_wgrad_kernel everywhere.
+static int wgrad_tr_env() {
+    static int v = [] { const char* e = getenv("M3D_X3W_TR"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
+static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M, int K, int N, int nbatch,
+                            int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
+    const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
+    const int64_t cus = num_cus();
+    int64_t splits = (cus + tiles - 1) / tiles;
+    const int64_t max_splits = (M + 63) / 64;              // >= 4 k-steps per workgroup
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int64_t mper = (M + splits - 1) / splits;
+    mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
+    splits = (M + mper - 1) / mper;
+    dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
+    hipLaunchKernelGGL(x3_wgrad_tr_kernel, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+}
+
 // M3D_GEMM_X3 bit 2: the batched Winograd weight-gradient GEMMs on x3_wgrad_kernel
 static int wgrad_x3_env() { return (x3_mask() >> 2) & 1; }
 
 // C[b] += A[b]^T B[b]: A [M][K], B [M][N], C [K][N], batch strides bsa/bsb/bsc
 static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M, int K, int N, int nbatch,
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
+    if (wgrad_tr_env() && K >= 192 && N >= 192) {
+        launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
+        return;
+    }
     const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;
     const int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
