@@ -113,14 +113,31 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
     m = bf16_bits(r);
     l = bf16_bits(r - __uint_as_float(m << 16));
 }
-// float4 (4 consecutive k) -> three 4 x bf16 packets (element j at bits 16j)
+// float4 (4 consecutive k) -> three 4 x bf16 packets (element j at bits 16j).
+// Two elements per conversion (v_cvt_pk_bf16_f32 with two sources) and per
+// subtraction (v_pk_add_f32): 20 VALU per float4 instead of 41 for four
+// scalar split3 -- the same bits (both subtractions exact).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(f32x2_t v) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ f32x2_t unpk_bf16(uint32_t p) {
+    return f32x2_t{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3x2(f32x2_t x, uint32_t& h, uint32_t& m, uint32_t& l) {
+    h = pk_bf16(x);
+    const f32x2_t r = x - unpk_bf16(h);
+    m = pk_bf16(r);
+    l = pk_bf16(r - unpk_bf16(m));
+}
 __device__ __forceinline__ void split3x4(const float4& v, uint2* o) {
-    uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
-    split3(v.x, h0, m0, l0); split3(v.y, h1, m1, l1);
-    split3(v.z, h2, m2, l2); split3(v.w, h3, m3, l3);
-    o[0] = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
-    o[1] = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
-    o[2] = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split3x2(f32x2_t{v.x, v.y}, h0, m0, l0);
+    split3x2(f32x2_t{v.z, v.w}, h1, m1, l1);
+    o[0] = make_uint2(h0, h1);
+    o[1] = make_uint2(m0, m1);
+    o[2] = make_uint2(l0, l1);
 }
 // byte offset of (row, k) in an X3 LDS plane: 32 k x bf16 = 64-B rows, 16-B
 // chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 phase over
@@ -1106,19 +1123,22 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
 // row-major [16 m][256 col] image (no register transpose).  The MFMA operand
 // wants 8 consecutive m of one column per lane: two ds_read_b64_tr_b16 (4 rows
 // x 16 columns per 16-lane group, gfx950's transposing LDS read) deliver it.
-// 16-B chunks are XOR-swizzled by 4*(m & 3) so the transposed reads (4 rows x
-// 4 chunks per 32-lane half) and the row writes are bank-conflict-free.  Two
-// LDS stages (2 x 48 KB); the loads of step t+2 are issued behind the MFMAs of
-// step t, their split + LDS writes follow the MFMAs of step t+1; one barrier
+// Rows are padded to 576 B so the transposed reads (4 rows x 64 contiguous
+// bytes per 32-lane half) and the row writes are bank-conflict-free.  Two LDS
+// stages (2 x 54 KB) and two register sets: the loads of step t+2 are issued
+// before the MFMAs of step t, the operands of step t+1 (loaded during step
+// t-1) are split and written into the other stage behind them; one barrier
 // per step.  fp32 atomics out (the m range is split over workgroups).
 typedef short v4s __attribute__((ext_vector_type(4)));
 constexpr int W2_BK = 16;
-constexpr int W2_PL = W2_BK * 256 * 2;          // one plane: 16 rows x 512 B
-constexpr int W2_STAGE = 6 * W2_PL;             // 3 planes of A + 3 of B = 48 KB
+constexpr int W2_PITCH = 512 + 64;              // row pitch: 256 bf16 + 64 B pad
+constexpr int W2_PL = W2_BK * W2_PITCH;         // one plane: 16 rows (9 KB)
+constexpr int W2_STAGE = 6 * W2_PL;             // 3 planes of A + 3 of B = 54 KB
 
-__device__ __forceinline__ int w2_off(int row, int col) {
-    return row * 512 + ((((col >> 3) ^ ((row & 3) << 2)) & 31) << 4) + (col & 7) * 2;
-}
+// The 64-B pad puts rows r..r+3 on four different 64-B bank groups, so a
+// transposed read (4 rows x 64 contiguous bytes per 32-lane half) is
+// conflict-free, and every fragment offset is a constant from one base.
+__device__ __forceinline__ int w2_off(int row, int col) { return row * W2_PITCH + col * 2; }
 __device__ __forceinline__ bf16x8 w2_frag(const char* plane, int o1, int o2) {
     typedef __attribute__((address_space(3))) v4s lds_v4s;
     const v4s r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + o1));
@@ -1126,6 +1146,10 @@ __device__ __forceinline__ bf16x8 w2_frag(const char* plane, int o1, int o2) {
     return __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// DBG (timing probes, selected by M3D_X3W_DBG): 1 no global loads, 2 no MFMAs,
+// 3 neither split nor LDS writes (MFMAs on a stale stage), 4 loads issued and
+// waited for at once, their data unused, 5 loads only (no split, no MFMA)
+template <int DBG>
 __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __restrict__ A,
                                                              const float* __restrict__ Bm,
                                                              float* __restrict__ C, int64_t M, int K,
@@ -1153,18 +1177,46 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
     // loader: rows lr and lr + 8 of the step, columns lc..lc+3 of both operands
     const int lr = tid >> 6, lc = (tid & 63) * 4;
     const bool aok = k0 + lc < K, bok = n0 + lc < N;
-    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A, (uint64_t)M * K * 4);
-    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(Bm, (uint64_t)M * N * 4);
-    float4 va[2], vb[2];
-    auto load = [&](int kt) {
+    const uint32_t mrows = (uint32_t)(me - ms);
+    // wave-uniform descriptors (a per-lane base would wrap every load in a
+    // readfirstlane waterfall loop); rows relative to ms, 32-bit offsets
+    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A + ms * K + k0, (uint64_t)(M - ms) * K * 4);
+    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(Bm + ms * N + n0, (uint64_t)(M - ms) * N * 4);
+    const uint32_t oc = (uint32_t)lc * 4u;
+    const uint32_t rowa = (uint32_t)K * 4u, rowb = (uint32_t)N * 4u;
+    const int nk = (int)((me - ms + W2_BK - 1) / W2_BK);
+    // Every workgroup walks its m range from a different step (rotation by
+    // its tile index; the N-tiles sharing an A tile, same index, stay in step
+    // for L2): the 256 concurrent streams start 8-16 MB apart, and in lockstep
+    // they would hit the same HBM channels (2.2 TB/s measured without it).
+    const int rot = (int)(((int64_t)bz * 17) % nk);
+    // steps past the last one load zeros (out-of-range offset): no branch in the loop
+    auto load = [&](int kt, float4 (&va)[2], float4 (&vb)[2]) {
+        const int ph = kt + rot >= nk ? kt + rot - nk : kt + rot;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int64_t m = ms + (int64_t)kt * W2_BK + lr + 8 * u;
-            va[u] = bload4(rsa, (aok && m < me) ? (uint32_t)(m * K + k0 + lc) * 4u : M3D_OOB);
-            vb[u] = bload4(rsb, (bok && m < me) ? (uint32_t)(m * N + n0 + lc) * 4u : M3D_OOB);
+            const uint32_t m = (uint32_t)ph * W2_BK + lr + 8 * u;
+            const bool in = kt < nk && m < mrows;
+            if (DBG == 1) {
+                va[u] = make_float4(m, u, kt, 1.0f);
+                vb[u] = make_float4(u, m, 2.0f, kt);
+            } else if (DBG == 4) {     // real loads, results sunk at once (no use)
+                float4 ta = bload4(rsa, (in && aok) ? oc + m * rowa : M3D_OOB);
+                float4 tb = bload4(rsb, (in && bok) ? oc + m * rowb : M3D_OOB);
+                asm volatile("" ::"v"(ta.x), "v"(tb.x));
+                va[u] = make_float4(m, u, kt, 1.0f);
+                vb[u] = make_float4(u, m, 2.0f, kt);
+            } else {
+                va[u] = bload4(rsa, (in && aok) ? oc + m * rowa : M3D_OOB);
+                vb[u] = bload4(rsb, (in && bok) ? oc + m * rowb : M3D_OOB);
+            }
         }
     };
-    auto store = [&](int buf) {
+    auto split_store = [&](int buf, const float4 (&va)[2], const float4 (&vb)[2]) {
+        if (DBG == 3 || DBG == 5) {
+            asm volatile("" ::"v"(va[0].x), "v"(va[1].x), "v"(vb[0].x), "v"(vb[1].x));
+            return;
+        }
         char* S = smem + buf * W2_STAGE;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -1183,17 +1235,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
     // (and +4), columns base + 16(g&1) + 4p .. +3
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
     const int trow = 8 * (g >> 1) + q, tcol = 16 * (g & 1) + 4 * p;
-    int aoff[4][2], boff[2][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        aoff[i][0] = w2_off(trow, wk * 128 + i * 32 + tcol);
-        aoff[i][1] = w2_off(trow + 4, wk * 128 + i * 32 + tcol);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        boff[j][0] = w2_off(trow, wn * 64 + j * 32 + tcol);
-        boff[j][1] = w2_off(trow + 4, wn * 64 + j * 32 + tcol);
-    }
+    const int abase = w2_off(trow, wk * 128 + tcol), bbase = w2_off(trow, wn * 64 + tcol);
     floatx16 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1201,25 +1243,25 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-    const int nk = (int)((me - ms + W2_BK - 1) / W2_BK);
-    load(0);
-    store(0);
-    if (nk > 1) load(1);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
+    auto mfma_step = [&](int kt) {
         const char* S = smem + (kt & 1) * W2_STAGE;
         bf16x8 bfr[2][3];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = w2_frag(S + (3 + pl) * W2_PL, boff[j][0], boff[j][1]);
+            for (int pl = 0; pl < 3; ++pl)
+                bfr[j][pl] = w2_frag(S + (3 + pl) * W2_PL + j * 64, bbase, bbase + 4 * W2_PITCH);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             bf16x8 af[3];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) af[pl] = w2_frag(S + pl * W2_PL, aoff[i][0], aoff[i][1]);
+            for (int pl = 0; pl < 3; ++pl) af[pl] = w2_frag(S + pl * W2_PL + i * 64, abase, abase + 4 * W2_PITCH);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
+                if (DBG == 2 || DBG == 5) {
+                    acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
+                    continue;
+                }
                 floatx16 c = acc[i][j];
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
@@ -1229,9 +1271,26 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
             }
         }
-        // the other stage was last read in step kt-1, before its closing barrier
-        if (kt + 1 < nk) store((kt + 1) & 1);
-        if (kt + 2 < nk) load(kt + 2);
+    };
+    // two named register sets (static indexing): X carries step kt+1 (loaded
+    // during step kt-1), Y receives step kt+2; the roles swap every step
+    float4 xa[2], xb[2], ya[2], yb[2];
+    load(0, xa, xb);
+    split_store(0, xa, xb);
+    load(1, xa, xb);
+    __syncthreads();
+    // sched_barrier(0) pins each step's loads ahead of its MFMAs (hipcc would
+    // sink them to the end of the step, leaving one step of latency cover)
+    for (int kt = 0; kt < nk; kt += 2) {
+        load(kt + 2, ya, yb);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(kt);
+        split_store((kt + 1) & 1, xa, xb);   // the other stage: last read in step kt-1
+        __syncthreads();
+        load(kt + 3, xa, xb);                // zeros past the end (no branch)
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(kt + 1);                   // past nk: a stage of zeros, no effect
+        split_store(kt & 1, ya, yb);
         __syncthreads();
     }
 #pragma unroll
@@ -1267,7 +1326,15 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
-    hipLaunchKernelGGL(x3_wgrad_tr_kernel, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+    static const int dbg = [] { const char* e = getenv("M3D_X3W_DBG"); return e ? atoi(e) : 0; }();
+    switch (dbg) {
+        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
+        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
+        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
+        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
+        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
+        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+    }
 }
 
 // M3D_GEMM_X3 bit 2: the batched Winograd weight-gradient GEMMs on x3_wgrad_kernel
