@@ -2056,6 +2056,151 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
     }
 }
 
+// ---- the same batched GEMM, 256x256 tiles, LDS-DMA staged -------------------
+// C[b][m][n] = sum_k A[b][m][k] B[b][n][k] on the pre-split planes (as
+// x3_gemm_kernel).  512 threads = 8 waves (2 x 4; 128 x 64 outputs = 4 x 2
+// 32x32 blocks per wave), one workgroup per CU.  A stage is 16 k of all six
+// planes (3 of A, 3 of B; 256 rows x 32 B = 8 KB each, 48 KB): every wave
+// moves 32 rows of each plane with one buffer_load_dwordx4 ... lds (1 KB,
+// written lane-linearly), so the conflict-free x3_off16 swizzle of the image
+// (chunk flipped for rows 8..15 of each 16) goes on the SOURCE address.  Three
+// LDS stages: the loads of step t+2 are issued right after the barrier that
+// ends step t-1's reads of that stage, and stay in flight across the next
+// barrier -- a counted vmcnt(6) retires exactly step t's DMA before the
+// barrier that precedes its reads (raw s_barrier: __syncthreads() would emit a
+// vmcnt(0) and drain the prefetch).  No VGPR staging, no VALU in the loop.
+constexpr int G2_BK = 16;
+constexpr int G2_PL = 256 * G2_BK * 2;   // one plane of one operand: 8 KB
+constexpr int G2_STAGE = 6 * G2_PL;      // 48 KB
+constexpr int G2_NST = 3;
+
+__device__ __forceinline__ void g2_dma(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff,
+                                             0, 0, 0);
+}
+
+// DBG (timing probes, M3D_X3_256_DBG): 1 no epilogue stores, 2 no MFMAs,
+// 3 no DMA (MFMAs on stale stages), 4 neither MFMAs nor stores (DMA only)
+template <int DBG>
+__global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
+    __shared__ __attribute__((aligned(16))) char smem[G2_NST * G2_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
+    const int64_t nbx = (g.M + 255) / 256, nby = g.N / 256;
+    const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
+    const int64_t L = (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+    if (L >= total) return;
+    const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+    const int64_t bz = T / per_batch, Tt = T - bz * per_batch;
+    const int64_t m0 = (Tt / nby) * 256;
+    const int64_t n0 = (Tt % nby) * 256;
+    // descriptors start at the tile's first row: rows past M read zeros
+    __amdgpu_buffer_rsrc_t rs[6];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+        rs[pl] = make_rsrc(g.a + pl * g.psa + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 2);
+        rs[3 + pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + n0 * g.K, (uint64_t)256 * g.K * 2);
+    }
+    // loader lane: row 32 wave + lane/2 of every plane, LDS slot lane&1 holds
+    // k-chunk (slot ^ row bit 3) -- the x3_off16 image
+    const int lrow = 32 * wave + (lane >> 1);
+    const uint32_t lsrc = (uint32_t)lrow * (uint32_t)g.K * 2u + (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4);
+    const int nk = g.K / G2_BK;
+    auto issue = [&](int kt) {
+        char* S = smem + (kt % G2_NST) * G2_STAGE + wave * 1024;
+        const uint32_t off = lsrc + (uint32_t)kt * (G2_BK * 2);
+        if (DBG == 3) return;
+#pragma unroll
+        for (int pl = 0; pl < 6; ++pl) g2_dma(rs[pl], S + pl * G2_PL, off);
+    };
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    issue(0);
+    if (nk > 1) issue(1);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // stage kt+2 reuses the stage of step kt-1, whose reads all waves
+        // finished before the barrier above
+        if (kt + 2 < nk) issue(kt + 2);
+        const char* S = smem + (kt % G2_NST) * G2_STAGE;
+        bf16x8 bfr[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int off = x3_off16(wn * 64 + j * 32 + l32, h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                bfr[j][pl] = *reinterpret_cast<const bf16x8*>(S + (3 + pl) * G2_PL + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int off = x3_off16(wm * 128 + i * 32 + l32, h);
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(S + pl * G2_PL + off);
+            // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (DBG == 2 || DBG == 4) {
+                    acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
+                    continue;
+                }
+                floatx16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+            }
+        }
+    }
+    if (DBG == 1 || DBG == 4) {   // keep the accumulators live, store nothing
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        if (t == 1.2345f) g.c[0] = t;
+        return;
+    }
+    // epilogue straight from the accumulators: per store instruction two
+    // 128-B row segments; rows past M dropped by the descriptor's range
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = (int)n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                // (a named copy: hipcc 7.2 miscompiles __builtin_bit_cast of a
+                // vector-element lvalue into a read of element 0)
+                const float v = acc[i][j][r];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                      (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u),
+                                                      0, 0);
+            }
+        }
+}
+
+// M3D_X3_256 (default 1): the Winograd point GEMMs with N % 256 == 0 on
+// x3_gemm256_kernel; 0 keeps x3_gemm_kernel everywhere (A/B)
+static int x3_256_env() {
+    static int v = [] { const char* e = getenv("M3D_X3_256"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 // M3D_WINO_NZ = 2 selects the F(2x2x2) tiles (A/B testing; default 4: F(2x2x4))
 static int wino_nz() {
     static int v = [] { const char* e = getenv("M3D_WINO_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
@@ -2475,6 +2620,19 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
     q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
     q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
+    if (!af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
+        const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
+        const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
+        static const int dbg = [] { const char* e = getenv("M3D_X3_256_DBG"); return e ? atoi(e) : 0; }();
+        switch (dbg) {
+            case 1: hipLaunchKernelGGL(x3_gemm256_kernel<1>, grid, dim3(512), 0, s, q); break;
+            case 2: hipLaunchKernelGGL(x3_gemm256_kernel<2>, grid, dim3(512), 0, s, q); break;
+            case 3: hipLaunchKernelGGL(x3_gemm256_kernel<3>, grid, dim3(512), 0, s, q); break;
+            case 4: hipLaunchKernelGGL(x3_gemm256_kernel<4>, grid, dim3(512), 0, s, q); break;
+            default: hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
+        }
+        return;
+    }
     const int64_t tiles = ((T + 127) / 128) * ((N + 127) / 128) * P;
     const bool bk16 = x3_bk_env() == 16;
     const bool occ3 = !bk16 && x3_occ3_env();

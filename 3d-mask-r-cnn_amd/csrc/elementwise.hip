@@ -482,12 +482,34 @@ using namespace m3d;
 
 static unsigned ew_grid(int64_t n) { return grid_for(n, 256, 256 * 32); }
 
+// KL.MaxPooling3D argument checks (the kernels index with 32-bit ints)
+static int check_pool_args(int64_t B, int64_t H, int64_t W, int64_t D, int64_t C, int kh, int kw, int kd,
+                           int sy, int sx, int sz, int py, int px, int pz, int64_t OH, int64_t OW, int64_t OD) {
+    if (B < 0 || H <= 0 || W <= 0 || D <= 0 || C <= 0 || OH <= 0 || OW <= 0 || OD <= 0)
+        return einval("maxpool3d: dimensions must be positive");
+    if (kh <= 0 || kw <= 0 || kd <= 0) return einval("maxpool3d: pool size must be positive");
+    if (kh * kw * kd > 255) return einval("maxpool3d: window larger than 255");
+    if (sy <= 0 || sx <= 0 || sz <= 0) return einval("maxpool3d: strides must be positive");
+    if (py < 0 || px < 0 || pz < 0) return einval("maxpool3d: padding must be non-negative");
+    if (B * H * W * D * C > 0x7FFFFFFFll || B * OH * OW * OD * C > 0x7FFFFFFFll)
+        return einval("maxpool3d: tensor larger than 2^31 elements");
+    return M3D_OK;
+}
+
+static int check_resample_args(const char* what, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C) {
+    if (B < 0 || H < 0 || W < 0 || D < 0 || C < 0) return einval(what);
+    if (C % 4) return einval("C must be a multiple of 4");
+    if (B * H * W * D * C > 0x7FFFFFFFll) return einval("tensor larger than 2^31 elements");
+    return M3D_OK;
+}
+
 extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
                                  int64_t C, int32_t kh, int32_t kw, int32_t kd, int32_t sy,
                                  int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
                                  int64_t OH, int64_t OW, int64_t OD, float* y, uint8_t* argmax,
                                  m3d_stream_t s) {
-    if (kh * kw * kd > 255) return einval("maxpool3d: window larger than 255");
+    int rc = check_pool_args(B, H, W, D, C, kh, kw, kd, sy, sx, sz, py, px, pz, OH, OW, OD);
+    if (rc) return rc;
     const int64_t total = B * OH * OW * OD * C;
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && B * H * W * D * C / 4 < 0x7FFFFFFF && total / 4 < 0x7FFFFFFF &&
@@ -509,6 +531,8 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
                                  int32_t kd, int32_t sy, int32_t sx, int32_t sz, int32_t py,
                                  int32_t px, int32_t pz, int64_t OH, int64_t OW, int64_t OD,
                                  float* dx, m3d_stream_t s) {
+    int rc = check_pool_args(B, H, W, D, C, kh, kw, kd, sy, sx, sz, py, px, pz, OH, OW, OD);
+    if (rc) return rc;
     const int64_t total = B * H * W * D * C;
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && total / 4 < 0x7FFFFFFF && B * OH * OW * OD * C / 4 < 0x7FFFFFFF &&
@@ -527,7 +551,8 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
 
 extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D,
                                    int64_t C, float* d_src, int32_t accumulate, m3d_stream_t s) {
-    if (C % 4) return einval("upsample221_bwd: C must be a multiple of 4");
+    if (int rc = check_resample_args("upsample221_bwd: negative dimension", B, H, W, D, C)) return rc;
+    if (C == 0) return einval("upsample221_bwd: C must be a positive multiple of 4");
     const int64_t total = B * H * W * D * (C / 4);
     if (total == 0) return M3D_OK;
     hipLaunchKernelGGL(upsample221_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
@@ -538,7 +563,7 @@ extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int6
 
 extern "C" int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
                                     int64_t C, float* y, m3d_stream_t s) {
-    if (C % 4) return einval("subsample221: C must be a multiple of 4");
+    if (int rc = check_resample_args("subsample221: negative dimension", B, H, W, D, C)) return rc;
     const int64_t total = B * ((H + 1) / 2) * ((W + 1) / 2) * D * (C / 4);
     if (total == 0) return M3D_OK;
     hipLaunchKernelGGL(subsample221_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
@@ -548,7 +573,7 @@ extern "C" int m3d_subsample221_fwd(const float* x, int64_t B, int64_t H, int64_
 
 extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64_t D,
                                     int64_t C, float* dx, m3d_stream_t s) {
-    if (C % 4) return einval("subsample221: C must be a multiple of 4");
+    if (int rc = check_resample_args("subsample221: negative dimension", B, H, W, D, C)) return rc;
     const int64_t total = B * ((H + 1) / 2) * ((W + 1) / 2) * D * (C / 4);
     if (total == 0) return M3D_OK;
     hipLaunchKernelGGL(subsample221_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
@@ -637,7 +662,10 @@ extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, 
                              const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
                              float lr, float momentum, float clipnorm, float* norms,
                              m3d_stream_t s) {
-    if (n_chunks <= 0) return M3D_OK;
+    if (n_chunks < 0 || n_segments < 0) return einval("sgd: negative chunk or segment count");
+    if (n_chunks == 0) return M3D_OK;
+    if (!params || !grads || !moments || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
+        return einval("sgd: null pointer");
     if (clipnorm > 0.f) {
         if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
             return check_launch("memset norms");
@@ -666,7 +694,8 @@ extern "C" int m3d_adam_keras(float* params, const float* grads, float* m, float
                               int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                               int32_t n_segments, float lr_t, float beta_1, float beta_2,
                               float epsilon, float clipnorm, float* norms, m3d_stream_t s) {
-    if (n_chunks <= 0) return M3D_OK;
+    if (n_chunks < 0 || n_segments < 0) return einval("adam: negative chunk or segment count");
+    if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !m || !v || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
         return einval("adam: null pointer");
     int rc = clip_norms(params, grads, n_chunks, seg_of_chunk, l2_coef, n_segments, clipnorm, norms, s);
@@ -687,7 +716,8 @@ extern "C" int m3d_adadelta_keras(float* params, const float* grads, float* accu
                                   int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                                   int32_t n_segments, float lr, float rho, float epsilon,
                                   float clipnorm, float* norms, m3d_stream_t s) {
-    if (n_chunks <= 0) return M3D_OK;
+    if (n_chunks < 0 || n_segments < 0) return einval("adadelta: negative chunk or segment count");
+    if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !accum || !delta_accum || !seg_of_chunk || !l2_coef ||
         (clipnorm > 0.f && !norms))
         return einval("adadelta: null pointer");

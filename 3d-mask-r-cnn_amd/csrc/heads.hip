@@ -133,7 +133,8 @@ extern "C" int m3d_detections_gather(const float* boxes_px, const float* scores,
                                      const int32_t* keep, const int32_t* num_keep,
                                      int32_t max_inst, const float* image_meta, float* det,
                                      m3d_stream_t s) {
-    if (max_inst <= 0) return M3D_OK;
+    if (max_inst < 0) return einval("detections_gather: negative DETECTION_MAX_INSTANCES");
+    if (max_inst == 0) return M3D_OK;
     hipLaunchKernelGGL(detections_kernel, dim3(grid_for(max_inst, 256)), dim3(256), 0, st(s), boxes_px,
                        scores, keep, num_keep, max_inst, image_meta, det);
     return check_launch("detections_kernel");

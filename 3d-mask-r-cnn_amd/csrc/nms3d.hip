@@ -335,7 +335,12 @@ static NmsWs nms_ws_layout(int64_t N, void* base) {
     const int64_t cb = (N + 63) / 64;
     char* p = (char*)base;
     size_t off = 0;
-    auto take = [&](size_t b) { size_t o = off; off += (b + 255) & ~(size_t)255; return p + o; };
+    // sizing pass (base == nullptr): offsets only, no arithmetic on a null pointer
+    auto take = [&](size_t b) {
+        size_t o = off;
+        off += (b + 255) & ~(size_t)255;
+        return p ? p + o : nullptr;
+    };
     w.keys = (uint64_t*)take(sizeof(uint64_t) * npad);
     w.sboxes = (float*)take(sizeof(float) * 6 * (N > 0 ? N : 1));
     w.mask = (uint64_t*)take(sizeof(uint64_t) * (size_t)(N > 0 ? N : 1) * (cb > 0 ? cb : 1));
@@ -358,11 +363,12 @@ extern "C" int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int
     if (N > (int64_t)0x7FFFFFFF) return einval("too many boxes");
     const int64_t cb = (N + 63) / 64;
     if (cb > 16384) return einval("too many boxes for the LDS-resident reduction (max 1048576)");
+    const bool work = N > 0 && max_out > 0;
+    if (work && ws_bytes < nms_ws_layout(N, nullptr).bytes) return einval("workspace too small");
     if (hipMemsetAsync(num_keep, 0, sizeof(int32_t), st(s)) != hipSuccess)
         return check_launch("memset num_keep");
-    if (N == 0 || max_out <= 0) return M3D_OK;
+    if (!work) return M3D_OK;
     NmsWs w = nms_ws_layout(N, workspace);
-    if (ws_bytes < w.bytes) return einval("workspace too small");
     const int64_t npad = pow2_at_least(N < 2 ? 2 : N);
     hipLaunchKernelGGL(nms_keys_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, st(s), scores, N,
                        npad, w.keys);
@@ -401,7 +407,8 @@ extern "C" int m3d_score_keys(const float* probs, int64_t A, int64_t* keys, m3d_
 
 extern "C" int m3d_score_keys_mapped(const float* probs, int64_t A, const int64_t* gidx,
                                      int64_t* keys, m3d_stream_t s) {
-    if (A <= 0) return M3D_OK;
+    if (A < 0) return einval("score_keys: negative anchor count");
+    if (A == 0) return M3D_OK;
     if (A > 0xFFFFFFFFll) return einval("score_keys: more than 2^32 anchors");
     hipLaunchKernelGGL(score_keys_kernel, dim3(grid_for(A, 256)), dim3(256), 0, st(s), probs, A,
                        gidx, keys);
@@ -412,7 +419,8 @@ extern "C" int m3d_proposal_decode(const float* probs, const float* deltas, cons
                                    const int64_t* order, int64_t k, const float std_dev[6],
                                    float image_depth, float* boxes, float* scores,
                                    m3d_stream_t s) {
-    if (k <= 0) return M3D_OK;
+    if (k < 0) return einval("proposal_decode: negative proposal count");
+    if (k == 0) return M3D_OK;
     Std6 sd;
     for (int q = 0; q < 6; ++q) sd.v[q] = std_dev[q];
     hipLaunchKernelGGL(proposal_decode_kernel, dim3(grid_for(k, 256)), dim3(256), 0, st(s), probs,
@@ -423,7 +431,8 @@ extern "C" int m3d_proposal_decode(const float* probs, const float* deltas, cons
 extern "C" int m3d_proposal_gather(const float* boxes, const int32_t* keep,
                                    const int32_t* num_keep, int32_t P, float* proposals,
                                    m3d_stream_t s) {
-    if (P <= 0) return M3D_OK;
+    if (P < 0) return einval("proposal_gather: negative proposal count");
+    if (P == 0) return M3D_OK;
     hipLaunchKernelGGL(proposal_gather_kernel, dim3(grid_for(P, 256)), dim3(256), 0, st(s), boxes,
                        keep, num_keep, P, proposals);
     return check_launch("proposal_gather_kernel");

@@ -665,6 +665,8 @@ extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* b
     Pyr P;
     int rc = make_pyr(P, nullptr, gmaps, fshape);
     if (rc) return rc;
+    if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
+    if (B < 0 || N < 0 || C <= 0) return einval("pyramid_roi_align3d_bwd: invalid B, N or C");
     for (int l = 0; l < 4; ++l)
         if (hipMemsetAsync(gmaps[l], 0,
                            sizeof(float) * (size_t)(B * P.H[l] * P.W[l] * P.D[l] * C),

@@ -129,7 +129,7 @@ def time_wino_gemm(S, reps=5):
 
 def time_wgrad_gemm(S, reps=5):
     """The Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2 through
-    m3d_gemm_wgrad_f32 (x3_wgrad_kernel by default)."""
+    m3d_gemm_wgrad_f32 (x3_wgrad_tr_kernel by default)."""
     from m3d import _lib
     L = _lib.load()
     nb, T, K, N = wgrad_gemm_shape(S)
@@ -146,8 +146,8 @@ def time_wgrad_gemm(S, reps=5):
     return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": X3_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4),
             "traffic": _pmc_traffic(f"wino_wgrad_gemm_rpn_shared1_S{S}"),
-            "kernel": f"x3_wgrad_kernel (fp32 GEMM as 6 bf16 MFMAs per product, operands split in the "
-                      f"LDS store): {nb} batched Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2, "
+            "kernel": f"x3_wgrad_tr_kernel (fp32 GEMM as 6 bf16 MFMAs per product, 256x256 tiles, operands "
+                      f"split in the LDS store): {nb} batched Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2, "
                       f"C[K][N] += A[M][K]^T B[M][N], M={T} K={K} N={N}",
             "peak_note": "bf16 MFMA dense peak 2516.6 TFLOP/s / 6; achieved counts fp32 FLOPs 2*M*K*N",
             "f32_mfma_peak_frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),

@@ -40,9 +40,11 @@ def build() -> str:
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "_build", "liboracle.so")
-        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(
-                os.path.join(_HERE, "oracle.c")):
+        # M3D_ORACLE_LIB: an instrumented build of the same oracle.c (the
+        # ASan/UBSan run of tests/test_sanitizers.py)
+        path = os.environ.get("M3D_ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")
+        if "M3D_ORACLE_LIB" not in os.environ and (not os.path.exists(path) or os.path.getmtime(path) <
+                                                   os.path.getmtime(os.path.join(_HERE, "oracle.c"))):
             build()
         L = ctypes.CDLL(path)
         fp = ctypes.POINTER(ctypes.c_float)

@@ -51,3 +51,36 @@ def test_ops_refuse_cpu_tensors():
                                torch.zeros(1, dtype=torch.int32), (2, 2, 2))
     with pytest.raises(ValueError, match="GPU"):
         ops.non_max_suppression_3d(torch.zeros(3, 6), torch.zeros(3), 2, 0.5)
+
+
+def test_tf_binding_matches_header():
+    """integration/tf/m3d_tf_ops.cc (the TF OpKernel binding, INTEGRATION.md
+    §2a; not buildable here: TF is absent) calls only declared, exported entry
+    points, with the declared argument count, and registers the wheel's four
+    op names on DEVICE_GPU."""
+    import m3d._lib as lib
+    src = open(os.path.join(ROOT, "integration", "tf", "m3d_tf_ops.cc")).read()
+    hdr = open(os.path.join(ROOT, "include", "m3d.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    L = lib.load()
+
+    def nargs(text, name):
+        i = text.index(name + "(") + len(name) + 1
+        depth, n, j = 1, 1, i
+        while depth:
+            c = text[j]
+            depth += c == "(" or -(c == ")")
+            n += c == "," and depth == 1
+            j += 1
+        return n if text[i:j - 1].strip() not in ("", "void") else 0
+
+    called = sorted(set(re.findall(r"\b(m3d_[a-z0-9_]+)\s*\(", src)) - {"m3d_status"})
+    assert "m3d_nms3d" in called and "m3d_crop_and_resize3d_fwd" in called
+    for name in called:
+        assert re.search(r"\b" + name + r"\s*\(", hdr), name
+        assert hasattr(L, name), name
+        assert nargs(re.sub(r"//[^\n]*", "", src), name) == nargs(hdr, name), name
+    for op in ("CropAndResize3D", "CropAndResize3DGradImage", "CropAndResize3DGradBoxes",
+               "NonMaxSuppression3D"):
+        assert f'REGISTER_OP("{op}")' in src
+        assert re.search(r'Name\("' + op + r'"\)\.Device\(DEVICE_GPU\)', src), op

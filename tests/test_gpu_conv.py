@@ -273,13 +273,16 @@ def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
     close(Cd, ref)
 
 
-def test_split3_exact_and_gemm_x3(cuda):
+@pytest.mark.parametrize("nb,M,K,N", [(3, 300, 96, 160), (2, 300, 64, 256), (3, 1000, 256, 512),
+                                     (1, 256, 128, 256), (2, 257, 512, 768), (96, 520, 256, 512)])
+def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
     """m3d_split3_f32: hi + mid + lo == x exactly (float64 sum of the bf16
-    planes); m3d_gemm_x3 (the Winograd point-GEMM kernel) against float64."""
+    planes); m3d_gemm_x3 (the Winograd point-GEMM kernels: x3_gemm_kernel,
+    and x3_gemm256_kernel for N % 256 == 0, M >= 256) against float64, ragged
+    M tiles."""
     from m3d import _lib
     L = _lib.load()
     g = torch.Generator().manual_seed(13)
-    nb, M, K, N = 3, 300, 96, 160
     A = torch.randn((nb, M, K), generator=g) * torch.exp(torch.randn((nb, M, K), generator=g) * 4)
     Bt = torch.randn((nb, N, K), generator=g)
     Ad, Bd = A.to(cuda), Bt.to(cuda)

@@ -1,0 +1,47 @@
+"""ASan + UBSan runs of the host code (sanitizers on host code
+only): the oracle's C restatement under its known-answer tests, and the host
+half of libm3d (argument validation, workspace sizing) through every entry
+point's rejection paths (tests/native/capi_asan.cpp).  CPU only; the builds
+live in tests/native/_build (tests/native/Makefile.sanitize), never on the GPU
+box.  The first build compiles libm3d once more (about 90 s on 8 cores)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+OUT = os.path.join(NATIVE, "_build")
+
+
+@pytest.fixture(scope="module")
+def sanitized_builds():
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-f", "Makefile.sanitize"], cwd=NATIVE, check=True,
+                   timeout=1200)
+    return OUT
+
+
+def _clean(text):
+    return "ERROR: AddressSanitizer" not in text and "runtime error:" not in text
+
+
+def test_capi_host_code_under_asan_ubsan(sanitized_builds):
+    r = subprocess.run([os.path.join(sanitized_builds, "capi_asan")], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and _clean(out), out[-4000:]
+    assert " 0 failures" in out
+
+
+def test_oracle_under_asan_ubsan(sanitized_builds):
+    libasan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True,
+                             check=True).stdout.strip()
+    env = dict(os.environ, LD_PRELOAD=libasan, ASAN_OPTIONS="detect_leaks=0",
+               M3D_ORACLE_LIB=os.path.join(sanitized_builds, "liboracle_asan.so"))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        "tests/test_oracle.py", "tests/test_golden.py"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and _clean(out), out[-4000:]
