@@ -275,6 +275,137 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(LineArgs a, Pyr P) {
     }
 }
 
+// ---- trilinear backward in gather form ----------------------------------------
+// The 8-corner scatter of A.2 is separable: the gradient of voxel (Y,X,Z) is
+// sum_{i,j,k} g[i][j][k] * ((wy(Y,i) * wx(X,j)) * wz(Z,k)), where wy(Y,i) is
+// 1 - yl_i if ty_i == Y and yl_i if by_i == Y (two terms when ty_i == by_i),
+// and samples outside the image along an axis contribute nothing (out of
+// bounds along any axis = no contribution, so the validity is separable too).
+// Corner slot s of an axis is corner s&1 (floor, ceil) of sample s>>1; lane s
+// of every wave holds slot s of each axis (voxel, weight, validity), so the
+// contributing slots of a voxel are one ballot.  One wave per (box, y slot,
+// x slot); a slot whose voxel an earlier slot already names exits, so every
+// touched (Y, X) column has one owner.  The wave walks the z slots the same
+// way and per touched voxel sums the per-term products g * ((wy*wx)*wz) of the
+// reference (only the summation order differs from the atomic scatter) from
+// the box's gradient rows -- L2-resident, the box's waves are XCD-contiguous --
+// and adds the sum with one atomic per channel instead of one per corner hit.
+// Boxes whose sample spacing is below a voxel share corners: a 14^3 crop of a
+// box spanning 8 voxels per axis makes 9*9*9 row atomics instead of 8*14^3.
+// Needs ch, cw, cd <= 32 (slots <= 64 lanes) and C % 64 == 0 (lanes over C).
+struct GatherArgs {
+    const float* grads;          // [nbox, ch, cw, cd, C]
+    const float* boxes;          // crop: [N,6]; pyramid: boxes_adj
+    const int32_t* box_ind;      // crop
+    const int32_t* levels;       // pyramid
+    float* gimage;               // crop: [B,H,W,D,C]
+    int64_t nbox, N;             // pyramid: N boxes per image
+    int H, W, D, ch, cw, cd;
+};
+
+struct SlotTab {
+    int vox;
+    float w;
+    bool ok;
+};
+
+// lane s: slot s of an axis with n samples over S voxels
+__device__ __forceinline__ SlotTab slot_tab(float b1, float b2, int S, int n, int s) {
+    SlotTab t{0, 0.0f, false};
+    if (s >= 2 * n) return t;
+    const float sc = axis_scale(b1, b2, S, n);
+    const float in = axis_coord(b1, b2, S, n, s >> 1, sc);
+    t.ok = !(in < 0 || in > (float)(S - 1));
+    if (!t.ok) return t;
+    const int lo = (int)floorf(in);
+    const float l = in - (float)lo;
+    t.vox = (s & 1) ? (int)ceilf(in) : lo;
+    t.w = (s & 1) ? l : 1.0f - l;
+    return t;
+}
+
+template <int CQ, bool PYR>
+__global__ __launch_bounds__(256) void gather_bwd_kernel(GatherArgs a, Pyr P) {
+    constexpr int C = 64 * CQ;
+    const int64_t wv = xcd_block() * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int sxn = 2 * a.cw;
+    const int64_t per_box = (int64_t)(2 * a.ch) * sxn;
+    if (wv >= a.nbox * per_box) return;
+    const int64_t n = wv / per_box;
+    const int rem = (int)(wv - n * per_box);
+    const int sy = rem / sxn, sx = rem - (rem / sxn) * sxn;
+    int H, W, D;
+    float* gimg;
+    if (PYR) {
+        const int l = a.levels[n] - 2;
+        H = P.H[l]; W = P.W[l]; D = P.D[l];
+        gimg = P.gmaps[l] + (size_t)(n / a.N) * H * W * D * C;
+    } else {
+        H = a.H; W = a.W; D = a.D;
+        gimg = a.gimage + (size_t)a.box_ind[n] * H * W * D * C;
+    }
+    const float* box = a.boxes + n * 6;
+    const SlotTab ty = slot_tab(box[0], box[3], H, a.ch, lane);
+    const SlotTab tx = slot_tab(box[1], box[4], W, a.cw, lane);
+    const SlotTab tz = slot_tab(box[2], box[5], D, a.cd, lane);
+    // this wave's (Y, X) column, owned by its first slot
+    if (!__builtin_amdgcn_readlane((int)ty.ok, sy) || !__builtin_amdgcn_readlane((int)tx.ok, sx)) return;
+    const int Y = __builtin_amdgcn_readlane(ty.vox, sy), X = __builtin_amdgcn_readlane(tx.vox, sx);
+    const uint64_t my = __ballot(ty.ok && ty.vox == Y), mx = __ballot(tx.ok && tx.vox == X);
+    if ((my & ((1ull << sy) - 1)) || (mx & ((1ull << sx) - 1))) return;
+    const float* g = a.grads + (size_t)n * a.ch * a.cw * a.cd * C + lane;
+    float* dst = gimg + ((size_t)Y * W + X) * D * C + lane;
+    const uint64_t zok = __ballot(tz.ok);
+    for (int sz = 0; sz < 2 * a.cd; ++sz) {
+        if (!((zok >> sz) & 1)) continue;
+        const int Z = __builtin_amdgcn_readlane(tz.vox, sz);
+        const uint64_t mz = __ballot(tz.ok && tz.vox == Z);
+        if (mz & ((1ull << sz) - 1)) continue;            // voxel Z done at an earlier slot
+        float acc[CQ];
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) acc[q] = 0.0f;
+        for (uint64_t m1 = my; m1; m1 &= m1 - 1) {
+            const int s1 = __builtin_ctzll(m1);
+            const float wy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ty.w), s1));
+            for (uint64_t m2 = mx; m2; m2 &= m2 - 1) {
+                const int s2 = __builtin_ctzll(m2);
+                const float wx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tx.w), s2));
+                const float wyx = wy * wx;
+                const float* gyx = g + ((size_t)(s1 >> 1) * a.cw + (s2 >> 1)) * a.cd * C;
+                for (uint64_t m3 = mz; m3; m3 &= m3 - 1) {
+                    const int s3 = __builtin_ctzll(m3);
+                    const float wz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tz.w), s3));
+                    const float w = wyx * wz;
+                    const float* gr = gyx + (size_t)(s3 >> 1) * C;
+#pragma unroll
+                    for (int q = 0; q < CQ; ++q) acc[q] += gr[64 * q] * w;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) unsafeAtomicAdd(dst + (size_t)Z * C + 64 * q, acc[q]);
+    }
+}
+
+// the gather-form backward for C in {64, 128, 256, 512} and crops <= 32 per
+// axis (M3D_ROI_BWD_GATHER=0: the per-sample atomic scatter everywhere)
+static bool gather_bwd_ok(int64_t C, int ch, int cw, int cd) {
+    static const int env = [] { const char* e = getenv("M3D_ROI_BWD_GATHER"); return e ? atoi(e) : 1; }();
+    return env && (C == 64 || C == 128 || C == 256 || C == 512) && ch <= 32 && cw <= 32 && cd <= 32;
+}
+
+template <bool PYR>
+static void launch_gather_bwd(const GatherArgs& a, const Pyr& P, int64_t C, hipStream_t s) {
+    const unsigned grid = grid_for(a.nbox * 4 * a.ch * a.cw, 4);
+    switch (C) {
+        case 64: hipLaunchKernelGGL((gather_bwd_kernel<1, PYR>), dim3(grid), dim3(256), 0, s, a, P); break;
+        case 128: hipLaunchKernelGGL((gather_bwd_kernel<2, PYR>), dim3(grid), dim3(256), 0, s, a, P); break;
+        case 256: hipLaunchKernelGGL((gather_bwd_kernel<4, PYR>), dim3(grid), dim3(256), 0, s, a, P); break;
+        default: hipLaunchKernelGGL((gather_bwd_kernel<8, PYR>), dim3(grid), dim3(256), 0, s, a, P);
+    }
+}
+
 // ------------------------------------------------------------------ kernels
 __global__ __launch_bounds__(256) void crop_fwd_kernel(const float* __restrict__ image, int B,
                                                        int H, int W, int D, int C,
@@ -595,6 +726,11 @@ extern "C" int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* 
                            (int)D, (int)C, method, grad_image);
         return check_launch("crop_bwd_serial_kernel");
     }
+    if (method == 0 && gather_bwd_ok(C, ch, cw, cd)) {
+        GatherArgs a{grads, boxes, box_ind, nullptr, grad_image, N, 0, (int)H, (int)W, (int)D, ch, cw, cd};
+        launch_gather_bwd<false>(a, Pyr{}, C, st(s));
+        return check_launch("gather_bwd_kernel");
+    }
     hipLaunchKernelGGL(crop_bwd_atomic_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s),
                        grads, boxes, box_ind, total, ch, cw, cd, (int)H, (int)W, (int)D, (int)C,
                        method, grad_image);
@@ -674,6 +810,11 @@ extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* b
             return check_launch("memset gmaps");
     const int64_t total = B * N * ph * pw * pd;
     if (total == 0) return M3D_OK;
+    if (gather_bwd_ok(C, ph, pw, pd)) {
+        GatherArgs a{grad_out, boxes_adj, nullptr, levels, nullptr, B * N, N, 0, 0, 0, ph, pw, pd};
+        launch_gather_bwd<true>(a, P, C, st(s));
+        return check_launch("gather_bwd_kernel<pyr>");
+    }
     hipLaunchKernelGGL(pyramid_bwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
                        (int)C, boxes_adj, levels, N, total, ph, pw, pd, grad_out);
     return check_launch("pyramid_bwd_kernel");

@@ -299,9 +299,45 @@ def time_roi_align_bwd(fmaps, S, n_rois=128, reps=5, pools=(7, 14), hi=128):
                                                      p, p, p, gptrs, fshape, C, _lib.stream()), "roi bwd")
         t = _event_time(launch, reps)
         nb = 4.0 * grad.numel() * (1 + 8) + 4.0 * img
-        res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "bytes": nb, "GBps": round(nb / t / 1e9, 1),
-                           "frac_hbm": round(nb / t / 1e9 / HBM_PEAK_GBS, 4)}
+        rows = touched_voxel_rows(badj.cpu().numpy().reshape(-1, 6), lev.cpu().numpy().reshape(-1),
+                                  [m.shape[1:4] for m in maps], p)
+        # minimal traffic of the backward: read the gradient once, zero-fill the
+        # image gradients once, read-modify-write each touched voxel row once
+        # per ROI (8 B per channel)
+        nmin = 4.0 * grad.numel() + 4.0 * img + 8.0 * C * rows
+        res[f"pool{p}"] = {"ms": round(t * 1e3, 4), "bytes": nmin, "GBps": round(nmin / t / 1e9, 1),
+                           "frac_hbm": round(nmin / t / 1e9 / HBM_PEAK_GBS, 4),
+                           "touched_voxel_rows": int(rows),
+                           "scatter_bytes": nb, "scatter_frac_hbm": round(nb / t / 1e9 / HBM_PEAK_GBS, 4),
+                           "note": "bytes = 4|grads| + 4|P2..P5| + 8*C*touched voxel rows (per ROI); "
+                                   "scatter_bytes = the per-sample 8-corner atomic form (4|grads| + 32|grads| "
+                                   "+ 4|P2..P5|)"}
     return res
+
+
+def touched_voxel_rows(boxes, levels, shapes, p):
+    """Sum over ROIs of the distinct feature-map voxels the trilinear backward
+    of a p^3 crop touches (per axis the floor/ceil corners of the in-bounds
+    samples, the float32 coordinate maths of SURVEY.md A.1; a box's voxel set
+    is the product of its three axis sets)."""
+    total = 0
+    f32 = np.float32
+    for b, lv in zip(boxes.astype(np.float32), levels):
+        H, W, D = shapes[int(lv) - 2]
+        n = 1
+        for ax, S in enumerate((H, W, D)):
+            b1, b2 = f32(b[ax]), f32(b[ax + 3])
+            i = np.arange(p, dtype=np.float32)
+            if p > 1:
+                sc = f32(f32(f32(b2 - b1) * f32(S - 1)) / f32(p - 1))
+                coord = f32(b1 * f32(S - 1)) + i * sc
+            else:
+                coord = np.full(1, f32(0.5 * float(f32(b1 + b2)) * (S - 1)), np.float32)
+            ok = (coord >= 0) & (coord <= S - 1)
+            vox = set(np.floor(coord[ok]).astype(int)) | set(np.ceil(coord[ok]).astype(int))
+            n *= len(vox)
+        total += n
+    return total
 
 
 def time_nms(dev, k=15000, max_out=6000, thr=0.7, reps=5, seed=4):
@@ -433,6 +469,10 @@ def roi_leg_large(S, dev, n_rois=512):
     with torch.no_grad():
         fmaps = model.features(image)
     r = time_roi_align(fmaps, S, n_rois=n_rois, hi=S)
+    try:
+        r["bwd"] = time_roi_align_bwd(fmaps, S, n_rois=n_rois, hi=S)
+    except Exception as e:  # report, never hide
+        r["bwd"] = {"error": repr(e)}
     r["config"] = f"{n_rois} ROIs on P2..P5 of a {S}^3 volume, C=256"
     del fmaps
     torch.cuda.empty_cache()

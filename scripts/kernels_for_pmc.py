@@ -46,7 +46,10 @@ else:
     with torch.no_grad():
         fmaps = model.features(synthetic_volume(S).to("cuda"))
     torch.cuda.synchronize()
-    if leg == "direct":
+    if leg.startswith("roibwd"):
+        print(bench.time_roi_align_bwd(fmaps, S, n_rois=NR, reps=5, pools=(int(leg[6:]),),
+                                       hi=128 if S == 128 else S))
+    elif leg == "direct":
         print(bench.time_direct_conv(model, fmaps, reps=3))
     else:
         print(bench.time_roi_align(fmaps, S, n_rois=NR, reps=3, pools=(int(leg[3:]),),

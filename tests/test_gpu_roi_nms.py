@@ -166,3 +166,31 @@ def test_detection_mask_targets_bit_exact(cuda):
     roi_masks = np.transpose(masks, (3, 0, 1, 2))[..., None][assign].astype(np.float32)
     want = np.rint(R.crop_and_resize_3d(roi_masks, rois, np.arange(P), (28, 28, 28))[..., 0])
     np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("C,crop", [(64, (7, 7, 7)), (256, (14, 14, 14)), (128, (5, 9, 3)), (64, (28, 2, 1))])
+def test_crop_grad_image_gather_form(cuda, C, crop):
+    """CropAndResize3DGradImage's fast mode (the gather-form backward for
+    C in {64..512}, crops <= 32 per axis) against the deterministic replay of
+    the reference's scatter order (bit-exact to the oracle): boxes smaller than
+    a voxel (all samples share corners), upsampled and downsampled boxes,
+    integer-aligned coordinates (floor == ceil), boxes partly outside the image
+    and flipped boxes (y2 < y1)."""
+    from m3d import ops
+    rng = np.random.default_rng(7)
+    B, H, W, D = 2, 12, 10, 20
+    lo = rng.uniform(-0.2, 0.9, (40, 3))
+    hi = lo + rng.choice([0.01, 0.1, 0.4, 0.9], size=(40, 3))
+    boxes = np.concatenate([lo, hi], 1)
+    boxes[:4] = [[0.0, 0.0, 0.0, 1.0, 1.0, 1.0], [2 / 11, 3 / 9, 5 / 19, 6 / 11, 6 / 9, 17 / 19],
+                 [0.5, 0.5, 0.5, 0.5, 0.5, 0.5], [0.9, 0.8, 0.7, 0.1, 0.2, 0.3]]
+    boxes = boxes.astype(np.float32)
+    bi = rng.integers(0, B, 40).astype(np.int32)
+    g = rng.normal(size=(40,) + crop + (C,)).astype(np.float32)
+    args = (T(g, cuda), T(boxes, cuda), T(bi, cuda), (B, H, W, D, C))
+    det = ops.crop_and_resize_3d_grad_image(*args, deterministic=True).cpu().numpy()
+    fast = ops.crop_and_resize_3d_grad_image(*args).cpu().numpy()
+    scale = np.abs(det).max()
+    assert scale > 0
+    np.testing.assert_allclose(fast, det, rtol=0, atol=2e-6 * scale)
+    assert np.array_equal(fast == 0, det == 0)        # the same voxels touched
