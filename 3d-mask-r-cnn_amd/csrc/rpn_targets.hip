@@ -125,16 +125,72 @@ __global__ void rpn_gt_best_kernel(const unsigned long long* __restrict__ gt_bes
     match[0xFFFFFFFFu - (uint32_t)(gt_best[g] & 0xFFFFFFFFull)] = 1;
 }
 
+// Top-k prefilter: a GT's IoU > 0 list holds ~10^5 anchors at 128^3, and one
+// workgroup per GT radix-selecting over all of it (contended LDS histogram
+// atomics, G workgroups on a 256-CU chip) took ~10 ms.  The global top-k
+// keys lie in the union of every 4096-entry chunk's top-k, so the chunks'
+// top-k (k rounds of a block max; keys are unique, 0 = empty slot) run in
+// parallel first, and the per-GT kernel selects over their union.
+constexpr int ATSS_CH = 4096, ATSS_KMAX = 64;
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t t = __shfl_xor(v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void atss_chunk_topk_kernel(const uint64_t* __restrict__ lists,
+                                                              const int32_t* __restrict__ list_n, int cap,
+                                                              int k, int nch, uint64_t* __restrict__ cand) {
+    __shared__ uint64_t red[4];
+    const int g = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
+    const int n = list_n[g] < cap ? list_n[g] : cap;
+    uint64_t* out = cand + ((int64_t)g * nch + c) * k;
+    const int64_t base = (int64_t)c * ATSS_CH;
+    if (base >= n) {                                        // past the list: empty slots
+        for (int r = tid; r < k; r += 256) out[r] = 0ull;
+        return;
+    }
+    uint64_t v[ATSS_CH / 256];
+#pragma unroll
+    for (int q = 0; q < ATSS_CH / 256; ++q) {
+        const int64_t j = base + tid + 256 * q;
+        v[q] = j < n ? lists[(int64_t)g * cap + j] : 0ull;
+    }
+    uint64_t last = ~0ull;
+    for (int r = 0; r < k; ++r) {
+        uint64_t best = 0;
+#pragma unroll
+        for (int q = 0; q < ATSS_CH / 256; ++q)
+            if (v[q] < last && v[q] > best) best = v[q];
+        best = wave_max_u64(best);
+        if ((tid & 63) == 0) red[tid >> 6] = best;
+        __syncthreads();
+        uint64_t m = red[0];
+        for (int w = 1; w < 4; ++w) m = red[w] > m ? red[w] : m;
+        if (tid == 0) out[r] = m;
+        last = m;
+        __syncthreads();
+    }
+}
+
 // One workgroup per GT: k-th largest key of its list (radix select, 8-bit
-// digits), stats over the top-k, ATSS marking.
+// digits, over the chunk top-k union `cand` when given), stats over the
+// top-k, ATSS marking.
 __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ lists,
                                                    const int32_t* __restrict__ list_n, int cap,
                                                    int64_t A, int topk_cfg, int min_pos, double pos_thr,
+                                                   const uint64_t* __restrict__ cand_all, int ncand,
                                                    int8_t* __restrict__ match) {
     const int g = blockIdx.x;
     const uint64_t* L = lists + (int64_t)g * cap;
     const int n = list_n[g] < cap ? list_n[g] : cap;
     if (n == 0) return;                                     // `not np.any(ious_g > 0)`: skip
+    const uint64_t* S = cand_all ? cand_all + (int64_t)g * ncand : L;   // selection set
+    const int ns = cand_all ? ncand : n;
     const int k = (int)(topk_cfg < A ? topk_cfg : A);
     __shared__ unsigned hist[256];
     __shared__ uint64_t s_prefix;
@@ -152,9 +208,9 @@ __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ 
         __syncthreads();
         const uint64_t pre = s_prefix;
         const uint64_t pmask = pass ? (~0ull << (64 - 8 * pass)) : 0ull;
-        for (int j = tid; j < n; j += blockDim.x) {
-            const uint64_t key = L[j];
-            if ((key & pmask) == pre) atomicAdd(&hist[(key >> shift) & 0xFF], 1u);
+        for (int j = tid; j < ns; j += blockDim.x) {
+            const uint64_t key = S[j];
+            if (key && (key & pmask) == pre) atomicAdd(&hist[(key >> shift) & 0xFF], 1u);
         }
         __syncthreads();
         if (tid == 0) {
@@ -211,8 +267,8 @@ __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ 
         uint64_t last = ~0ull;
         while (taken < mp && taken < n) {                   // selection by repeated max (mp small)
             uint64_t bestk = 0;
-            for (int j = 0; j < n; ++j)
-                if (L[j] < last && L[j] > bestk) bestk = L[j];
+            for (int j = 0; j < ns; ++j)                    // the mp <= k best are in the selection set
+                if (S[j] < last && S[j] > bestk) bestk = S[j];
             match[0xFFFFFFFFu - (uint32_t)(bestk & 0xFFFFFFFFull)] = 1;
             last = bestk;
             ++taken;
@@ -230,8 +286,37 @@ __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ 
 struct SelState {
     uint64_t prefix;
     long long need;
+    int active;                  // this balancing stage drops anchors
     unsigned long long hist[256];
 };
+
+// Balancing stage set-up on the device (no host round trip): stage 0 keeps
+// the target_pos positives with the largest keys when there are more;
+// stage 1 keeps min(total - positives, negatives) of the negatives.
+__global__ void sel_init_kernel(const unsigned long long* __restrict__ cnt, int stage, int target_pos,
+                                int total, SelState* st) {
+    if (threadIdx.x == 0) {
+        long long keep;
+        bool active;
+        if (stage == 0) {
+            keep = target_pos;
+            active = (long long)cnt[0] > keep;
+        } else {
+            keep = (long long)total - (long long)cnt[0];
+            if (keep > (long long)cnt[1]) keep = (long long)cnt[1];
+            active = (long long)cnt[1] > keep;
+        }
+        st->active = active ? 1 : 0;
+        if (keep <= 0) {
+            st->need = 0;
+            st->prefix = stage == 0 ? ~0ull : 0ull;   // keep none (keys < ~0; hash keys > 0)
+        } else {
+            st->need = keep;
+            st->prefix = 0;
+        }
+    }
+    for (int q = threadIdx.x; q < 256; q += blockDim.x) st->hist[q] = 0;
+}
 
 // key of anchor i for the balancing selections: positives by (iou max, ~i),
 // negatives by a seeded random 32-bit hash (then ~i)
@@ -258,7 +343,7 @@ __global__ __launch_bounds__(256) void sel_hist_kernel(const int8_t* __restrict_
     const uint64_t pre = st->prefix;
     const int shift = 56 - 8 * pass;
     const uint64_t pmask = pass ? (~0ull << (64 - 8 * pass)) : 0ull;
-    if (st->need > 0) {
+    if (st->active && st->need > 0) {
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A;
              i += (int64_t)gridDim.x * blockDim.x) {
             if (match[i] != want) continue;
@@ -277,7 +362,7 @@ __global__ void sel_pick_kernel(SelState* st, int pass, int from_below) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     long long need = st->need;
     const int shift = 56 - 8 * pass;
-    if (need > 0) {
+    if (st->active && need > 0) {
         int d;
         if (!from_below) {
             for (d = 255; d > 0; --d) {
@@ -299,10 +384,9 @@ __global__ void sel_pick_kernel(SelState* st, int pass, int from_below) {
 // drop (set 0) the flagged anchors outside the kept set
 __global__ __launch_bounds__(256) void sel_apply_kernel(int8_t* __restrict__ match, int64_t A, int want,
                                                         int mode, const float* __restrict__ iou_max,
-                                                        uint32_t seed, const SelState* st, int from_below,
-                                                        int active) {
+                                                        uint32_t seed, const SelState* st, int from_below) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A || !active || match[i] != want) return;
+    if (i >= A || !st->active || match[i] != want) return;
     const uint64_t key = sel_key(mode, iou_max, i, seed);
     const uint64_t kth = st->prefix;
     const bool keep = from_below ? key <= kth : key >= kth;
@@ -326,6 +410,17 @@ __global__ __launch_bounds__(256) void count_kernel(const int8_t* __restrict__ m
         atomicAdd(cnt, (unsigned long long)cp);
         atomicAdd(cnt + 1, (unsigned long long)cn);
     }
+}
+
+// counts_dev[0..2] = positives, negatives, 1 if a GT's IoU>0 list overflowed list_cap
+__global__ void counts_out_kernel(const unsigned long long* __restrict__ cnt, const int32_t* __restrict__ list_n,
+                                  int G, int cap, int32_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    int over = 0;
+    for (int g = 0; g < G; ++g) over |= list_n[g] > cap;
+    out[0] = (int32_t)cnt[0];
+    out[1] = (int32_t)cnt[1];
+    out[2] = over;
 }
 
 // rpn_bbox rows: positives in ascending anchor order.  Block-level counts
@@ -412,6 +507,8 @@ struct RtWs {
     SelState* st;
     unsigned long long* cnt;
     int32_t* bcount;
+    int32_t* cdev;
+    uint64_t* cand;              // [G][nch][k] chunk top-k (k <= ATSS_KMAX)
 };
 
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -429,6 +526,8 @@ static size_t rt_layout(int64_t A, int64_t G, int64_t cap, char* base, RtWs* w) 
     t.st = (SelState*)take(sizeof(SelState));
     t.cnt = (unsigned long long*)take(sizeof(unsigned long long) * 2);
     t.bcount = (int32_t*)take(sizeof(int32_t) * (nb > 0 ? nb : 1));
+    t.cdev = (int32_t*)take(sizeof(int32_t) * 3);
+    t.cand = (uint64_t*)take(sizeof(uint64_t) * (size_t)(G > 0 ? G : 1) * ((cap + ATSS_CH - 1) / ATSS_CH) * ATSS_KMAX);
     if (w) *w = t;
     return off;
 }
@@ -437,109 +536,77 @@ extern "C" size_t m3d_rpn_targets_workspace_bytes(int64_t A, int64_t G, int64_t 
     return rt_layout(A, G, list_cap, nullptr, nullptr);
 }
 
-// Host-side control flow needs the positive / negative counts between the
-// balancing stages: they are read back once (two 8-byte copies); this is a
-// data-loader op (the reference runs it in numpy in its generator).
-extern "C" int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
-                               float pos_iou, float neg_iou, int32_t total, float positive_ratio,
-                               int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
-                               uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
-                               void* workspace, size_t ws_bytes, int32_t* counts_out, m3d_stream_t s) {
+// Stream-ordered, no host round trip: the balancing stages are set up on the
+// device from the label counts (sel_init_kernel), so a training step can build
+// its targets on the GPU each iteration.  counts_dev (device int32[3], may be
+// NULL): final positives, negatives, and 1 if a GT overlapped more than
+// list_cap anchors (its ATSS candidate list was truncated; the synchronous
+// m3d_rpn_targets reports that as M3D_EINVAL).
+static int rpn_targets_impl(const float* anchors, int64_t A, const float* gt_boxes, int64_t G, float pos_iou,
+                            float neg_iou, int32_t total, float positive_ratio, int32_t atss_topk,
+                            int32_t atss_min_pos, const float rpn_bbox_std_dev[6], uint32_t seed,
+                            int8_t* rpn_match, float* rpn_bbox, int64_t list_cap, void* workspace,
+                            size_t ws_bytes, int32_t* counts_dev, hipStream_t hs) {
     if (A <= 0 || G < 0 || G > RT_MAX_G) return einval("rpn_targets: need A > 0 and 0 <= G <= 256");
     if (A > 0xFFFFFFFFll) return einval("rpn_targets: more than 2^32 anchors");
     if (total <= 0) return einval("rpn_targets: RPN_TRAIN_ANCHORS_PER_IMAGE must be positive");
+    if (list_cap <= 0 || list_cap > 0x7FFFFFFF) return einval("rpn_targets: list_cap must be in [1, 2^31)");
     if (ws_bytes < m3d_rpn_targets_workspace_bytes(A, G, list_cap)) return einval("rpn_targets: workspace too small");
-    hipStream_t hs = st(s);
     RtWs w;
     rt_layout(A, G, list_cap, (char*)workspace, &w);
     if (hipMemsetAsync(rpn_bbox, 0, sizeof(float) * 6 * (size_t)total, hs) != hipSuccess)
         return check_launch("memset rpn_bbox");
     if (G == 0) {                                            // empty GT: everything negative
         if (hipMemsetAsync(rpn_match, 0xFF, (size_t)A, hs) != hipSuccess) return check_launch("memset");
+        if (counts_dev) {
+            if (hipMemsetAsync(w.cnt, 0, sizeof(unsigned long long) * 2, hs) != hipSuccess)
+                return check_launch("memset");
+            hipLaunchKernelGGL(count_kernel, dim3(1024), dim3(256), 0, hs, rpn_match, A, w.cnt);
+            hipLaunchKernelGGL(counts_out_kernel, dim3(1), dim3(64), 0, hs, w.cnt, w.list_n, 0, (int)list_cap,
+                               counts_dev);
+            return check_launch("rpn_targets counts");
+        }
         return M3D_OK;
     }
     if (hipMemsetAsync(rpn_match, 0, (size_t)A, hs) != hipSuccess ||
         hipMemsetAsync(w.gt_best, 0, sizeof(unsigned long long) * G, hs) != hipSuccess ||
-        hipMemsetAsync(w.list_n, 0, sizeof(int32_t) * G, hs) != hipSuccess ||
-        hipMemsetAsync(w.cnt, 0, sizeof(unsigned long long) * 2, hs) != hipSuccess)
+        hipMemsetAsync(w.list_n, 0, sizeof(int32_t) * G, hs) != hipSuccess)
         return check_launch("memset");
     const unsigned gA = grid_for(A, 256);
     hipLaunchKernelGGL(rpn_iou_kernel, dim3(gA), dim3(256), 0, hs, anchors, A, gt_boxes, (int)G, w.iou_max, w.arg,
                        w.gt_best, w.lists, w.list_n, (int)list_cap);
     hipLaunchKernelGGL(rpn_gt_best_kernel, dim3(1), dim3(RT_MAX_G), 0, hs, w.gt_best, (int)G, rpn_match);
     hipLaunchKernelGGL(rpn_label_kernel, dim3(gA), dim3(256), 0, hs, w.iou_max, A, pos_iou, neg_iou, rpn_match);
+    const int kk = (int)(atss_topk < A ? atss_topk : A);
+    const int nch = (int)((list_cap + ATSS_CH - 1) / ATSS_CH);
+    const bool pre = kk >= 1 && kk <= ATSS_KMAX && nch > 1;
+    if (pre)
+        hipLaunchKernelGGL(atss_chunk_topk_kernel, dim3((unsigned)nch, (unsigned)G), dim3(256), 0, hs, w.lists,
+                           w.list_n, (int)list_cap, kk, nch, w.cand);
     hipLaunchKernelGGL(atss_kernel, dim3((unsigned)G), dim3(256), 0, hs, w.lists, w.list_n, (int)list_cap, A,
-                       (int)atss_topk, (int)atss_min_pos, (double)pos_iou, rpn_match);
+                       (int)atss_topk, (int)atss_min_pos, (double)pos_iou, pre ? w.cand : nullptr, nch * kk,
+                       rpn_match);
     int rc = check_launch("rpn_targets labels");
     if (rc) return rc;
-    int32_t ncap = 0;
-    std::vector<int32_t> ln(G);
-    if (hipMemcpyAsync(ln.data(), w.list_n, sizeof(int32_t) * G, hipMemcpyDeviceToHost, hs) != hipSuccess ||
-        hipStreamSynchronize(hs) != hipSuccess)
-        return check_launch("list counts");
-    for (int g = 0; g < G; ++g) ncap = ln[g] > ncap ? ln[g] : ncap;
-    if (ncap > list_cap) {
-        set_error("rpn_targets: a GT overlaps %d anchors, more than list_cap=%lld", ncap, (long long)list_cap);
-        return M3D_EINVAL;
-    }
-    // balancing
+    // balancing (core/data_generators.py:2150-2165)
     const int target_pos = (int)nearbyint((double)total * (double)positive_ratio);   // round() half-even
-    auto counts = [&](unsigned long long* hc) -> int {
+    auto count = [&]() {
         if (hipMemsetAsync(w.cnt, 0, sizeof(unsigned long long) * 2, hs) != hipSuccess) return check_launch("memset");
         hipLaunchKernelGGL(count_kernel, dim3(1024), dim3(256), 0, hs, rpn_match, A, w.cnt);
-        if (hipMemcpyAsync(hc, w.cnt, sizeof(unsigned long long) * 2, hipMemcpyDeviceToHost, hs) != hipSuccess ||
-            hipStreamSynchronize(hs) != hipSuccess)
-            return check_launch("counts");
-        return M3D_OK;
+        return check_launch("count_kernel");
     };
-    auto select = [&](int want, int mode, long long keep, int from_below) -> int {
-        SelState init{};
-        init.prefix = 0;
-        init.need = keep;
-        if (hipMemcpyAsync(w.st, &init, sizeof(SelState), hipMemcpyHostToDevice, hs) != hipSuccess)
-            return check_launch("sel init");
+    auto stage = [&](int st_id, int want, int mode, int from_below) {
+        hipLaunchKernelGGL(sel_init_kernel, dim3(1), dim3(256), 0, hs, w.cnt, st_id, target_pos, (int)total, w.st);
         for (int pass = 0; pass < 8; ++pass) {
             hipLaunchKernelGGL(sel_hist_kernel, dim3(1024), dim3(256), 0, hs, rpn_match, A, want, mode, w.iou_max,
                                seed, pass, w.st);
             hipLaunchKernelGGL(sel_pick_kernel, dim3(1), dim3(64), 0, hs, w.st, pass, from_below);
         }
         hipLaunchKernelGGL(sel_apply_kernel, dim3(gA), dim3(256), 0, hs, rpn_match, A, want, mode, w.iou_max, seed,
-                           w.st, from_below, 1);
-        if (hipStreamSynchronize(hs) != hipSuccess) return check_launch("select");   // init struct lifetime
-        return check_launch("select");
+                           w.st, from_below);
+        return check_launch("rpn_targets balancing");
     };
-    unsigned long long hc[2];
-    if ((rc = counts(hc))) return rc;
-    if ((long long)hc[0] > target_pos && target_pos >= 0) {
-        if (target_pos == 0) {
-            SelState z{};
-            z.prefix = ~0ull;                                // keep nothing
-            if (hipMemcpyAsync(w.st, &z, sizeof(SelState), hipMemcpyHostToDevice, hs) != hipSuccess)
-                return check_launch("sel");
-            hipLaunchKernelGGL(sel_apply_kernel, dim3(gA), dim3(256), 0, hs, rpn_match, A, 1, 0, w.iou_max, seed,
-                               w.st, 0, 1);
-            if (hipStreamSynchronize(hs) != hipSuccess) return check_launch("sel");
-        } else if ((rc = select(1, 0, target_pos, 0))) {
-            return rc;
-        }
-        if ((rc = counts(hc))) return rc;
-    }
-    const long long npos = (long long)hc[0], nneg = (long long)hc[1];
-    long long target_neg = total - npos;
-    if (target_neg > nneg) target_neg = nneg;
-    if (nneg > target_neg) {
-        if (target_neg <= 0) {
-            SelState z{};
-            z.prefix = 0;                                    // from_below keep key <= 0: none (keys > 0)
-            if (hipMemcpyAsync(w.st, &z, sizeof(SelState), hipMemcpyHostToDevice, hs) != hipSuccess)
-                return check_launch("sel");
-            hipLaunchKernelGGL(sel_apply_kernel, dim3(gA), dim3(256), 0, hs, rpn_match, A, -1, 1, w.iou_max, seed,
-                               w.st, 1, 1);
-            if (hipStreamSynchronize(hs) != hipSuccess) return check_launch("sel");
-        } else if ((rc = select(-1, 1, target_neg, 1))) {
-            return rc;
-        }
-    }
+    if ((rc = count()) || (rc = stage(0, 1, 0, 0)) || (rc = count()) || (rc = stage(1, -1, 1, 1))) return rc;
     // deltas of the positives in anchor order
     const unsigned nb = (unsigned)((A + SCAN_CHUNK - 1) / SCAN_CHUNK);
     hipLaunchKernelGGL(pos_block_count_kernel, dim3(nb), dim3(256), 0, hs, rpn_match, A, w.bcount);
@@ -548,12 +615,55 @@ extern "C" int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_
     for (int q = 0; q < 6; ++q) sd.v[q] = rpn_bbox_std_dev[q];
     hipLaunchKernelGGL(pos_deltas_kernel, dim3(nb), dim3(256), 0, hs, rpn_match, A, w.bcount, anchors, gt_boxes,
                        w.arg, sd, (int)total, rpn_bbox);
-    rc = check_launch("rpn_targets deltas");
+    if ((rc = check_launch("rpn_targets deltas"))) return rc;
+    if (counts_dev) {
+        if ((rc = count())) return rc;
+        hipLaunchKernelGGL(counts_out_kernel, dim3(1), dim3(64), 0, hs, w.cnt, w.list_n, (int)G, (int)list_cap,
+                           counts_dev);
+        return check_launch("rpn_targets counts");
+    }
+    return M3D_OK;
+}
+
+extern "C" int m3d_rpn_targets_async(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
+                                     float pos_iou, float neg_iou, int32_t total, float positive_ratio,
+                                     int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
+                                     uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
+                                     void* workspace, size_t ws_bytes, int32_t* counts_dev, m3d_stream_t s) {
+    return rpn_targets_impl(anchors, A, gt_boxes, G, pos_iou, neg_iou, total, positive_ratio, atss_topk,
+                            atss_min_pos, rpn_bbox_std_dev, seed, rpn_match, rpn_bbox, list_cap, workspace,
+                            ws_bytes, counts_dev, st(s));
+}
+
+// The data-loader form (the reference runs build_rpn_targets in numpy in its
+// generator): the async path, then the counts read back once (stream sync)
+// and a truncated candidate list reported as M3D_EINVAL.
+extern "C" int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
+                               float pos_iou, float neg_iou, int32_t total, float positive_ratio,
+                               int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
+                               uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
+                               void* workspace, size_t ws_bytes, int32_t* counts_out, m3d_stream_t s) {
+    hipStream_t hs = st(s);
+    int rc = rpn_targets_impl(anchors, A, gt_boxes, G, pos_iou, neg_iou, total, positive_ratio, atss_topk,
+                              atss_min_pos, rpn_bbox_std_dev, seed, rpn_match, rpn_bbox, list_cap, workspace,
+                              ws_bytes, nullptr, hs);
     if (rc) return rc;
+    RtWs w;
+    rt_layout(A, G, list_cap, (char*)workspace, &w);
+    if (hipMemsetAsync(w.cnt, 0, sizeof(unsigned long long) * 2, hs) != hipSuccess) return check_launch("memset");
+    hipLaunchKernelGGL(count_kernel, dim3(1024), dim3(256), 0, hs, rpn_match, A, w.cnt);
+    hipLaunchKernelGGL(counts_out_kernel, dim3(1), dim3(64), 0, hs, w.cnt, w.list_n, (int)G, (int)list_cap, w.cdev);
+    int32_t hc[3];
+    if (hipMemcpyAsync(hc, w.cdev, sizeof(hc), hipMemcpyDeviceToHost, hs) != hipSuccess ||
+        hipStreamSynchronize(hs) != hipSuccess)
+        return check_launch("rpn_targets counts");
+    if (hc[2]) {
+        set_error("rpn_targets: a GT overlaps more than list_cap=%lld anchors", (long long)list_cap);
+        return M3D_EINVAL;
+    }
     if (counts_out) {
-        if ((rc = counts(hc))) return rc;
-        counts_out[0] = (int32_t)hc[0];
-        counts_out[1] = (int32_t)hc[1];
+        counts_out[0] = hc[0];
+        counts_out[1] = hc[1];
     }
     return M3D_OK;
 }

@@ -88,6 +88,8 @@ _SIGS = {
     "m3d_rpn_targets_workspace_bytes": [c_i64, c_i64, c_i64],
     "m3d_rpn_targets": [c_p, c_i64, c_p, c_i64, c_f, c_f, c_i32, c_f, c_i32, c_i32, c_p, ctypes.c_uint32, c_p,
                         c_p, c_i64, c_p, c_sz, c_p, c_p],
+    "m3d_rpn_targets_async": [c_p, c_i64, c_p, c_i64, c_f, c_f, c_i32, c_f, c_i32, c_i32, c_p, ctypes.c_uint32,
+                              c_p, c_p, c_i64, c_p, c_sz, c_p, c_p],
     "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,

@@ -76,8 +76,47 @@ class RPNTargets:
         return t
 
 
+class DeviceRPNTargets:
+    """RPN targets resident on the device (m3d.targets.RPNTargetBuilder builds
+    them inside the step): rpn_match int8 [A] and rpn_bbox [n, 6] (positives in
+    anchor order).  The loss graphs' tf.where index sets become masks over all
+    anchors and their counts stay on the device, so nothing waits for the host;
+    the sums run in a different order than the index-set form (same terms)."""
+
+    def __init__(self, rpn_match, rpn_bbox):
+        self.match = rpn_match.reshape(-1)
+        self.bbox = rpn_bbox.reshape(-1, 6)
+
+
+def _rpn_class_loss_device(t: DeviceRPNTargets, rpn_class_logits, alpha, gamma):
+    m = t.match
+    logits = rpn_class_logits.reshape(-1, 2)
+    labels = (m == 1).long()
+    valid = (m != 0).to(logits.dtype)
+    ce = torch.nn.functional.cross_entropy(logits, labels, reduction="none")
+    p_t = torch.softmax(logits, dim=-1).gather(1, labels[:, None])[:, 0]
+    ce = torch.pow(1.0 - p_t, gamma) * ce
+    alpha_t = torch.where(labels == 1, torch.full_like(ce, alpha), torch.full_like(ce, 1.0 - alpha))
+    return (alpha_t * ce * valid).sum() / valid.sum().clamp(min=1.0)
+
+
+def _rpn_bbox_loss_device(t: DeviceRPNTargets, rpn_bbox):
+    pos = t.match == 1
+    rows = (torch.cumsum(pos.to(torch.int32), 0) - 1).clamp(0, t.bbox.shape[0] - 1)
+    pred = rpn_bbox.reshape(-1, 6).clamp(-5.0, 5.0)
+    diff = (t.bbox.index_select(0, rows.long()) - pred).clamp(-2.0, 2.0)
+    ad = diff.abs()
+    xy, zm = _xy_z_masks(diff.device)
+    h = torch.where(ad < 1.0, 0.5 * diff * diff, ad - 0.5) * xy + \
+        torch.where(ad < 0.5, 0.5 * diff * diff, 0.5 * ad - 0.25) * zm
+    posf = pos.to(h.dtype)
+    return (h * posf[:, None]).sum() / (6.0 * posf.sum().clamp(min=1.0))
+
+
 def rpn_class_loss(t: RPNTargets, rpn_class_logits, alpha=0.90, gamma=1.5):
     """core/models.py:1589-1625."""
+    if isinstance(t, DeviceRPNTargets):
+        return _rpn_class_loss_device(t, rpn_class_logits, alpha, gamma)
     if t.n_cls == 0:
         return rpn_class_logits.sum() * 0.0
     logits = rpn_class_logits.reshape(-1, 2).index_select(0, t.cls_idx)
@@ -103,6 +142,8 @@ def _xy_z_masks(dev):
 
 def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     """core/models.py:1629-1673."""
+    if isinstance(t, DeviceRPNTargets):
+        return _rpn_bbox_loss_device(t, rpn_bbox)
     if t.n_pos == 0:
         return rpn_bbox.sum() * 0.0
     pred = rpn_bbox.reshape(-1, 6).index_select(0, t.pos_idx).clamp(-5.0, 5.0)

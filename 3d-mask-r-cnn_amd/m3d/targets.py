@@ -129,3 +129,52 @@ def build_rpn_targets(anchors, gt_class_ids, gt_boxes, config, seed=0, list_cap=
                             sd, int(seed) & 0xFFFFFFFF, ptr(match8), ptr(bbox), cap, ptr(ws), wsb, cnt,
                             stream()), "rpn_targets")
     return match8.to(torch.int32), bbox
+
+
+class RPNTargetBuilder:
+    """``build_rpn_targets`` inside the training step: the same ATSS labels,
+    balancing and deltas as :func:`build_rpn_targets`
+    (core/data_generators.py:2031-2178, called per volume at :986), through
+    the stream-ordered ``m3d_rpn_targets_async`` -- no host round trip, so the
+    GPU builds each step's targets right before its forward.  Workspace and
+    outputs are allocated once for the anchor set and reused.
+
+    builder(gt_boxes, seed) with gt_boxes a normalised [G,6] DEVICE tensor
+    returns m3d.model.DeviceRPNTargets (rpn_match int8 [A], rpn_bbox
+    [RPN_TRAIN_ANCHORS_PER_IMAGE, 6]); ``counts`` (device int32[3]) holds the
+    last call's positives, negatives and list-overflow flag."""
+
+    def __init__(self, anchors, config, max_gt=64, list_cap=None):
+        ops._dev(anchors)
+        self.L = _lib.load()
+        self.anchors = anchors.contiguous()
+        self.A = int(anchors.shape[0])
+        self.max_gt = int(max_gt)
+        dev = anchors.device
+        self.total = int(getattr(config, "RPN_TRAIN_ANCHORS_PER_IMAGE", 2048))
+        self.pos_iou = float(getattr(config, "RPN_POSITIVE_IOU", 0.15))
+        self.neg_iou = float(getattr(config, "RPN_NEGATIVE_IOU", 0.05))
+        self.ratio = float(getattr(config, "RPN_POSITIVE_RATIO", 0.5))
+        self.topk = int(getattr(config, "ATSS_TOPK", 24))
+        self.min_pos = int(getattr(config, "ATSS_MIN_POS_PER_GT", 4))
+        self.sd = (_lib.c_f * 6)(*[float(np.float32(v)) for v in config.RPN_BBOX_STD_DEV])
+        self.cap = int(list_cap or min(self.A, 1 << 20))
+        self.wsb = int(self.L.m3d_rpn_targets_workspace_bytes(self.A, self.max_gt, self.cap))
+        self.ws = torch.empty(max(self.wsb, 1), device=dev, dtype=torch.uint8)
+        self.match = torch.empty((self.A,), device=dev, dtype=torch.int8)
+        self.bbox = torch.empty((self.total, 6), device=dev, dtype=torch.float32)
+        self.counts = torch.zeros((3,), device=dev, dtype=torch.int32)
+
+    def __call__(self, gt_boxes, seed=0):
+        from .model import DeviceRPNTargets
+        ops._dev(gt_boxes)
+        gt = gt_boxes.detach().float().reshape(-1, 6).contiguous()
+        G = int(gt.shape[0])
+        if G > self.max_gt:
+            raise ValueError(f"{G} GT boxes, builder sized for max_gt={self.max_gt}")
+        check(self.L.m3d_rpn_targets_async(ptr(self.anchors), self.A, ptr(gt), G, self.pos_iou, self.neg_iou,
+                                           self.total, self.ratio, self.topk, self.min_pos, self.sd,
+                                           int(seed) & 0xFFFFFFFF, ptr(self.match), ptr(self.bbox), self.cap,
+                                           ptr(self.ws), self.wsb, ptr(self.counts), stream()),
+              "rpn_targets_async")
+        return DeviceRPNTargets(self.match, self.bbox)

@@ -372,6 +372,78 @@ def time_allreduce(flat, world, reps=3):
 
 
 # ---------------------------------------------------------------- depth-slab leg
+def targets_in_step_leg(model, image, steps, warmup, dev, n_gt=8, seed=11):
+    """The configs[1] step with its RPN targets built on the GPU every
+    iteration (core/data_generators.py:986 calls build_rpn_targets per volume):
+    m3d.targets.RPNTargetBuilder (ATSS labels, balancing, deltas; stream-ordered,
+    no host round trip) from seeded GT boxes, then the same training step.
+    Reports the step time, the builder alone, and the positives it found."""
+    from m3d.targets import RPNTargetBuilder
+    S = image.shape[1]
+    rng = np.random.default_rng(seed)
+    side = rng.uniform(12, 40, (n_gt, 3)) / S
+    lo = rng.uniform(0, 1, (n_gt, 3)) * (1 - side)
+    gt = torch.from_numpy(np.concatenate([lo, lo + side], 1).astype(np.float32)).to(dev)
+    builder = RPNTargetBuilder(model.anchors.reshape(-1, 6), model.config, max_gt=n_gt)
+    for i in range(warmup):
+        model.train_step(image, builder(gt, seed=i))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        r = model.train_step(image, builder(gt, seed=1000 + i))
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    tb = _event_time(lambda: builder(gt, seed=7), 5)
+    cnt = builder.counts.cpu().tolist()
+    return {"workload": f"configs[1] step with GPU-built RPN targets ({n_gt} GT boxes, ATSS), {S}^3",
+            "ms_per_step": round(el * 1e3, 2), "volumes_per_s": round(1.0 / el, 4),
+            "builder_ms": round(tb * 1e3, 3), "positives": cnt[0], "negatives": cnt[1],
+            "loss": round(float(r["loss"]), 5)}
+
+
+def configs0_leg(dev, steps, warmup, seed=5, S=64):
+    """BASELINE configs[0]: RPN training on one synthetic 64^3 toy-shapes
+    volume (generate_data.py, restated seeded in m3d.toydata), GT boxes ->
+    RPN targets built on the GPU each step (RPNTargetBuilder) -> the training
+    step; beside it the same step through the CPU oracle port (targets from
+    the numpy restatement oracle/heads_ref.build_rpn_targets)."""
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN
+    from m3d.targets import RPNTargetBuilder
+    from m3d.toydata import network_input, toy_volume
+    from oracle import heads_ref as HR
+    v = toy_volume(S, seed=seed)
+    cfg = synthetic_rpn_config(S)
+    model = RPN(cfg, device=dev, seed=1)
+    image = torch.from_numpy(network_input(v["image"])).to(dev)
+    gt = (v["boxes"] / np.float32(S)).astype(np.float32)
+    builder = RPNTargetBuilder(model.anchors.reshape(-1, 6), cfg, max_gt=32)
+    gtd = torch.from_numpy(gt).to(dev)
+    for i in range(warmup):
+        model.train_step(image, builder(gtd, seed=i))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        r = model.train_step(image, builder(gtd, seed=100 + i))
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    res = {"workload": f"configs[0]: RPN training step on one {S}^3 toy-shapes volume ({len(gt)} objects), "
+                       f"GPU-built ATSS targets", "ms_per_step": round(el * 1e3, 2),
+           "volumes_per_s": round(1.0 / el, 3), "loss": round(float(r["loss"]), 5),
+           "positives": int(builder.counts[0])}
+    try:
+        anchors = model.anchors.reshape(-1, 6).cpu().numpy()
+        rm, rb = HR.build_rpn_targets(anchors, gt, float(cfg.RPN_POSITIVE_IOU), float(cfg.RPN_NEGATIVE_IOU),
+                                      int(cfg.RPN_TRAIN_ANCHORS_PER_IMAGE), float(getattr(cfg, "RPN_POSITIVE_RATIO", 0.5)),
+                                      int(cfg.ATSS_TOPK), int(cfg.ATSS_MIN_POS_PER_GT), cfg.RPN_BBOX_STD_DEV, 7)
+        res["cpu_baseline"] = cpu_baseline(model, S, (rm.reshape(1, -1, 1), rb[None]))
+    except Exception as e:  # report, never hide
+        res["cpu_baseline"] = {"error": repr(e)}
+    del model
+    torch.cuda.empty_cache()
+    return res
+
+
 def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     """BASELINE configs[4]: ONE S^3 volume per step, split into depth slabs over
     all ranks (halo exchange + SUM gradient all-reduce over RCCL, merged
@@ -518,29 +590,63 @@ def mrcnn_inference_leg(S, steps, warmup, dev):
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(model, S, depth_slab=0, threads=None):
-    """The oracle restatement (oracle/model_ref.py, torch-CPU fp32) timed for one
-    fwd+bwd of the same network on a depth slab of the volume (S x S x depth_slab),
-    scaled to whole volumes by the depth ratio (work is linear in depth)."""
+def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
+    """The oracle restatement timed on the host for the SAME step as the GPU
+    leg: oracle/model_ref.py forward (torch-CPU fp32) -> the RPN losses of
+    core/models.py:1589-1673 with the compiled weights (1.0 / 1.5,
+    core/models.py:3366-3369) on the same synthetic targets -> backward ->
+    the Keras SGD update of every weight (oracle/optim_ref.py: L2 term,
+    clipnorm, momentum) -> the ProposalLayer (oracle/ops_ref.py: top-k,
+    decode, the C NMS restatement 15000 -> 6000).  With depth_slab the
+    network runs on an S x S x depth_slab slab and its time is scaled to the
+    whole volume (work is linear in depth); the ProposalLayer and SGD always
+    run at full size."""
     from oracle import model_ref as MR
+    from oracle import ops_ref as R
+    from oracle import optim_ref as OR
     depth_slab = depth_slab or S
     if threads:
         torch.set_num_threads(threads)
+    cfg = model.config
     params = model.store.state_dict()
     ref = MR.RefRPN(params, dtype=torch.float32)
-    for k, v in ref.p.items():
-        if not k.endswith(("moving_mean:0", "moving_variance:0")):
-            v.requires_grad_(True)
+    trainable = [k for k in ref.p if not k.endswith(("moving_mean:0", "moving_variance:0"))]
+    for k in trainable:
+        ref.p[k].requires_grad_(True)
+    match, bbox = targets_np
     x = torch.tanh(0.5 * torch.randn((1, S, S, depth_slab, 1), generator=torch.Generator().manual_seed(0)))
     t0 = time.perf_counter()
     o = ref.forward(x)
-    loss = o["rpn_class_logits"].square().mean() + o["rpn_bbox"].square().mean()
+    if depth_slab == S:
+        m = torch.from_numpy(match.astype(np.int64))
+        loss = MR.rpn_class_loss(m, o["rpn_class_logits"]) * 1.0 + \
+            MR.rpn_bbox_loss(torch.from_numpy(bbox), m, o["rpn_bbox"]) * 1.5
+    else:   # slab: the anchors differ from the targets' -- same reduction work, synthetic objective
+        loss = o["rpn_class_logits"].square().mean() + o["rpn_bbox"].square().mean()
     loss.backward()
-    t = time.perf_counter() - t0
-    vol_per_s = (depth_slab / S) / t
-    return {"value": vol_per_s, "unit": "volumes/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/model_ref.py torch-CPU fp32 fwd+bwd on a {S}x{S}x{depth_slab} depth slab "
-                      f"({t:.1f} s)" + (f", scaled x{S // depth_slab} to one {S}^3 volume" if depth_slab != S else "")}
+    t_net = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    opt = model.optimizer
+    lr, mom, clip = float(opt.current_lr()), float(opt.params.get("momentum", 0.0)), opt.clipnorm
+    state = {}
+    for k in trainable:
+        p = model.store.by_name.get(k)
+        l2 = cfg.WEIGHT_DECAY / ref.p[k].numel() if (p is not None and p.l2) else 0.0
+        OR.step("SGD", ref.p[k].detach().numpy(), ref.p[k].grad.numpy(), state.setdefault(k, {}), 0, lr,
+                clipnorm=clip, l2coef=l2, momentum=mom)
+    probs = o["rpn_class"].detach().numpy()
+    deltas = o["rpn_bbox"].detach().numpy()
+    if depth_slab == S:
+        anchors = model.anchors.cpu().numpy()
+        R.proposal_layer(probs, deltas, anchors, cfg.POST_NMS_ROIS_TRAINING, cfg.RPN_NMS_THRESHOLD,
+                         cfg.PRE_NMS_LIMIT, np.asarray(cfg.RPN_BBOX_STD_DEV, np.float32), float(cfg.IMAGE_DEPTH))
+    t_rest = time.perf_counter() - t1
+    t = t_net * (S / depth_slab) + t_rest
+    return {"value": 1.0 / t, "unit": "volumes/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"one RPN training step (the GPU step's work) on the host: oracle/model_ref.py torch-CPU fp32 fwd + RPN "
+                      f"losses + bwd on a {S}x{S}x{depth_slab} volume ({t_net:.1f} s"
+                      + (f", scaled x{S // depth_slab}" if depth_slab != S else "")
+                      + f"), oracle SGD update of all weights + ProposalLayer (C NMS) {t_rest:.1f} s"}
 
 
 # ---------------------------------------------------------------- main
@@ -635,6 +741,15 @@ def main():
                                                proposals=props)
         except Exception as e:  # report, never hide
             out["depth_slab"] = {"error": repr(e)}
+    if world == 1 and not args.no_extras:
+        try:
+            out["configs0"] = configs0_leg(dev, max(3, args.steps // 2), 2)
+        except Exception as e:  # report, never hide
+            out["configs0"] = {"error": repr(e)}
+        try:
+            out["targets_in_step"] = targets_in_step_leg(model, image, max(3, args.steps // 2), 2, dev)
+        except Exception as e:  # report, never hide
+            out["targets_in_step"] = {"error": repr(e)}
     if rank == 0 and not args.no_extras:
         with torch.no_grad():
             fmaps = model.features(image)
@@ -679,7 +794,7 @@ def main():
                 out["mrcnn_inference"] = {"error": repr(e)}
         if world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(model, S, args.cpu_slab)
+                out["cpu_baseline"] = cpu_baseline(model, S, (match, bbox), args.cpu_slab)
             except Exception as e:
                 out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -332,8 +332,13 @@ int m3d_detection_targets(const float* proposals, int64_t N, const int32_t* gt_c
  * the anchors with IoU > 0, capacity list_cap each); ties where the reference
  * is implementation-defined go to the larger IoU, then the smaller anchor
  * index; np.random.choice of the dropped negatives -> a seeded random subset.
- * Synchronises the stream (the balancing needs the label counts on the host),
- * counts_out[2] = final (positives, negatives) if non-NULL.
+ * m3d_rpn_targets synchronises the stream once at the end (host counts_out[2]
+ * = final (positives, negatives) if non-NULL; M3D_EINVAL if a GT overlapped
+ * more than list_cap anchors).  m3d_rpn_targets_async is the same computation
+ * fully stream-ordered (balancing set up on the device, no host round trip,
+ * hipGraph-capturable) for building the targets inside a training step:
+ * counts_dev (DEVICE int32[3], may be NULL) = positives, negatives, list
+ * overflow flag.
  * workspace: m3d_rpn_targets_workspace_bytes(A, G, list_cap). */
 size_t m3d_rpn_targets_workspace_bytes(int64_t A, int64_t G, int64_t list_cap);
 int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
@@ -341,6 +346,11 @@ int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_boxes, int6
                     int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
                     uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
                     void* workspace, size_t ws_bytes, int32_t* counts_out, m3d_stream_t s);
+int m3d_rpn_targets_async(const float* anchors, int64_t A, const float* gt_boxes, int64_t G,
+                          float pos_iou, float neg_iou, int32_t total, float positive_ratio,
+                          int32_t atss_topk, int32_t atss_min_pos, const float rpn_bbox_std_dev[6],
+                          uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
+                          void* workspace, size_t ws_bytes, int32_t* counts_dev, m3d_stream_t s);
 
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.

@@ -88,3 +88,43 @@ def test_build_rpn_targets(cuda, S, D, G, topk, minpos):
     assert np.array_equal(m, rm), (np.sum(m != rm), np.sum(m == 1), np.sum(rm == 1))
     assert (m == 1).sum() > 0 and (m == -1).sum() > 0
     np.testing.assert_allclose(b.cpu().numpy(), rb, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("S,D,G,total", [(64, 16, 6, 512), (64, 32, 12, 256), (64, 16, 1, 64), (64, 16, 0, 128)])
+def test_rpn_targets_async_in_step_form(cuda, S, D, G, total):
+    """m3d_rpn_targets_async (device-side balancing, no host round trip; the
+    in-step builder RPNTargetBuilder) produces exactly the synchronous
+    builder's rpn_match / rpn_bbox / counts -- including the stage where the
+    positives exceed RPN_TRAIN_ANCHORS_PER_IMAGE * ratio and the empty-GT case
+    -- and DeviceRPNTargets' mask-form losses equal the index-set losses of
+    the host-prepared RPNTargets."""
+    from m3d.anchors import get_anchors
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPNTargets, rpn_bbox_loss, rpn_class_loss
+    from m3d.targets import RPNTargetBuilder, build_rpn_targets
+    cfg = synthetic_rpn_config(S, depth=D, RPN_POSITIVE_IOU=0.3, RPN_NEGATIVE_IOU=0.1,
+                               RPN_TRAIN_ANCHORS_PER_IMAGE=total, ATSS_TOPK=24, ATSS_MIN_POS_PER_GT=4)
+    anchors = torch.from_numpy(get_anchors(cfg)).to(cuda)
+    rng = np.random.default_rng(S + G + total)
+    lo = rng.uniform(0, [S - 24, S - 24, D - 6], (G, 3))
+    gt_px = np.concatenate([lo, lo + rng.uniform([8, 8, 2], [24, 24, 6], (G, 3))], 1).astype(np.float32)
+    gt_n = np.clip(gt_px / np.array([S, S, D, S, S, D], np.float32), 0, 1).astype(np.float32).reshape(-1, 6)
+    m_sync, b_sync = build_rpn_targets(anchors, np.ones(G, np.int32), gt_n, cfg, seed=5)
+    builder = RPNTargetBuilder(anchors, cfg, max_gt=16)
+    t = builder(torch.from_numpy(gt_n).to(cuda), seed=5)
+    m_async = t.match.to(torch.int32)
+    assert torch.equal(m_async, m_sync)
+    assert torch.equal(t.bbox, b_sync)
+    cnt = builder.counts.cpu().numpy()
+    ms = m_sync.cpu().numpy()
+    assert cnt[0] == (ms == 1).sum() and cnt[1] == (ms == -1).sum() and cnt[2] == 0
+    assert cnt[0] + cnt[1] <= total or G == 0      # empty GT: every anchor negative, no balancing
+    # losses: mask form (device) vs index-set form (host-prepared)
+    A = anchors.shape[0]
+    g = torch.Generator(device=cuda).manual_seed(3)
+    logits = torch.randn((1, A, 2), device=cuda, generator=g)
+    deltas = torch.randn((1, A, 6), device=cuda, generator=g)
+    host = RPNTargets(ms.reshape(1, -1, 1), b_sync.cpu().numpy()[None], cuda)
+    for fn, x in ((rpn_class_loss, logits), (rpn_bbox_loss, deltas)):
+        a, b = float(fn(t, x)), float(fn(host, x))
+        assert abs(a - b) <= 1e-6 * max(1.0, abs(b)), (fn.__name__, a, b)
