@@ -482,13 +482,58 @@ __global__ __launch_bounds__(256) void crop_bwd_serial_kernel(
     }
 }
 
-// grad wrt boxes (TF CropAndResizeBackpropBoxes generalised to 3-D), one
-// workgroup per box, block reduction of the 6 partial sums.
-__global__ __launch_bounds__(256) void crop_bwd_boxes_kernel(
+// CropAndResize3DGradBoxes with the wheel's compiled formulas (DESIGN.md A.4,
+// whl _crop_and_resize_3d_grad_boxes_ops.so Compute @0x3980): ratios
+// (S-1)/(n-1), the depth scale (z2 - y1)(H-1)/(ch-1) as compiled, image
+// gradients in the compiled association, out[a] += ((S-1) - r i) g_a and
+// out[a+3] += (g_a i) r, or the double-precision update for n == 1.  One wave
+// per box: the sample loop is wave-uniform, lanes compute the terms of 64
+// channels, and the six outputs take them one channel after the other in the
+// reference order (box -> y -> x -> z -> c), so the result is bit-identical
+// to the sequential CPU op (oracle_crop_and_resize3d_grad_boxes).
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ double laned(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// per-channel terms of one axis: float pair (n > 1) or the double term (n == 1)
+struct GbTerm {
+    float lo, hi;
+    double d;
+};
+__device__ __forceinline__ GbTerm gb_term(int n, int i, float g, float r, int S) {
+    GbTerm t;
+    if (n > 1) {
+        t.lo = ((float)(S - 1) - r * (float)i) * g;
+        t.hi = (g * (float)i) * r;
+        t.d = 0.0;
+    } else {
+        t.lo = t.hi = 0.0f;
+        t.d = (double)g * 0.5 * (double)(S - 1);
+    }
+    return t;
+}
+__device__ __forceinline__ void gb_acc(int n, const GbTerm& t, int l, float& a, float& b) {
+    if (n > 1) {
+        a += lanef(t.lo, l);
+        b += lanef(t.hi, l);
+    } else {
+        const double d = laned(t.d, l);
+        a = (float)((double)a + d);
+        b = (float)(d + (double)b);
+    }
+}
+
+__global__ __launch_bounds__(64) void crop_bwd_boxes_kernel(
     const float* __restrict__ grads, const float* __restrict__ image, int B, int H, int W, int D,
     int C, const float* __restrict__ boxes, const int32_t* __restrict__ box_ind, int ch, int cw,
     int cd, float* __restrict__ gboxes) {
-    const int n = blockIdx.x;
+    const int n = blockIdx.x, lane = threadIdx.x;
     const float* bx = boxes + (size_t)n * 6;
     const float y1 = bx[0], x1 = bx[1], z1 = bx[2], y2 = bx[3], x2 = bx[4], z2 = bx[5];
     const float* img = image + (size_t)box_ind[n] * H * W * D * C;
@@ -497,61 +542,59 @@ __global__ __launch_bounds__(256) void crop_bwd_boxes_kernel(
     const float dr = cd > 1 ? (float)(D - 1) / (float)(cd - 1) : 0.0f;
     const float hs = ch > 1 ? (y2 - y1) * hr : 0.0f;
     const float ws = cw > 1 ? (x2 - x1) * wr : 0.0f;
-    const float ds = cd > 1 ? (z2 - z1) * dr : 0.0f;
-    float acc[6] = {0, 0, 0, 0, 0, 0};
+    const float ds = cd > 1 ? (z2 - y1) * hr : 0.0f;       // sic: the compiled depth scale (A.4)
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f, a4 = 0.0f, a5 = 0.0f;
     const size_t rowD = (size_t)D * C, rowW = (size_t)W * rowD;
-    const int64_t total = (int64_t)ch * cw * cd * C;
-    for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
-        const int c = (int)(e % C);
-        int64_t t = e / C;
-        const int z = (int)(t % cd); t /= cd;
-        const int x = (int)(t % cw);
-        const int y = (int)(t / cw);
+    for (int y = 0; y < ch; ++y) {
         const float in_y = axis_coord(y1, y2, H, ch, y, hs);
-        const float in_x = axis_coord(x1, x2, W, cw, x, ws);
-        const float in_z = axis_coord(z1, z2, D, cd, z, ds);
-        if (in_y < 0 || in_y > (float)(H - 1) || in_x < 0 || in_x > (float)(W - 1) ||
-            in_z < 0 || in_z > (float)(D - 1))
-            continue;
+        if (in_y < 0 || in_y > (float)(H - 1)) continue;
         const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
-        const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
-        const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
-        const float yl = in_y - (float)ty, xl = in_x - (float)lx, zl = in_z - (float)fz;
-        const float tlf = img[ty * rowW + lx * rowD + (size_t)fz * C + c];
-        const float tlk = img[ty * rowW + lx * rowD + (size_t)kz * C + c];
-        const float trf = img[ty * rowW + rx * rowD + (size_t)fz * C + c];
-        const float trk = img[ty * rowW + rx * rowD + (size_t)kz * C + c];
-        const float blf = img[by * rowW + lx * rowD + (size_t)fz * C + c];
-        const float blk = img[by * rowW + lx * rowD + (size_t)kz * C + c];
-        const float brf = img[by * rowW + rx * rowD + (size_t)fz * C + c];
-        const float brk = img[by * rowW + rx * rowD + (size_t)kz * C + c];
-        const float tl = tlf + (tlk - tlf) * zl, tr = trf + (trk - trf) * zl;
-        const float bl = blf + (blk - blf) * zl, br = brf + (brk - brf) * zl;
-        float gy = (1 - xl) * (bl - tl) + xl * (br - tr);
-        float gx = (1 - yl) * (tr - tl) + yl * (br - bl);
-        const float dtl = tlk - tlf, dtr = trk - trf, dbl = blk - blf, dbr = brk - brf;
-        const float dtop = dtl + (dtr - dtl) * xl, dbot = dbl + (dbr - dbl) * xl;
-        float gz = dtop + (dbot - dtop) * yl;
-        const float tg = grads[((((size_t)n * ch + y) * cw + x) * cd + z) * C + c];
-        gy *= tg; gx *= tg; gz *= tg;
-        if (ch > 1) { acc[0] += gy * ((float)(H - 1) - (float)y * hr); acc[3] += gy * ((float)y * hr); }
-        else { acc[0] += gy * 0.5f * (float)(H - 1); acc[3] += gy * 0.5f * (float)(H - 1); }
-        if (cw > 1) { acc[1] += gx * ((float)(W - 1) - (float)x * wr); acc[4] += gx * ((float)x * wr); }
-        else { acc[1] += gx * 0.5f * (float)(W - 1); acc[4] += gx * 0.5f * (float)(W - 1); }
-        if (cd > 1) { acc[2] += gz * ((float)(D - 1) - (float)z * dr); acc[5] += gz * ((float)z * dr); }
-        else { acc[2] += gz * 0.5f * (float)(D - 1); acc[5] += gz * 0.5f * (float)(D - 1); }
+        const float yl = in_y - (float)ty, yl1 = 1.0f - yl;
+        for (int x = 0; x < cw; ++x) {
+            const float in_x = axis_coord(x1, x2, W, cw, x, ws);
+            if (in_x < 0 || in_x > (float)(W - 1)) continue;
+            const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+            const float xl = in_x - (float)lx, xl1 = 1.0f - xl;
+            for (int z = 0; z < cd; ++z) {
+                const float in_z = axis_coord(z1, z2, D, cd, z, ds);
+                if (in_z < 0 || in_z > (float)(D - 1)) continue;
+                const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+                const float zl = in_z - (float)fz, zl1 = 1.0f - zl;
+                const float* gr = grads + ((((size_t)n * ch + y) * cw + x) * cd + z) * C;
+                for (int c0 = 0; c0 < C; c0 += 64) {
+                    const int c = c0 + lane;
+                    float igy = 0.0f, igx = 0.0f, igz = 0.0f, tg = 0.0f;
+                    if (c < C) {
+                        const float tlf = img[ty * rowW + lx * rowD + (size_t)fz * C + c];
+                        const float tlk = img[ty * rowW + lx * rowD + (size_t)kz * C + c];
+                        const float trf = img[ty * rowW + rx * rowD + (size_t)fz * C + c];
+                        const float trk = img[ty * rowW + rx * rowD + (size_t)kz * C + c];
+                        const float blf = img[by * rowW + lx * rowD + (size_t)fz * C + c];
+                        const float blk = img[by * rowW + lx * rowD + (size_t)kz * C + c];
+                        const float brf = img[by * rowW + rx * rowD + (size_t)fz * C + c];
+                        const float brk = img[by * rowW + rx * rowD + (size_t)kz * C + c];
+                        igy = ((blf - tlf) * xl1 + (brf - trf) * xl) * zl1 + ((blk - tlk) * xl1 + (brk - trk) * xl) * zl;
+                        igx = ((trf - tlf) * yl1 + (brf - blf) * yl) * zl1 + ((trk - tlk) * yl1 + (brk - blk) * yl) * zl;
+                        igz = ((tlk - tlf) * yl1 + (blk - blf) * yl) * xl1 + ((trk - trf) * yl1 + (brk - brf) * yl) * xl;
+                        tg = gr[c];
+                    }
+                    const GbTerm ty_ = gb_term(ch, y, igy * tg, hr, H);
+                    const GbTerm tx_ = gb_term(cw, x, igx * tg, wr, W);
+                    const GbTerm tz_ = gb_term(cd, z, igz * tg, dr, D);
+                    const int cnt = C - c0 < 64 ? C - c0 : 64;
+                    for (int l = 0; l < cnt; ++l) {       // channel order, one term at a time
+                        gb_acc(ch, ty_, l, a0, a3);
+                        gb_acc(cw, tx_, l, a1, a4);
+                        gb_acc(cd, tz_, l, a2, a5);
+                    }
+                }
+            }
+        }
     }
-    __shared__ float red[6][256];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = acc[q];
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + off];
-        __syncthreads();
+    if (lane == 0) {
+        float* o = gboxes + (size_t)n * 6;
+        o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3; o[4] = a4; o[5] = a5;
     }
-    if (threadIdx.x < 6) gboxes[(size_t)n * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
 // ---- PyramidROIAlign ----------------------------------------------------------
@@ -745,7 +788,7 @@ extern "C" int m3d_crop_and_resize3d_bwd_boxes(const float* grads, const float* 
     int rc = check_crop_args(B, H, W, D, C, ch, cw, cd, 0);
     if (rc) return rc;
     if (N == 0) return M3D_OK;
-    hipLaunchKernelGGL(crop_bwd_boxes_kernel, dim3((unsigned)N), dim3(256), 0, st(s), grads,
+    hipLaunchKernelGGL(crop_bwd_boxes_kernel, dim3((unsigned)N), dim3(64), 0, st(s), grads,
                        image, (int)B, (int)H, (int)W, (int)D, (int)C, boxes, box_ind, ch, cw, cd,
                        grad_boxes);
     return check_launch("crop_bwd_boxes_kernel");

@@ -173,10 +173,37 @@ int oracle_crop_and_resize3d_grad_image(const float* grads, const float* boxes,
 }
 
 /* ------------------------------------------------------------------------ */
-/* CropAndResize3DGradBoxes (whl Compute @0x3980): TF-2.2                    */
-/* CropAndResizeBackpropBoxes generalised to 3-D trilinear sampling.         */
-/* out[n] = (dy1, dx1, dz1, dy2, dx2, dz2).                                   */
-/* ------------------------------------------------------------------------ */
+/* CropAndResize3DGradBoxes, out[n] = (dy1, dx1, dz1, dy2, dx2, dz2),         */
+/* restated from the wheel's compiled code (SURVEY.md
+ * style appendix A.4 in DESIGN.md; whl _crop_and_resize_3d_grad_boxes_ops.so,
+ * CropAndResize3DGradBoxesOp::Compute @0x3980):
+ *  - ratios r = (S-1)/(n-1) per axis (0 when n == 1), @0x3f4a-0x3fdb;
+ *  - scales hs = (y2-y1)*rh, ws = (x2-x1)*rw and, as compiled, the DEPTH
+ *    scale ds = (z2 - y1)*rh (y1 and the height ratio, @0x4059-0x4071);
+ *  - loops box -> y -> x -> z -> c, a sample out of bounds on an axis is
+ *    skipped (@0x40f4, 0x4250, 0x43c2); in = b1*(S-1) + i*scale, or
+ *    (float)((double)(b1+b2)*0.5*(double)(S-1)) when n == 1 (@0x4a50...);
+ *  - image gradients per channel in the compiled association (@0x46a4-0x47c6):
+ *      igy = ((blf-tlf)(1-xl) + (brf-trf)xl)(1-zl) + ((blk-tlk)(1-xl) + (brk-trk)xl)zl
+ *      igx = ((trf-tlf)(1-yl) + (brf-blf)yl)(1-zl) + ((trk-tlk)(1-yl) + (brk-blk)yl)zl
+ *      igz = ((tlk-tlf)(1-yl) + (blk-blf)yl)(1-xl) + ((trk-trf)(1-yl) + (brk-brf)yl)xl
+ *    times the incoming gradient;
+ *  - accumulation into the zero-filled float output, sequentially
+ *    (@0x4590-0x469e): out[a] += ((S-1) - r*i) * g_a and out[a+3] += (g_a*i)*r
+ *    for n > 1; for n == 1 both get (float)((double)out + (double)g_a*0.5*(double)(S-1))
+ *    (@0x47d0-0x48e3).
+ * Not reachable from the reference graph. */
+static void gb_add(float* o, int n, int i, float g, float r, int S) {
+    if (n > 1) {
+        o[0] += ((float)(S - 1) - r * (float)i) * g;
+        o[3] += (g * (float)i) * r;
+    } else {
+        const double d = (double)g * 0.5 * (double)(S - 1);
+        o[0] = (float)((double)o[0] + d);
+        o[3] = (float)(d + (double)o[3]);
+    }
+}
+
 int oracle_crop_and_resize3d_grad_boxes(const float* grads, const float* image,
                                         int B, int H, int W, int D, int C,
                                         const float* boxes, const int32_t* box_ind, int N,
@@ -193,67 +220,50 @@ int oracle_crop_and_resize3d_grad_boxes(const float* grads, const float* image,
         const float dr = cd > 1 ? (float)(D - 1) / (float)(cd - 1) : 0.0f;
         const float hs = ch > 1 ? (y2 - y1) * hr : 0.0f;
         const float ws = cw > 1 ? (x2 - x1) * wr : 0.0f;
-        const float ds = cd > 1 ? (z2 - z1) * dr : 0.0f;
+        const float ds = cd > 1 ? (z2 - y1) * hr : 0.0f;      /* sic: the compiled depth scale */
         float* gb = out + (size_t)n * 6;
         for (int y = 0; y < ch; ++y) {
             const float in_y = axis_coord(y1, y2, H, ch, y, hs);
             if (in_y < 0 || in_y > (float)(H - 1)) continue;
             const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
-            const float yl = in_y - (float)ty;
+            const float yl = in_y - (float)ty, yl1 = 1.0f - yl;
             for (int x = 0; x < cw; ++x) {
                 const float in_x = axis_coord(x1, x2, W, cw, x, ws);
                 if (in_x < 0 || in_x > (float)(W - 1)) continue;
                 const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
-                const float xl = in_x - (float)lx;
+                const float xl = in_x - (float)lx, xl1 = 1.0f - xl;
                 for (int z = 0; z < cd; ++z) {
                     const float in_z = axis_coord(z1, z2, D, cd, z, ds);
                     if (in_z < 0 || in_z > (float)(D - 1)) continue;
                     const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
-                    const float zl = in_z - (float)fz;
+                    const float zl = in_z - (float)fz, zl1 = 1.0f - zl;
                     const float* g = grads + ((((size_t)n * ch + y) * cw + x) * cd + z) * C;
 #define V(yy, xx, zz) (img + (((size_t)(yy) * W + (xx)) * D + (zz)) * C)
-                    const float *tlf = V(ty, lx, fz), *tlk = V(ty, lx, kz);
-                    const float *trf = V(ty, rx, fz), *trk = V(ty, rx, kz);
-                    const float *blf = V(by, lx, fz), *blk = V(by, lx, kz);
-                    const float *brf = V(by, rx, fz), *brk = V(by, rx, kz);
+                    const float *ptlf = V(ty, lx, fz), *ptlk = V(ty, lx, kz);
+                    const float *ptrf = V(ty, rx, fz), *ptrk = V(ty, rx, kz);
+                    const float *pblf = V(by, lx, fz), *pblk = V(by, lx, kz);
+                    const float *pbrf = V(by, rx, fz), *pbrk = V(by, rx, kz);
 #undef V
                     for (int c = 0; c < C; ++c) {
-                        /* z-interpolated corner values */
-                        const float tl = tlf[c] + (tlk[c] - tlf[c]) * zl;
-                        const float tr = trf[c] + (trk[c] - trf[c]) * zl;
-                        const float bl = blf[c] + (blk[c] - blf[c]) * zl;
-                        const float br = brf[c] + (brk[c] - brf[c]) * zl;
-                        float gy = (1 - xl) * (bl - tl) + xl * (br - tr);
-                        float gx = (1 - yl) * (tr - tl) + yl * (br - bl);
-                        /* d/dz: bilinear (y,x) blend of the z-differences */
-                        const float dtl = tlk[c] - tlf[c], dtr = trk[c] - trf[c];
-                        const float dbl = blk[c] - blf[c], dbr = brk[c] - brf[c];
-                        const float dtop = dtl + (dtr - dtl) * xl;
-                        const float dbot = dbl + (dbr - dbl) * xl;
-                        float gz = dtop + (dbot - dtop) * yl;
+                        const float tlf = ptlf[c], tlk = ptlk[c], trf = ptrf[c], trk = ptrk[c];
+                        const float blf = pblf[c], blk = pblk[c], brf = pbrf[c], brk = pbrk[c];
+                        const float igy = ((blf - tlf) * xl1 + (brf - trf) * xl) * zl1 +
+                                          ((blk - tlk) * xl1 + (brk - trk) * xl) * zl;
+                        const float igx = ((trf - tlf) * yl1 + (brf - blf) * yl) * zl1 +
+                                          ((trk - tlk) * yl1 + (brk - blk) * yl) * zl;
+                        const float igz = ((tlk - tlf) * yl1 + (blk - blf) * yl) * xl1 +
+                                          ((trk - trf) * yl1 + (brk - brf) * yl) * xl;
                         const float tg = g[c];
-                        gy *= tg; gx *= tg; gz *= tg;
-                        if (ch > 1) {
-                            gb[0] += gy * ((float)(H - 1) - (float)y * hr);
-                            gb[3] += gy * ((float)y * hr);
-                        } else {
-                            gb[0] += gy * 0.5f * (float)(H - 1);
-                            gb[3] += gy * 0.5f * (float)(H - 1);
-                        }
-                        if (cw > 1) {
-                            gb[1] += gx * ((float)(W - 1) - (float)x * wr);
-                            gb[4] += gx * ((float)x * wr);
-                        } else {
-                            gb[1] += gx * 0.5f * (float)(W - 1);
-                            gb[4] += gx * 0.5f * (float)(W - 1);
-                        }
-                        if (cd > 1) {
-                            gb[2] += gz * ((float)(D - 1) - (float)z * dr);
-                            gb[5] += gz * ((float)z * dr);
-                        } else {
-                            gb[2] += gz * 0.5f * (float)(D - 1);
-                            gb[5] += gz * 0.5f * (float)(D - 1);
-                        }
+                        float o[4];
+                        o[0] = gb[0]; o[3] = gb[3];
+                        gb_add(o, ch, y, igy * tg, hr, H);
+                        gb[0] = o[0]; gb[3] = o[3];
+                        o[0] = gb[1]; o[3] = gb[4];
+                        gb_add(o, cw, x, igx * tg, wr, W);
+                        gb[1] = o[0]; gb[4] = o[3];
+                        o[0] = gb[2]; o[3] = gb[5];
+                        gb_add(o, cd, z, igz * tg, dr, D);
+                        gb[2] = o[0]; gb[5] = o[3];
                     }
                 }
             }

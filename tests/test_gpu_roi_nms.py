@@ -55,7 +55,9 @@ def test_crop_grad_boxes_and_autograd(cuda):
     out = ops.crop_and_resize_3d(img, boxes, T(f["box_ind"], cuda), (5, 4, 3), "trilinear", -1.5)
     out.backward(T(f["grads"], cuda))
     np.testing.assert_allclose(img.grad.cpu().numpy(), f["grad_image_trilinear"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(boxes.grad.cpu().numpy(), f["grad_boxes"], rtol=1e-4, atol=1e-3)
+    # CropAndResize3DGradBoxes follows the wheel's compiled formulas and its
+    # sequential summation order: bit-identical to the oracle
+    np.testing.assert_array_equal(boxes.grad.cpu().numpy(), f["grad_boxes"])
 
 
 def test_crop_validation_messages(cuda):
@@ -194,3 +196,21 @@ def test_crop_grad_image_gather_form(cuda, C, crop):
     assert scale > 0
     np.testing.assert_allclose(fast, det, rtol=0, atol=2e-6 * scale)
     assert np.array_equal(fast == 0, det == 0)        # the same voxels touched
+
+
+@pytest.mark.parametrize("C,crop", [(256, (14, 14, 14)), (70, (7, 1, 5)), (8, (1, 1, 1))])
+def test_crop_grad_boxes_bit_exact(cuda, C, crop):
+    """CropAndResize3DGradBoxes (A.4: the wheel's depth scale, association and
+    sequential channel order) bit-identical to the oracle, incl. single-sample
+    axes (double-precision update) and C not a multiple of 64."""
+    from m3d import ops
+    from oracle import ops_ref as R
+    rng = np.random.default_rng(17)
+    img = rng.normal(size=(2, 9, 11, 13, C)).astype(np.float32)
+    lo = rng.uniform(-0.1, 0.7, (6, 3))
+    boxes = np.concatenate([lo, lo + rng.uniform(0.05, 0.5, (6, 3))], 1).astype(np.float32)
+    bi = np.array([0, 1, 1, 0, 1, 0], np.int32)
+    g = rng.normal(size=(6,) + crop + (C,)).astype(np.float32)
+    got = ops.crop_and_resize_3d_grad_boxes(T(g, cuda), T(img, cuda), T(boxes, cuda), T(bi, cuda)).cpu().numpy()
+    want = R.crop_and_resize_3d_grad_boxes(g, img, boxes, bi)
+    np.testing.assert_array_equal(got, want)

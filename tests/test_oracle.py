@@ -109,22 +109,74 @@ def test_grad_image_is_adjoint_of_forward():
         assert abs(lhs - rhs) <= 1e-4 * (abs(lhs) + 1.0)
 
 
-def test_grad_boxes_matches_finite_differences():
+def _fd_box_grad(img, boxes, g, crop, j, eps=1e-3):
+    bp, bm = boxes.copy(), boxes.copy()
+    bp[0, j] += eps
+    bm[0, j] -= eps
+    fp = np.sum(R.crop_and_resize_3d(img, bp, [0], crop).astype(np.float64) * g)
+    fm = np.sum(R.crop_and_resize_3d(img, bm, [0], crop).astype(np.float64) * g)
+    return (fp - fm) / (2 * eps)
+
+
+def _grad_boxes_f64(g, img, box, crop):
+    """Independent float64 numpy evaluation of A.4 (the wheel's sampling, incl.
+    its depth scale (z2 - y1)(H-1)/(ch-1), and its analytic box gradient)."""
+    _, H, W, D, _ = img.shape
+    ch, cw, cd = crop
+    y1, x1, z1, y2, x2, z2 = (float(v) for v in box)
+    r = [(S - 1) / (n - 1) if n > 1 else 0.0 for S, n in ((H, ch), (W, cw), (D, cd))]
+    scale = [(y2 - y1) * r[0], (x2 - x1) * r[1], (z2 - y1) * r[0]]
+    lo, hi = [y1, x1, z1], [y2, x2, z2]
+    out = np.zeros(6)
+    im = img[0].astype(np.float64)
+    for iy in range(ch):
+        for ix in range(cw):
+            for iz in range(cd):
+                p = [lo[a] * (S - 1) + i * scale[a] if n > 1 else 0.5 * (lo[a] + hi[a]) * (S - 1)
+                     for a, (S, i, n) in enumerate(((H, iy, ch), (W, ix, cw), (D, iz, cd)))]
+                if any(v < 0 or v > S - 1 for v, S in zip(p, (H, W, D))):
+                    continue
+                t = [int(np.floor(v)) for v in p]
+                b = [int(np.ceil(v)) for v in p]
+                l = [v - tt for v, tt in zip(p, t)]
+                c = {(a, bb, cc): im[(t, b)[a][0], (t, b)[bb][1], (t, b)[cc][2]]
+                     for a in (0, 1) for bb in (0, 1) for cc in (0, 1)}
+                wy, wx, wz = ((1 - l[0], l[0]), (1 - l[1], l[1]), (1 - l[2], l[2]))
+                gy = sum(wx[bb] * wz[cc] * (c[1, bb, cc] - c[0, bb, cc]) for bb in (0, 1) for cc in (0, 1))
+                gx = sum(wy[a] * wz[cc] * (c[a, 1, cc] - c[a, 0, cc]) for a in (0, 1) for cc in (0, 1))
+                gz = sum(wy[a] * wx[bb] * (c[a, bb, 1] - c[a, bb, 0]) for a in (0, 1) for bb in (0, 1))
+                gg = g[0, iy, ix, iz].astype(np.float64)
+                for a, (n, i, S, ga) in enumerate(((ch, iy, H, gy), (cw, ix, W, gx), (cd, iz, D, gz))):
+                    d = np.sum(ga * gg)
+                    out[a] += d * ((S - 1) - i * r[a]) if n > 1 else d * 0.5 * (S - 1)
+                    out[a + 3] += d * i * r[a] if n > 1 else d * 0.5 * (S - 1)
+    return out
+
+
+def test_grad_boxes_compiled_formulas():
+    """CropAndResize3DGradBoxes (restated from the wheel's
+    compiled code): (1) against an independent float64 evaluation of the same
+    formulas on boxes where the wheel's depth scale (z2 - y1)(H-1)/(ch-1)
+    differs from the forward's; (2) where the two coincide (y1 == z1,
+    (H-1)/(ch-1) == (D-1)/(cd-1)) it is the finite-difference derivative of
+    CropAndResize3D for all six coordinates; (3) single-sample axes (n == 1)."""
     rng = np.random.default_rng(4)
-    y, x, z = np.meshgrid(np.linspace(0, 1, 9), np.linspace(0, 1, 8), np.linspace(0, 1, 7), indexing="ij")
+    y, x, z = np.meshgrid(np.linspace(0, 1, 9), np.linspace(0, 1, 8), np.linspace(0, 1, 9), indexing="ij")
     img = np.stack([np.sin(3 * y + x) * np.cos(2 * z), y * x + z * z], -1)[None].astype(np.float32)
-    boxes = np.array([[0.11, 0.21, 0.16, 0.71, 0.79, 0.61]], np.float32)  # no sample on a grid line (kink)
-    g = rng.normal(size=(1, 4, 3, 5, 2)).astype(np.float32)
-    gb = R.crop_and_resize_3d_grad_boxes(g, img, boxes, [0])
-    eps = 1e-3
+    g = rng.normal(size=(1, 4, 3, 4, 2)).astype(np.float32)
+    for box in ([0.11, 0.21, 0.19, 0.71, 0.79, 0.63], [0.3, 0.05, 0.02, 0.9, 0.6, 0.95]):
+        boxes = np.array([box], np.float32)
+        gb = R.crop_and_resize_3d_grad_boxes(g, img, boxes, [0])[0]
+        ref = _grad_boxes_f64(g, img, boxes[0], (4, 3, 4))
+        assert np.allclose(gb, ref, rtol=1e-5, atol=1e-5), (gb, ref)
+    aligned = np.array([[0.16, 0.21, 0.16, 0.71, 0.79, 0.61]], np.float32)
+    gb = R.crop_and_resize_3d_grad_boxes(g, img, aligned, [0])
     for j in range(6):
-        bp, bm = boxes.copy(), boxes.copy()
-        bp[0, j] += eps
-        bm[0, j] -= eps
-        fp = np.sum(R.crop_and_resize_3d(img, bp, [0], (4, 3, 5)).astype(np.float64) * g)
-        fm = np.sum(R.crop_and_resize_3d(img, bm, [0], (4, 3, 5)).astype(np.float64) * g)
-        fd = (fp - fm) / (2 * eps)
+        fd = _fd_box_grad(img, aligned, g, (4, 3, 4), j)
         assert abs(gb[0, j] - fd) <= 2e-2 * (abs(fd) + 0.1), (j, gb[0, j], fd)
+    g1 = rng.normal(size=(1, 1, 3, 1, 2)).astype(np.float32)
+    gb1 = R.crop_and_resize_3d_grad_boxes(g1, img, aligned, [0])[0]
+    assert np.allclose(gb1, _grad_boxes_f64(g1, img, aligned[0], (1, 3, 1)), rtol=1e-5, atol=1e-5)
 
 
 # ---------------------------------------------------------------- NMS
