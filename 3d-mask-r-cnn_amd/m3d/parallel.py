@@ -128,13 +128,14 @@ class OverlappedAllReduce:
             self.store.grad_flat.mul_(1.0 / self.world)
 
 
-def data_parallel_train_step(model, image, targets, world, proposals=True, overlap=True):
+def data_parallel_train_step(model, image, targets, world, proposals=True, overlap=True, force_hook=False):
     """model.train_step with the gradient average inserted before SGD; with
-    ``overlap`` the buckets are all-reduced during the backward."""
+    ``overlap`` the buckets are all-reduced during the backward (``force_hook``:
+    also for a one-rank group, to exercise the collective path)."""
     from . import nn as mnn
     model.store.zero_grad()
     hook = None
-    if world > 1 and overlap:
+    if (world > 1 or force_hook) and overlap:
         hook = getattr(model, "_dp_hook", None)
         if hook is None or hook.world != world:
             hook = model._dp_hook = OverlappedAllReduce(model.store, world)

@@ -1,5 +1,5 @@
-"""Worker of tests/test_gpu_dp.py (torch.distributed.run, gloo, every rank on
-cuda:0): one data-parallel RPN step with the all-reduce after the backward and
+"""Worker of tests/test_gpu_dp.py (torch.distributed.run, gloo with every rank
+on cuda:0, or RCCL ("nccl") with one rank): one data-parallel RPN step with the all-reduce after the backward and
 one with buckets all-reduced during the backward (OverlappedAllReduce) from
 the same initial state; writes per-rank comparisons to OUT_DIR/rank<r>.json."""
 import json
@@ -15,7 +15,8 @@ import torch.distributed as dist  # noqa: E402
 
 def main():
     out_dir = sys.argv[1]
-    dist.init_process_group("gloo")
+    backend = sys.argv[2] if len(sys.argv) > 2 else "gloo"
+    dist.init_process_group(backend, device_id=torch.device("cuda", 0) if backend == "nccl" else None)
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -33,7 +34,7 @@ def main():
         if overlap:
             model._dp_hook = parallel.OverlappedAllReduce(model.store, world, bucket=1 << 20)
         r = parallel.data_parallel_train_step(model, image, RPNTargets(match, bbox, dev), world,
-                                              proposals=False, overlap=overlap)
+                                              proposals=False, overlap=overlap, force_hook=overlap)
         torch.cuda.synchronize()
         res[overlap] = (model.store.flat.detach().clone(), model.store.grad_flat.clone(), float(r["loss"]),
                         getattr(getattr(model, "_dp_hook", None), "n_early", None),

@@ -36,3 +36,20 @@ def test_overlapped_dp_step_matches(cuda, tmp_path):
     for x in res:
         assert x["grads_close"] and x["grads_same_on_ranks"] and x["param_max_diff"] < 1e-6, x
         assert x["n_buckets"] > 8 and x["n_early"] >= x["n_buckets"] - 2, x
+
+
+def test_overlapped_dp_step_rccl_device_path(cuda, tmp_path):
+    """The RCCL device path of the data-parallel step (backend "nccl", one rank:
+    RCCL refuses two ranks on one GPU): bucketed async all-reduces launched from
+    the autograd thread under the weight-gradient side stream, waited on by the
+    compute stream before SGD -- the same gradients and parameters as the step
+    without collectives."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path), "nccl"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = json.load(open(tmp_path / "rank0.json"))
+    assert x["grads_close"] and x["grads_same_on_ranks"] and x["param_max_diff"] < 1e-6, x
+    assert x["n_buckets"] > 8 and x["n_early"] >= x["n_buckets"] - 2, x
