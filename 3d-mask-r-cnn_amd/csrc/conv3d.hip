@@ -67,6 +67,11 @@ struct Epi {
     int ysy, ysx, ysz;
     int accumulate;
     int simple;       // y row == m (same grid, unit store stride)
+    // depth-slab halo (wino_output_kernel<.., HALO>): output z over the
+    // halo-extended grid; planes [hlo, hlo + dl) go to y (depth dl), the halo
+    // planes to yh [B][H][W][2][N] (plane 0 below, 1 above)
+    float* yh;
+    int hlo, dl;
     int deconv = 0;   // > 0: 2x2x2 stride-2 transposed conv, n = tap * deconv + o
 };
 
@@ -1396,6 +1401,10 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
 struct WinoGeom {
     int B, H, W, D, Din, pz, TY, TX, TZ;
     int64_t T;
+    // depth-slab halo (wino_input_kernel<.., HALO>): planes z = -1 and z = Din
+    // of the slab read from halo [B][H][W][2][C] (plane 0 / 1) when present
+    const float* halo;
+    int hlo, hhi;
 };
 
 __device__ __forceinline__ void bt4(float& a0, float& a1, float& a2, float& a3) {
@@ -1513,7 +1522,7 @@ __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b
 // (2ty-1, 2tx-1, NZ*tz-pz); xi = (a*4 + b)*P + k.
 // X3O: U is written as the three bf16 planes of split3 (uint16 [3][points][T][C])
 // for x3_gemm_kernel -- the split is done once here, not per GEMM k-tile.
-template <int NZ, bool X3O = false>
+template <int NZ, bool X3O = false, bool HALO = false>
 __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
                                                          int C, float* __restrict__ U) {
     constexpr int P = ZT<NZ>::P;
@@ -1528,6 +1537,8 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     // returns 0 (the zero padding), so all 16*P loads issue back to back
     // (conditional global loads compiled to a branch + wait per element)
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(x, (uint64_t)g.B * g.H * g.W * g.Din * C * 4);
+    __amdgpu_buffer_rsrc_t rh;
+    if constexpr (HALO) rh = make_rsrc(g.halo, (uint64_t)g.B * g.H * g.W * 2 * C * 4);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
         const int y = 2 * ty - 1 + a;
@@ -1542,6 +1553,17 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
                 const bool in = ok && (unsigned)z < (unsigned)g.Din;
                 d[a][bb][k] = __builtin_bit_cast(
                     float, __builtin_amdgcn_raw_buffer_load_b32(rs, in ? (row + (uint32_t)z * C) * 4u : M3D_OOB, 0, 0));
+                if constexpr (HALO) {
+                    // only the first / last window planes can reach a neighbour's plane
+                    if (k == 0 || k == P - 1) {
+                        const int q = z < 0 ? 0 : 1;
+                        const bool hz = ok && ((z == -1 && g.hlo) || (z == g.Din && g.hhi));
+                        const uint32_t hoff = (uint32_t)((((b * g.H + y) * g.W + xx) * 2 + q) * C + c) * 4u;
+                        const float hv = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(rh, hz ? hoff : M3D_OOB, 0, 0));
+                        d[a][bb][k] = hz ? hv : d[a][bb][k];
+                    }
+                }
             }
         }
     }
@@ -1681,9 +1703,24 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
 }
 
 // Y tile (2x2xNZ) = (A^T (x) A^T (x) Az^T) M[.][t][n], then the conv epilogue.
+template <int NZ, bool HALO>
+__device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, const WinoGeom& g,
+                                                 int N, const Epi& e);
 template <int NZ>
 __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, WinoGeom g,
                                                           int N, Epi e) {
+    wino_output_body<NZ, false>(Mt, g, N, e);
+}
+// depth-slab data gradient: interior planes into e.y, halo planes into e.yh
+template <int NZ>
+__global__ __launch_bounds__(256) void wino_output_halo_kernel(const float* __restrict__ Mt, WinoGeom g,
+                                                               int N, Epi e) {
+    wino_output_body<NZ, true>(Mt, g, N, e);
+}
+
+template <int NZ, bool HALO>
+__device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, const WinoGeom& g,
+                                                 int N, const Epi& e) {
     constexpr int P = ZT<NZ>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.T * N) return;
@@ -1731,7 +1768,19 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
             for (int k = 0; k < NZ; ++k) {
                 const int z = NZ * tz + k;
                 if (z >= g.D) continue;
-                const int64_t row = (((int64_t)b * g.H + y) * g.W + xx) * g.D + z;
+                const int64_t col = ((int64_t)b * g.H + y) * g.W + xx;
+                if constexpr (HALO) {
+                    const int zi = z - e.hlo;
+                    if (zi < 0 || zi >= e.dl) {          // a neighbour's plane: its gradient, fresh
+                        e.yh[(col * 2 + (zi < 0 ? 0 : 1)) * N + n] = o[a][bb][k];
+                        continue;
+                    }
+                    float* dst = e.y + (col * e.dl + zi) * e.ldy + n;
+                    const float v = o[a][bb][k];
+                    *dst = e.accumulate ? v + *dst : v;
+                    continue;
+                }
+                const int64_t row = col * g.D + z;
                 float v = o[a][bb][k];
                 if (e.bias) v += bias;
                 if (e.z) e.z[row * N + n] = v;
@@ -2229,6 +2278,8 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
     g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
     g.T = B * g.TY * g.TX * g.TZ;
+    g.halo = nullptr;
+    g.hlo = g.hhi = 0;
     return g;
 }
 
@@ -2591,6 +2642,22 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, in
         if ((nz) == 4) hipLaunchKernelGGL((kern<4, true>), __VA_ARGS__);         \
         else hipLaunchKernelGGL((kern<2, true>), __VA_ARGS__);                   \
     } while (0)
+// the input transform, reading a depth slab's halo planes when g.halo is set
+#define WINO_INPUT(nz, x3o, grid, s, x, g, C, U)                                                          \
+    do {                                                                                                   \
+        const bool h_ = (g).halo != nullptr;                                                               \
+        if ((nz) == 4) {                                                                                   \
+            if (x3o) { if (h_) hipLaunchKernelGGL((wino_input_kernel<4, true, true>), grid, dim3(256), 0, s, x, g, C, U); \
+                       else hipLaunchKernelGGL((wino_input_kernel<4, true, false>), grid, dim3(256), 0, s, x, g, C, U); } \
+            else { if (h_) hipLaunchKernelGGL((wino_input_kernel<4, false, true>), grid, dim3(256), 0, s, x, g, C, U); \
+                   else hipLaunchKernelGGL((wino_input_kernel<4, false, false>), grid, dim3(256), 0, s, x, g, C, U); } \
+        } else {                                                                                           \
+            if (x3o) { if (h_) hipLaunchKernelGGL((wino_input_kernel<2, true, true>), grid, dim3(256), 0, s, x, g, C, U); \
+                       else hipLaunchKernelGGL((wino_input_kernel<2, true, false>), grid, dim3(256), 0, s, x, g, C, U); } \
+            else { if (h_) hipLaunchKernelGGL((wino_input_kernel<2, false, true>), grid, dim3(256), 0, s, x, g, C, U); \
+                   else hipLaunchKernelGGL((wino_input_kernel<2, false, false>), grid, dim3(256), 0, s, x, g, C, U); } \
+        }                                                                                                  \
+    } while (0)
 
 // M3D_X3_BK (16 | 32) and M3D_X3_PERSIST (0 | 1): x3_gemm_kernel variant (A/B)
 static int x3_bk_env() {
@@ -2698,12 +2765,13 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
                     const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
                     const float* bn_scale, const float* bn_shift, const float* residual,
                     int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
-                    size_t ws_bytes, hipStream_t s) {
+                    size_t ws_bytes, hipStream_t s, const float* halo = nullptr, int hlo = 0, int hhi = 0) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
-    const WinoGeom g = wino_geom(B, H, W, OD, D, pz);
+    WinoGeom g = wino_geom(B, H, W, OD, D, pz);
+    g.halo = halo; g.hlo = hlo; g.hhi = hhi;
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
     if (gemm_x3_env() && !u_keep) {
         float* wt = ws.WT;
@@ -2712,11 +2780,7 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
         WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
                           (int)Cin, (int)Cout, 0, ws.V);
         const bool af32 = x3_af32_env();
-        if (af32)
-            WINO_LAUNCH(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g, (int)Cin, ws.U);
-        else
-            WINO_LAUNCH_NZ_X3(wino_nz(), wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
-                              (int)Cin, ws.U);
+        WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
         wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s, af32);
         Epi o{};
         o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
@@ -2728,8 +2792,7 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     if (u_keep) ws.U = u_keep;
     WINO_LAUNCH(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
                        (int)Cin, (int)Cout, 0, ws.V);
-    WINO_LAUNCH(wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, s, x, g,
-                       (int)Cin, ws.U);
+    WINO_INPUT(wino_nz(), false, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
     Epi e{};
     e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
@@ -2769,10 +2832,36 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
 // dx [B,H,W,D,Cin] = conv_transpose(dz [B,H,W,OD,Cout]): a 'same'-type 3x3x3
 // correlation of dz with the flipped, transposed kernel, tiles over dx's grid,
 // dz read at z = 2tz - (2 - pz) + k.
+static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                         int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                         void* workspace, size_t ws_bytes, hipStream_t s, float* dx_halo = nullptr,
+                         int hlo = 0);
+
 extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H,
                                         int64_t W, int64_t D, int64_t Cin, int64_t Cout,
                                         int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                                         void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s));
+}
+
+// the data-gradient output transform: dx over the (halo-extended) grid, or,
+// for a depth slab with dx_halo, interior planes into dx (depth dl) and the
+// neighbours' planes into dx_halo [B][H][W][2][C]
+static void wino_dgrad_out(const float* Mt, const WinoGeom& g, int C, float* dx, int accumulate,
+                           float* dx_halo, int hlo, int dl, int nz, hipStream_t hs) {
+    Epi o{};
+    o.y = dx; o.ldy = C; o.accumulate = accumulate;
+    if (dx_halo) {
+        o.yh = dx_halo; o.hlo = hlo; o.dl = dl;
+        WINO_LAUNCH_NZ(nz, wino_output_halo_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+        return;
+    }
+    WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+}
+
+static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                         int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                         void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -2782,55 +2871,50 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
     WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz);
     if (gemm_x3_env()) {
-        WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+        WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
                           (int)Cin, (int)Cout, 1, ws.V);
         const bool af32 = x3_af32_env();
         if (af32)
-            WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+            WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
                            (int)Cout, ws.U);
         else
-            WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+            WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
                               (int)Cout, ws.U);
-        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), st(s), af32);
-        Epi o{};
-        o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
-        WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
-                       g, (int)Cin, o);
+        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), hs, af32);
+        wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs);
         return check_launch("conv3d winograd bwd-data (x3)");
     }
-    WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w,
+    WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
                        (int)Cin, (int)Cout, 1, ws.V);
-    WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+    WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
                        (int)Cout, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cout, ws.V, (int)Cin);
     Epi e{};
     e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
-    dispatch_gemm<false, true>(p, e, st(s), wino_points(nz));
-    Epi o{};
-    o.y = dx; o.ldy = Cin; o.accumulate = accumulate;
-    WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), ws.M,
-                       g, (int)Cin, o);
+    dispatch_gemm<false, true>(p, e, hs, wino_points(nz));
+    wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs);
     return check_launch("conv3d winograd bwd-data");
 }
 
 static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, int64_t B,
                            int64_t H, int64_t W, int64_t D, int64_t Cin, int64_t Cout, int64_t OD,
-                           int32_t pz, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s) {
+                           int32_t pz, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s,
+                           const float* halo = nullptr, int hlo = 0, int hhi = 0) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
     const int nz = wino_wgrad_nz();
-    const WinoGeom g = wino_geom(B, H, W, OD, D, pz, nz);
+    WinoGeom g = wino_geom(B, H, W, OD, D, pz, nz);
+    g.halo = halo; g.hlo = hlo; g.hhi = hhi;
     WinoWs ws = wino_ws(workspace, g, Cin, Cout, nz);   // V <- dW_hat, U <- B^T x, M <- A dz
     if (hipMemsetAsync(ws.V, 0, sizeof(float) * wino_points(nz) * (size_t)Cin * Cout, st(s)) != hipSuccess)
         return check_launch("memset dW_hat");
     if (u_in)
         ws.U = const_cast<float*>(u_in);       // the forward's transformed input, kept
     else
-        WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cin, 256)), dim3(256), 0, st(s), x, g,
-                           (int)Cin, ws.U);
+        WINO_INPUT(nz, false, dim3(grid_for(g.T * Cin, 256)), st(s), x, g, (int)Cin, ws.U);
     WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     if (wgrad_x3_env() && Cout > 64) {
@@ -2853,6 +2937,56 @@ extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64
                                           int64_t OD, int32_t pz, float* dw, void* workspace,
                                           size_t ws_bytes, m3d_stream_t s) {
     return bwd_weight_wino(x, nullptr, dz, B, H, W, D, Cin, Cout, OD, pz, dw, workspace, ws_bytes, s);
+}
+
+// ---- depth-slab forms: interior slab + separate halo planes -----------------
+// x [B,H,W,Dl,C] is this rank's slab, x_halo [B,H,W,2,C] the neighbours'
+// boundary planes (plane 0 = z -1 from the lower rank, valid if has_lo;
+// plane 1 = z Dl from the upper rank, valid if has_hi).  The same tiles and
+// arithmetic as the halo-extended tensor (bit-identical results) without
+// materialising it.  workspace: m3d_conv3d_wino_workspace_bytes(B, H, W,
+// Dl + has_lo + has_hi, Dl, Cin, Cout).
+static int halo_check(const void* x_halo, int32_t has_lo, int32_t has_hi) {
+    if ((has_lo | has_hi) & ~1) return einval("conv3d winograd halo: has_lo / has_hi must be 0 or 1");
+    if ((has_lo || has_hi) && !x_halo) return einval("conv3d winograd halo: halo planes missing");
+    return M3D_OK;
+}
+
+extern "C" int m3d_conv3d_fwd_wino_halo(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi,
+                                        int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
+                                        const float* w, int64_t Cout, const float* bias, const float* bn_scale,
+                                        const float* bn_shift, const float* residual, int32_t relu, float* z_out,
+                                        float* y, float* u_keep, void* workspace, size_t ws_bytes,
+                                        m3d_stream_t s) {
+    int rc = halo_check(x_halo, has_lo, has_hi);
+    if (rc) return rc;
+    if (u_keep && wino_nz() != wino_wgrad_nz())
+        return einval("conv3d winograd: forward and weight-gradient tiles differ (m3d_conv3d_wino_u_bytes == 0)");
+    return fwd_wino(x, B, H, W, Dl, Cin, w, Cout, Dl, 1, bias, bn_scale, bn_shift, residual, relu, z_out, y,
+                    u_keep, workspace, ws_bytes, st(s), x_halo, has_lo, has_hi);
+}
+
+// dx [B,H,W,Dl,Cin] (interior, accumulate as m3d_conv3d_bwd_data_wino) and
+// dx_halo [B,H,W,2,Cin] = the gradient of the neighbours' halo planes (always
+// written; planes of absent neighbours are left untouched)
+extern "C" int m3d_conv3d_bwd_data_wino_halo(const float* dz, const float* w, int32_t has_lo, int32_t has_hi,
+                                             int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
+                                             int64_t Cout, float* dx, float* dx_halo, int32_t accumulate,
+                                             void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    int rc = halo_check(dx_halo, has_lo, has_hi);
+    if (rc) return rc;
+    return bwd_data_wino(dz, w, B, H, W, Dl + has_lo + has_hi, Cin, Cout, Dl, 1 - has_lo, dx, accumulate,
+                         workspace, ws_bytes, st(s), (has_lo || has_hi) ? dx_halo : nullptr, has_lo);
+}
+
+extern "C" int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_halo, int32_t has_lo,
+                                               int32_t has_hi, const float* dz, int64_t B, int64_t H, int64_t W,
+                                               int64_t Dl, int64_t Cin, int64_t Cout, float* dw, void* workspace,
+                                               size_t ws_bytes, m3d_stream_t s) {
+    int rc = halo_check(x_halo, has_lo, has_hi);
+    if (rc) return rc;
+    return bwd_weight_wino(x, nullptr, dz, B, H, W, Dl, Cin, Cout, Dl, 1, dw, workspace, ws_bytes, s, x_halo,
+                           has_lo, has_hi);
 }
 
 extern "C" int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H,

@@ -54,6 +54,12 @@ _SIGS = {
     "m3d_conv3d_bwd_weight": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
                               c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                               c_p, c_p],
+    "m3d_conv3d_fwd_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p,
+                                 c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
+                                      c_p, c_i32, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_weight_wino_halo": [c_p, c_p, c_i32, c_i32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                        c_p, c_p, c_sz, c_p],
     "m3d_gemm_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_p],
     "m3d_gemm_wgrad_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
     "m3d_split3_f32": [c_p, c_i64, c_p, c_p],

@@ -87,6 +87,11 @@ def _L():
     return _lib.load()
 
 
+# depth-slab sharding: the Winograd convs read the neighbours' halo planes beside
+# the slab (m3d_conv3d_*_wino_halo); M3D_SLAB_HALO_PLANES=0 builds the
+# halo-extended copy of every z-window input instead (torch.cat, the old path)
+SLAB_HALO_PLANES = os.environ.get("M3D_SLAB_HALO_PLANES", "1") != "0"
+
 # Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
 WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
 WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
@@ -216,8 +221,11 @@ class _ConvBNAct(torch.autograd.Function):
     source of y (FPN top-down add, core/models.py:3193-3204)."""
 
     @staticmethod
-    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None):
+    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, halo=None):
         B, H, W, D, Cin = x.shape
+        # depth slab (m3d.slab): halo = (planes [B,H,W,2,C], has_lo, has_hi) read by the
+        # Winograd kernels beside x instead of a halo-extended copy of x
+        ctx.halo = halo
         kh, kw, kd = geo.k
         Cout = w.shape[-1]
         OH, OW, OD = geo.out
@@ -236,15 +244,24 @@ class _ConvBNAct(torch.autograd.Function):
         else:
             ctx.bn = None
         ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
+        if halo is not None and not ctx.wino:
+            raise ValueError("halo planes are read by the Winograd kernels only")
         ctx.u = None
         if ctx.wino:
-            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
+            dext = D + (halo[1] + halo[2] if halo is not None else 0)
+            ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             # training: keep the transformed input U for the weight gradient when
             # the forward and weight-gradient tiles agree (u_bytes > 0)
             nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4 \
                 if grads is not None and grads.get("kernel") is not None \
                 and min(Cin, Cout) >= WINO_WGRAD_MIN_C else 0
-            if nu > 0:
+            if halo is not None:
+                ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
+                check(_L().m3d_conv3d_fwd_wino_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], B, H, W, D, Cin,
+                                                    ptr(w), Cout, ptr(b), ptr(scale), ptr(shift), ptr(residual),
+                                                    1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u), ptr(ws), wsb,
+                                                    stream()), "conv3d_fwd_wino_halo")
+            elif nu > 0:
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32)
                 check(_L().m3d_conv3d_fwd_wino_keep(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
                                                     ptr(b), ptr(scale), ptr(shift), ptr(residual),
@@ -306,15 +323,31 @@ class _ConvBNAct(torch.autograd.Function):
         if side is not None:
             dz.record_stream(side)
             x.record_stream(side)
+        halo = ctx.halo
+        dext = D + (halo[1] + halo[2] if halo is not None else 0)
+        if halo is not None and side is not None:
+            halo[0].record_stream(side)
         if ctx.wino:
             if grads.get("kernel") is not None:
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                     if min(Cin, Cout) < WINO_WGRAD_MIN_C:
-                        check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
-                                                      OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
-                                                      stream()), "conv3d_bwd_weight")
+                        xw, gw = x, geo
+                        if halo is not None:        # the direct kernel reads the halo-extended slab
+                            parts = ([halo[0][:, :, :, :1]] if halo[1] else []) + [x] + \
+                                ([halo[0][:, :, :, 1:]] if halo[2] else [])
+                            xw = torch.cat(parts, dim=3)
+                            gw = ConvGeom(geo.k, geo.stride, (geo.pad[0], geo.pad[1], 1 - halo[1]), geo.out)
+                        check(L.m3d_conv3d_bwd_weight(ptr(xw), ptr(dz), B, H, W, xw.shape[3], Cin, kh, kw, kd,
+                                                      Cout, OH, OW, OD, *gw.stride, *gw.pad,
+                                                      ptr(grads["kernel"]), stream()), "conv3d_bwd_weight")
+                    elif halo is not None and ctx.u is None:
+                        wsw, wswb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
+                        check(L.m3d_conv3d_bwd_weight_wino_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], ptr(dz),
+                                                                B, H, W, D, Cin, Cout, ptr(grads["kernel"]),
+                                                                ptr(wsw), wswb, stream()),
+                              "conv3d_bwd_weight_wino_halo")
                     else:
-                        wsw, wswb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
+                        wsw, wswb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
                         if ctx.u is not None:
                             ctx.u.record_stream(torch.cuda.current_stream())
                             check(L.m3d_conv3d_bwd_weight_wino_u(ptr(ctx.u), ptr(dz), B, H, W, D, Cin, Cout,
@@ -327,18 +360,26 @@ class _ConvBNAct(torch.autograd.Function):
                                                                wswb, stream()),
                                   "conv3d_bwd_weight_wino")
                 ctx.u = None
-            ws, wsb = _wino_ws(B, H, W, D, OD, Cin, Cout, x.device)
+            ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             dx = None
             if ctx.need_dx:
                 dx, acc = _link_take(ctx.link, x)
                 if dx is None:
                     dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
-                check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
-                                                 geo.pad[2], ptr(dx), acc, ptr(ws), wsb, stream()),
-                      "conv3d_bwd_data_wino")
+                if halo is not None:
+                    dh = torch.empty_like(halo[0])
+                    check(L.m3d_conv3d_bwd_data_wino_halo(ptr(dz), ptr(w), halo[1], halo[2], B, H, W, D, Cin,
+                                                          Cout, ptr(dx), ptr(dh), acc, ptr(ws), wsb, stream()),
+                          "conv3d_bwd_data_wino_halo")
+                    slab.return_halo_grads(dx, dh)
+                else:
+                    check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                     geo.pad[2], ptr(dx), acc, ptr(ws), wsb, stream()),
+                          "conv3d_bwd_data_wino")
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
-            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None
+            ctx.halo = None
+            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
@@ -375,7 +416,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
-        return dx, dr, None, None, None, None, None, None, None, None, None
+        return dx, dr, None, None, None, None, None, None, None, None, None, None
 
 
 def _slab_extend(x, geo):
@@ -406,10 +447,16 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)
     if residual is not None:
         residual = residual.contiguous()
-    x, geo = _slab_extend(x, geo)
+    halo = None
+    if (slab.current() is not None and SLAB_HALO_PLANES and res_mode != 2
+            and use_winograd(geo, x.shape[-1], w.shape[-1], tuple(x.shape[1:4]))):
+        # Winograd convs read the neighbours' planes beside the slab (no extended copy)
+        halo = slab.halo_planes(x.contiguous(), 1)
+    else:
+        x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                            need_dx and x.requires_grad, link)
+                            need_dx and x.requires_grad, link, halo)
 
 
 class _MaxPool(torch.autograd.Function):

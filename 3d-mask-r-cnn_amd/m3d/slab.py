@@ -190,6 +190,41 @@ class _HaloZ(torch.autograd.Function):
         return gx, None, None
 
 
+def halo_planes(x, r=1):
+    """The neighbours' r boundary planes of slab x [B,H,W,Dl,C] without
+    building the halo-extended slab: (halo [B,H,W,2r,C] -- planes [0, r) from
+    the lower rank, [r, 2r) from the upper --, has_lo, has_hi).  The Winograd
+    kernels read them beside x (m3d_conv3d_*_wino_halo); a rank at the volume's
+    end has no plane there (its padding is zero)."""
+    sg = _ACTIVE
+    B, H, W, D, C = x.shape
+    if r > D:
+        raise ValueError(f"z-halo of {r} planes exceeds the slab")
+    from_lo, from_hi = sg.exchange(x[:, :, :, :r] if sg.lo is not None else None,
+                                   x[:, :, :, D - r:] if sg.hi is not None else None, (B, H, W, r, C))
+    halo = torch.empty((B, H, W, 2 * r, C), device=x.device, dtype=x.dtype)
+    if from_lo is not None:
+        halo[:, :, :, :r] = from_lo
+    if from_hi is not None:
+        halo[:, :, :, r:] = from_hi
+    return halo, int(from_lo is not None), int(from_hi is not None)
+
+
+def return_halo_grads(dx, dhalo, r=1):
+    """Backward of halo_planes: send the gradient of each neighbour's planes
+    (dhalo [B,H,W,2r,C]) to it and add what the neighbours send for this
+    rank's boundary planes into dx [B,H,W,Dl,C] in place."""
+    sg = _ACTIVE
+    B, H, W, D, C = dx.shape
+    from_lo, from_hi = sg.exchange(dhalo[:, :, :, :r] if sg.lo is not None else None,
+                                   dhalo[:, :, :, r:] if sg.hi is not None else None, (B, H, W, r, C))
+    if from_lo is not None:
+        dx[:, :, :, :r] += from_lo
+    if from_hi is not None:
+        dx[:, :, :, D - r:] += from_hi
+    return dx
+
+
 def halo_z(x, r):
     """(x_ext, n_lower_halo_planes) under the active slab group (identity when
     not sharded or r == 0)."""

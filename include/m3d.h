@@ -210,6 +210,28 @@ int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, in
 int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H, int64_t W,
                                  int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
                                  float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
+/* Depth-slab forms (multi-GPU sharding of one volume, m3d/slab.py): x is this
+ * rank's slab [B,H,W,Dl,C] and x_halo [B,H,W,2,C] the neighbours' boundary
+ * planes (plane 0 = z -1 from the lower rank, valid if has_lo; plane 1 = z Dl
+ * from the upper rank, valid if has_hi) -- the halo-extended slab is never
+ * materialised; results are bit-identical to the extended-tensor calls.  The
+ * data gradient writes the slab's interior into dx [B,H,W,Dl,Cin] (accumulate
+ * as above) and the gradient of the neighbours' planes into dx_halo
+ * [B,H,W,2,Cin].  workspace: m3d_conv3d_wino_workspace_bytes(B,H,W,
+ * Dl + has_lo + has_hi, Dl, Cin, Cout).  u_keep as m3d_conv3d_fwd_wino_keep
+ * (NULL: not kept). */
+int m3d_conv3d_fwd_wino_halo(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi, int64_t B,
+                             int64_t H, int64_t W, int64_t Dl, int64_t Cin, const float* w, int64_t Cout,
+                             const float* bias, const float* bn_scale, const float* bn_shift,
+                             const float* residual, int32_t relu, float* z_out, float* y, float* u_keep,
+                             void* workspace, size_t ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_data_wino_halo(const float* dz, const float* w, int32_t has_lo, int32_t has_hi, int64_t B,
+                                  int64_t H, int64_t W, int64_t Dl, int64_t Cin, int64_t Cout, float* dx,
+                                  float* dx_halo, int32_t accumulate, void* workspace, size_t ws_bytes,
+                                  m3d_stream_t s);
+int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi,
+                                    const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
+                                    int64_t Cout, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
 
 /* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
  * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],

@@ -55,6 +55,47 @@ def test_halo_conv_equals_single_volume(world):
         assert nlo == (1 if rank > 0 else 0) and nhi == (1 if rank < world - 1 else 0)
 
 
+def _halo_planes_conv(rank, world, D=12):
+    """The Winograd slab form: halo_planes() hands the kernels the neighbours'
+    planes beside the slab (emulated here by a conv over [halo_lo, x, halo_hi]);
+    the data gradient comes back as (interior dx, dhalo) and return_halo_grads
+    routes dhalo to its owners -- equal to the single-volume conv."""
+    from m3d import slab
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((1, 5, 4, D, 3), generator=g, dtype=torch.float64)
+    w = torch.randn((3, 3, 3, 3, 2), generator=g, dtype=torch.float64)
+    gy = torch.randn((1, 5, 4, D, 2), generator=g, dtype=torch.float64)
+    xf = x.clone().requires_grad_(True)
+    yf = _conv_z(xf, w, 1, 1, 1)
+    (yf * gy).sum().backward()
+    sg = slab.SlabGroup(D, rank, world)
+    xs = x[:, :, :, sg.z0:sg.z1].clone()
+    with slab.active(sg):
+        halo, hlo, hhi = slab.halo_planes(xs, 1)
+        xe = torch.cat(([halo[:, :, :, :1]] if hlo else []) + [xs] + ([halo[:, :, :, 1:]] if hhi else []), 3)
+        xe.requires_grad_(True)
+        ys = _conv_z(xe, w, 1 - hlo, 1 - hhi, 1)
+        (ys * gy[:, :, :, sg.z0:sg.z1]).sum().backward()
+        dx = xe.grad[:, :, :, hlo:hlo + sg.Dl].clone()
+        dh = torch.zeros_like(halo)
+        if hlo:
+            dh[:, :, :, :1] = xe.grad[:, :, :, :1]
+        if hhi:
+            dh[:, :, :, 1:] = xe.grad[:, :, :, -1:]
+        slab.return_halo_grads(dx, dh)
+    ok_y = torch.allclose(ys, yf[:, :, :, sg.z0:sg.z1], rtol=0, atol=1e-12)
+    ok_g = torch.allclose(dx, xf.grad[:, :, :, sg.z0:sg.z1], rtol=0, atol=1e-12)
+    return [ok_y, ok_g, hlo, hhi]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_planes_equal_single_volume(world):
+    out = run(_halo_planes_conv, world)
+    for rank, (ok_y, ok_g, hlo, hhi) in out.items():
+        assert ok_y and ok_g, rank
+        assert hlo == (1 if rank > 0 else 0) and hhi == (1 if rank < world - 1 else 0)
+
+
 def _stem_halo(rank, world):
     return _halo_conv(rank, world, D=16, k=7)
 
