@@ -82,6 +82,13 @@ int main() {
                                            nullptr, 0, s));
     EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino_u(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, nullptr, 0, s));
 
+    EXPECT_EINVAL(m3d_conv3d_fwd_wino_halo(nf, nf, 2, 0, 1, 8, 8, 8, 128, nf, 128, nf, nf, nf, nf, 0, of, of,
+                                           of, nullptr, 0, s));
+    EXPECT_EINVAL(m3d_conv3d_bwd_data_wino_halo(nf, nf, 1, 0, 1, 8, 8, 8, 128, 128, of, nullptr, 0, nullptr, 0,
+                                                s));
+    EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino_halo(nf, nullptr, 0, 1, nf, 1, 8, 8, 8, 128, 128, of, nullptr, 0,
+                                                  s));
+
     // GEMMs
     EXPECT_EINVAL(m3d_gemm_f32(nf, nf, of, 1, 0, 4, 4, nf, 0, 0, s));
     EXPECT_EINVAL(m3d_gemm_wgrad_f32(nf, nf, of, 1, 4, -4, 4, s));
@@ -99,6 +106,8 @@ int main() {
                                         oi, oi, nullptr, 0, s));
     EXPECT_EINVAL(m3d_rpn_targets(nf, 64, nf, 2, 0.5f, 0.3f, 0, 0.5f, 9, 1, sd, 7u, nullptr, of, 64, nullptr, 0,
                                   oi, s));
+    EXPECT_EINVAL(m3d_rpn_targets_async(nf, 64, nf, 2, 0.5f, 0.3f, 128, 0.5f, 9, 1, sd, 7u, nullptr, of, 0,
+                                        nullptr, 0, oi, s));
 
     // pooling / resampling / BN / optimizers
     EXPECT_EINVAL(m3d_maxpool3d_fwd(nf, 1, 8, 8, 8, 4, 3, 3, 3, 0, 2, 1, 0, 0, 1, 4, 4, 8, of, nullptr, s));
