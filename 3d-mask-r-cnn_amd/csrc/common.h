@@ -28,6 +28,17 @@ inline int check_launch(const char* what) {
 
 inline hipStream_t st(m3d_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Deterministic mode (m3d_set_deterministic): the reductions that would add
+// fp32 partial sums with atomics in arrival order (weight-gradient m-splits,
+// per-tensor clip norms) write the partials into the registered scratch and
+// sum them in a fixed order instead.
+struct DetState {
+    int on;
+    void* scratch;
+    size_t bytes;
+};
+const DetState& det();
+
 inline unsigned grid_for(int64_t n, int per_block, int64_t cap = 1 << 30) {
     int64_t g = (n + per_block - 1) / per_block;
     if (g < 1) g = 1;

@@ -665,13 +665,72 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
 }
 
 // -------------------------------------------------------------------------
+// Weight-gradient epilogue target.  Default: fp32 atomics into C (the m-splits
+// of a tile arrive in any order, so the last bits vary run to run).
+// Deterministic mode (m3d_set_deterministic): each split stores its tile into
+// part[split][batch][K][N] of the registered scratch and wg_reduce_kernel adds
+// the splits to C in split order; with a single split (the scratch too small
+// for two), the one writer of each element adds to C without an atomic.
+// -------------------------------------------------------------------------
+struct WgOut {
+    float* part;
+    int64_t pstride;      // floats per split (nbatch * K * N)
+    int plain;
+};
+
+__device__ __forceinline__ void wg_put(const WgOut& o, float* C, float* P, int64_t idx, float v) {
+    if (P) P[idx] = v;
+    else if (o.plain) C[idx] += v;
+    else unsafeAtomicAdd(C + idx, v);
+}
+
+// C[b*bsc + r] += sum_{s = 0..splits-1} part[s][b][r]  (r < K*N), summed in s order
+__global__ __launch_bounds__(256) void wg_reduce_kernel(const float* __restrict__ part, int splits,
+                                                        int64_t pstride, int64_t kn, int64_t bsc,
+                                                        float* __restrict__ C) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= pstride) return;
+    float s = part[i];
+    for (int q = 1; q < splits; ++q) s += part[q * pstride + i];
+    const int64_t b = i / kn, r = i - b * kn;
+    C[b * bsc + r] += s;
+}
+
+// deterministic-mode target for `splits` m-splits of an nbatch x K x N gradient
+// (splits may be lowered to what the scratch holds)
+static WgOut wg_out(int64_t& splits, int64_t nbatch, int64_t K, int64_t N) {
+    WgOut o{nullptr, 0, 0};
+    const DetState& d = det();
+    if (!d.on) return o;
+    const int64_t per = nbatch * K * N;
+    const int64_t fit = (int64_t)(d.bytes / sizeof(float)) / per;
+    if (splits <= 1 || fit < 2) {
+        splits = 1;
+        o.plain = 1;
+        return o;
+    }
+    if (splits > fit) splits = fit;
+    o.part = static_cast<float*>(d.scratch);
+    o.pstride = per;
+    return o;
+}
+
+static void wg_finish(const WgOut& o, int64_t splits, int64_t nbatch, int64_t K, int64_t N, int64_t bsc,
+                      float* C, hipStream_t s) {
+    if (!o.part) return;
+    hipLaunchKernelGGL(wg_reduce_kernel, dim3(grid_for(o.pstride, 256)), dim3(256), 0, s, o.part, (int)splits,
+                       o.pstride, K * N, nbatch > 1 ? bsc : K * N, C);
+}
+
+// -------------------------------------------------------------------------
 // bwd-weight: dW[k][n] += sum_m im2col(X)[m][k] * dZ[m][n]
-// grid (K/BI, N/BJ, splits); each block reduces its m-range, fp32 atomics out.
+// grid (K/BI, N/BJ, splits); each block reduces its m-range, fp32 atomics out
+// (or the deterministic-mode target, WgOut).
 // -------------------------------------------------------------------------
 template <int BI, int BJ, int WI, int WJ, bool AVEC>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float* __restrict__ dz,
                                                             float* __restrict__ dw,
-                                                            int64_t m_per_split) {
+                                                            int64_t m_per_split, WgOut wo) {
     constexpr int BKM = 32;
     constexpr int TI = BI / (WI * 32), TJ = BJ / (WJ * 32);
     static_assert(WI * WJ == 4, "4 waves");
@@ -697,6 +756,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
     const int n0 = (rem / gridDim.x) * BJ;
     const int64_t nsplit = (p.M + m_per_split - 1) / m_per_split;
     const int64_t batch = bz_ / nsplit;
+    float* const wp = wo.part ? wo.part + (bz_ % nsplit) * wo.pstride + batch * (int64_t)p.K * p.N : nullptr;
     if (batch) {
         p.a += batch * p.bsa;
         dz += batch * p.bsw;
@@ -833,7 +893,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = k0 + wi * TI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (k < p.K) unsafeAtomicAdd(dw + (int64_t)k * p.N + n, acc[i][j][r]);
+                if (k < p.K) wg_put(wo, dw, wp, (int64_t)k * p.N + n, acc[i][j][r]);
             }
         }
 }
@@ -976,13 +1036,15 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
     const int64_t max_splits = (p.M + minm - 1) / minm;             // >= minm m per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
+    const WgOut wo = wg_out(splits, nbatch, p.K, p.N);
     int64_t mper = (p.M + splits - 1) / splits;
     mper = (mper + 31) / 32 * 32;
     splits = (p.M + mper - 1) / mper;
     dim3 grid((unsigned)((p.K + BI - 1) / BI), (unsigned)((p.N + BJ - 1) / BJ),
               (unsigned)(splits * nbatch));
     hipLaunchKernelGGL((conv_wgrad_kernel<BI, BJ, WI, WJ, AVEC>), grid, dim3(256), 0, s, p, dz, dw,
-                       mper);
+                       mper, wo);
+    wg_finish(wo, splits, nbatch, p.K, p.N, p.bsy, dw, s);
 }
 
 
@@ -1000,7 +1062,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
                                                             const float* __restrict__ Bm,
                                                             float* __restrict__ C, int64_t M, int K, int N,
                                                             int64_t m_per_split, int64_t bsa, int64_t bsb,
-                                                            int64_t bsc) {
+                                                            int64_t bsc, WgOut wo) {
     constexpr int BI = 128, BJ = 128, TI = 2, TJ = 2, BKM = 32;
     constexpr int PL = 128 * BKM * 2;                    // bytes per plane (128 rows x 64 B)
     __shared__ __attribute__((aligned(16))) char smem[6 * PL];
@@ -1016,6 +1078,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
     const int n0 = (rem / gridDim.x) * BJ;
     const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
     const int64_t batch = bz / nsplit;
+    float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
     A += batch * bsa;
     Bm += batch * bsb;
     C += batch * bsc;
@@ -1113,7 +1176,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = k0 + wi * TI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (k < K) unsafeAtomicAdd(C + (int64_t)k * N + n, acc[i][j][r]);
+                if (k < K) wg_put(wo, C, wp, (int64_t)k * N + n, acc[i][j][r]);
             }
         }
 }
@@ -1159,7 +1222,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
                                                              const float* __restrict__ Bm,
                                                              float* __restrict__ C, int64_t M, int K,
                                                              int N, int64_t m_per_split, int64_t bsa,
-                                                             int64_t bsb, int64_t bsc) {
+                                                             int64_t bsb, int64_t bsc, WgOut wo) {
     __shared__ __attribute__((aligned(16))) char smem[2 * W2_STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
@@ -1173,6 +1236,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
     const int n0 = (rem / gridDim.x) * 256;
     const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
     const int64_t batch = bz / nsplit;
+    float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
     A += batch * bsa;
     Bm += batch * bsb;
     C += batch * bsc;
@@ -1307,7 +1371,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = k0 + wk * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (k < K) unsafeAtomicAdd(C + (int64_t)k * N + n, acc[i][j][r]);
+                if (k < K) wg_put(wo, C, wp, (int64_t)k * N + n, acc[i][j][r]);
             }
         }
 }
@@ -1327,19 +1391,21 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t max_splits = (M + 63) / 64;              // >= 4 k-steps per workgroup
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
+    const WgOut wo = wg_out(splits, nbatch, K, N);
     int64_t mper = (M + splits - 1) / splits;
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
     static const int dbg = [] { const char* e = getenv("M3D_X3W_DBG"); return e ? atoi(e) : 0; }();
     switch (dbg) {
-        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
-        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
-        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
-        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
-        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc); break;
-        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
+        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
+        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
+        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
+        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
+        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
     }
+    wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
 }
 
 // M3D_GEMM_X3 bit 2: the batched Winograd weight-gradient GEMMs on x3_wgrad_kernel
@@ -1358,15 +1424,17 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
+    const WgOut wo = wg_out(splits, nbatch, K, N);
     int64_t mper = (M + splits - 1) / splits;
     mper = (mper + 31) / 32 * 32;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 127) / 128), (unsigned)((N + 127) / 128), (unsigned)(splits * nbatch));
     static const int occ = [] { const char* e = getenv("M3D_X3W_OCC"); return e && atoi(e) == 3 ? 3 : 2; }();
     if (occ == 2)
-        hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+        hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
     else
-        hipLaunchKernelGGL((x3_wgrad_kernel<3>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc);
+        hipLaunchKernelGGL((x3_wgrad_kernel<3>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
+    wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
 }
 
 // =========================================================================

@@ -388,6 +388,46 @@ __global__ __launch_bounds__(256) void sgd_norm_kernel(const float* __restrict__
     flush();
 }
 
+// Deterministic mode: chunk_norm_kernel writes each chunk's sum of squares
+// (fixed reduction tree) to part[chunk]; seg_norm_kernel (one block per
+// segment) adds the chunks of its segment in chunk order per thread and a
+// fixed tree across threads.  No assumption on the chunk -> segment order.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const float r = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(256) void chunk_norm_kernel(const float* __restrict__ w,
+                                                         const float* __restrict__ g,
+                                                         const int32_t* __restrict__ seg_of_chunk,
+                                                         const float* __restrict__ l2,
+                                                         float* __restrict__ part) {
+    __shared__ float red[4];
+    const int64_t ch = blockIdx.x;
+    const float lc = l2[seg_of_chunk[ch]];
+    const int64_t off = ch * 1024 + threadIdx.x * 4;
+    const float4 wv = *(const float4*)(w + off), gv = *(const float4*)(g + off);
+    const float a = gv.x + lc * wv.x, b = gv.y + lc * wv.y, c = gv.z + lc * wv.z, d = gv.w + lc * wv.w;
+    const float r = block_sum256(a * a + b * b + c * c + d * d, red);
+    if (threadIdx.x == 0) part[ch] = r;
+}
+
+__global__ __launch_bounds__(256) void seg_norm_kernel(const int32_t* __restrict__ seg_of_chunk,
+                                                       const float* __restrict__ part, int64_t n_chunks,
+                                                       float* __restrict__ norms) {
+    __shared__ float red[4];
+    const int seg = blockIdx.x;
+    float s = 0.0f;
+    for (int64_t c = threadIdx.x; c < n_chunks; c += 256)
+        if (seg_of_chunk[c] == seg) s += part[c];
+    const float r = block_sum256(s, red);
+    if (threadIdx.x == 0) norms[seg] = r;
+}
+
 __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ w,
                                                          const float* __restrict__ g,
                                                          float* __restrict__ v,
@@ -658,6 +698,31 @@ extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, i
     return check_launch("bn_sums_reduce_kernel");
 }
 
+// per-segment squared norms of (grad + l2 * w) for tf.clip_by_norm
+static int clip_norms(const float* params, const float* grads, int64_t n_chunks,
+                      const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
+                      float clipnorm, float* norms, m3d_stream_t s) {
+    if (!(clipnorm > 0.f)) return M3D_OK;
+    const DetState& d = det();
+    if (d.on) {
+        if (d.bytes < sizeof(float) * (size_t)n_chunks)
+            return einval("clip norms (deterministic mode): scratch smaller than n_chunks floats");
+        float* part = static_cast<float*>(d.scratch);
+        hipLaunchKernelGGL(chunk_norm_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params, grads,
+                           seg_of_chunk, l2_coef, part);
+        int rc = check_launch("chunk_norm_kernel");
+        if (rc || n_segments == 0) return rc;
+        hipLaunchKernelGGL(seg_norm_kernel, dim3((unsigned)n_segments), dim3(256), 0, st(s), seg_of_chunk,
+                           (const float*)part, (int64_t)n_chunks, norms);
+        return check_launch("seg_norm_kernel");
+    }
+    if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
+        return check_launch("memset norms");
+    hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)((n_chunks + SGD_NORM_CHUNKS - 1) / SGD_NORM_CHUNKS)),
+                       dim3(256), 0, st(s), params, grads, seg_of_chunk, l2_coef, (int64_t)n_chunks, norms);
+    return check_launch("sgd_norm_kernel");
+}
+
 extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
                              const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
                              float lr, float momentum, float clipnorm, float* norms,
@@ -666,28 +731,11 @@ extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, 
     if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !moments || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
         return einval("sgd: null pointer");
-    if (clipnorm > 0.f) {
-        if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
-            return check_launch("memset norms");
-        hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)((n_chunks + SGD_NORM_CHUNKS - 1) / SGD_NORM_CHUNKS)),
-                           dim3(256), 0, st(s), params, grads, seg_of_chunk, l2_coef, (int64_t)n_chunks, norms);
-        int rc = check_launch("sgd_norm_kernel");
-        if (rc) return rc;
-    }
+    int rc = clip_norms(params, grads, n_chunks, seg_of_chunk, l2_coef, n_segments, clipnorm, norms, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(sgd_update_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st(s), params,
                        grads, moments, seg_of_chunk, l2_coef, norms, lr, momentum, clipnorm);
     return check_launch("sgd_update_kernel");
-}
-
-static int clip_norms(const float* params, const float* grads, int64_t n_chunks,
-                      const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
-                      float clipnorm, float* norms, m3d_stream_t s) {
-    if (!(clipnorm > 0.f)) return M3D_OK;
-    if (hipMemsetAsync(norms, 0, sizeof(float) * n_segments, st(s)) != hipSuccess)
-        return check_launch("memset norms");
-    hipLaunchKernelGGL(sgd_norm_kernel, dim3((unsigned)((n_chunks + SGD_NORM_CHUNKS - 1) / SGD_NORM_CHUNKS)),
-                       dim3(256), 0, st(s), params, grads, seg_of_chunk, l2_coef, (int64_t)n_chunks, norms);
-    return check_launch("sgd_norm_kernel");
 }
 
 extern "C" int m3d_adam_keras(float* params, const float* grads, float* m, float* v, float* vhat,

@@ -177,6 +177,16 @@ __global__ __launch_bounds__(256) void atss_chunk_topk_kernel(const uint64_t* __
     }
 }
 
+// sum over a 256-thread block: wave butterfly, then the four waves in order
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const double r = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return r;
+}
+
 // One workgroup per GT: k-th largest key of its list (radix select, 8-bit
 // digits, over the chunk top-k union `cand` when given), stats over the
 // top-k, ATSS marking.
@@ -195,12 +205,12 @@ __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ 
     __shared__ unsigned hist[256];
     __shared__ uint64_t s_prefix;
     __shared__ int s_need;
-    __shared__ double s_sum, s_sq;
+    __shared__ double s_red[4];
     __shared__ int s_cand;
     const int tid = threadIdx.x;
     // threshold key K* = k-th largest key (or the smallest key if n <= k)
     const int kk = k < n ? k : n;
-    if (tid == 0) { s_prefix = 0; s_need = kk; s_sum = 0.0; s_sq = 0.0; s_cand = 0; }
+    if (tid == 0) { s_prefix = 0; s_need = kk; s_cand = 0; }
     __syncthreads();
     for (int pass = 0; pass < 8; ++pass) {
         const int shift = 56 - 8 * pass;
@@ -227,22 +237,21 @@ __global__ __launch_bounds__(256) void atss_kernel(const uint64_t* __restrict__ 
     }
     const uint64_t kth = s_prefix;                          // exact: keys are unique
     // mean / std over the top-k IoUs (entries beyond the list are zeros)
+    // sums in a fixed order (per-thread strided, then a fixed tree): the same
+    // mean / std on every run, unlike shared-memory atomics
     double sum = 0.0;
     for (int j = tid; j < n; j += blockDim.x)
         if (L[j] >= kth) sum += (double)__uint_as_float((uint32_t)(L[j] >> 32));
-    atomicAdd(&s_sum, sum);
-    __syncthreads();
-    const double mu = s_sum / (double)k;
+    const double mu = block_sum_d(sum, s_red) / (double)k;
     double sq = 0.0;
     for (int j = tid; j < n; j += blockDim.x)
         if (L[j] >= kth) {
             const double dv = (double)__uint_as_float((uint32_t)(L[j] >> 32)) - mu;
             sq += dv * dv;
         }
-    atomicAdd(&s_sq, sq);
-    __syncthreads();
+    const double ssq = block_sum_d(sq, s_red);
     const double zeros = (double)(k - kk);                  // top-k members with IoU 0
-    const double sd = sqrt((s_sq + zeros * mu * mu) / (double)k);
+    const double sd = sqrt((ssq + zeros * mu * mu) / (double)k);
     // np.mean / np.std return float32; thr = max(pos, mu + sd) in Python
     // float; `ious_g >= thr` compares in float32
     const double s32 = (double)(float)mu + (double)(float)sd;

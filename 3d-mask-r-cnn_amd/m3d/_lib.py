@@ -111,11 +111,14 @@ _SIGS = {
     "m3d_adam_keras": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_f, c_p,
                        c_p],
     "m3d_adadelta_keras": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_p, c_p],
+    "m3d_set_deterministic": [c_i32, c_p, c_sz],
+    "m3d_get_deterministic": [],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_conv3d_wino_workspace_bytes": c_sz,
-             "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32}
+             "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32,
+             "m3d_get_deterministic": c_i32}
 
 EXPORTED = tuple(_SIGS)
 
@@ -160,3 +163,26 @@ def ptr(t) -> int:
 
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
+
+
+_DET_SCRATCH = None
+
+
+def set_deterministic(on: bool = True, scratch_bytes: int = 256 << 20, device=None) -> None:
+    """Bitwise run-to-run reproducible training (m3d_set_deterministic): the
+    weight-gradient m-splits and the clip norms are summed in a fixed order
+    through a device scratch of ``scratch_bytes`` instead of fp32 atomics.  The
+    scratch is shared by those reductions, so they must stay ordered on one
+    stream at a time (the training step's weight-gradient stream, then the
+    optimizer after the join).  A weight gradient larger than half the scratch
+    runs unsplit (still deterministic, slower)."""
+    global _DET_SCRATCH
+    lib = load()
+    if not on:
+        check(lib.m3d_set_deterministic(0, None, 0), "set_deterministic")
+        _DET_SCRATCH = None
+        return
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    buf = torch.empty(max(int(scratch_bytes), 4096) // 4, dtype=torch.float32, device=dev)
+    check(lib.m3d_set_deterministic(1, buf.data_ptr(), buf.numel() * 4), "set_deterministic")
+    _DET_SCRATCH = buf

@@ -650,6 +650,27 @@ def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
 
 
 # ---------------------------------------------------------------- main
+def deterministic_leg(step, steps, warmup):
+    """The same N=1 training step in deterministic mode (m3d.set_deterministic:
+    weight-gradient m-splits and clip norms summed in a fixed order through a
+    scratch buffer, no fp32 atomics): ms/step, and whether two runs of the
+    weights' update agree bit for bit is covered by tests/test_gpu_determinism."""
+    from m3d import _lib
+    _lib.set_deterministic(True)
+    try:
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    finally:
+        _lib.set_deterministic(False)
+    return {"ms_per_step": round(el / steps * 1e3, 2), "steps": steps, "scratch_mb": 256}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -750,6 +771,10 @@ def main():
             out["targets_in_step"] = targets_in_step_leg(model, image, max(3, args.steps // 2), 2, dev)
         except Exception as e:  # report, never hide
             out["targets_in_step"] = {"error": repr(e)}
+        try:
+            out["deterministic"] = deterministic_leg(step, max(3, args.steps // 2), 2)
+        except Exception as e:  # report, never hide
+            out["deterministic"] = {"error": repr(e)}
     if rank == 0 and not args.no_extras:
         with torch.no_grad():
             fmaps = model.features(image)

@@ -14,7 +14,8 @@
  *   - return 0 (M3D_OK) on success, M3D_EINVAL for an argument the reference
  *     op would reject (m3d_last_error() then holds the reference's
  *     InvalidArgument text), M3D_EHIP for a HIP launch error.
- *   - no global mutable state apart from the thread-local error string.
+ *   - no global mutable state apart from the thread-local error string and
+ *     the process-wide deterministic-mode switch (m3d_set_deterministic).
  */
 #ifndef M3D_H
 #define M3D_H
@@ -34,6 +35,19 @@ typedef struct ihipStream_t* m3d_stream_t; /* == hipStream_t */
 
 const char* m3d_last_error(void);
 int m3d_abi_version(void);
+
+/* Deterministic mode (process-wide; the analogue of TF_DETERMINISTIC_OPS for
+ * the reference's training graph, core/models.py:3340-3387).  on = 1: every
+ * weight-gradient GEMM (m3d_conv3d_bwd_weight*, m3d_gemm_wgrad_f32) stores its
+ * m-split partial tiles into `scratch` and adds them to dW in split order
+ * instead of fp32 atomics, and the optimizers' clip norms are summed in chunk
+ * order; results are then bitwise identical run to run.  `scratch` (device,
+ * 16-B aligned, >= 4096 bytes) is shared by those reductions: launch them on
+ * one stream at a time.  A gradient whose two splits do not fit runs unsplit.
+ * The ROIAlign backward keeps its atomics (use crop_and_resize3d_bwd_image's
+ * deterministic flag).  on = 0 restores the atomic reductions. */
+int m3d_set_deterministic(int32_t on, void* scratch, size_t bytes);
+int32_t m3d_get_deterministic(void);
 
 /* ---------------------------------------------------------------------------
  * CropAndResize3D family.  Replaces the TF custom ops of the vendored wheel

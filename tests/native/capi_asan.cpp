@@ -120,6 +120,12 @@ int main() {
     EXPECT_EINVAL(m3d_sgd_keras(of, nf, of, -1, ni, nf, 1, 0.01f, 0.9f, 5.f, of, s));
     EXPECT_EINVAL(m3d_adam_keras(of, nf, of, of, of, -1, ni, nf, 1, 1e-3f, 0.9f, 0.999f, 1e-7f, 5.f, of, s));
     EXPECT_EINVAL(m3d_adadelta_keras(of, nf, of, of, -1, ni, nf, 1, 1.f, 0.95f, 1e-7f, 5.f, of, s));
+    EXPECT_EINVAL(m3d_set_deterministic(1, nullptr, 1 << 20));
+    EXPECT_EINVAL(m3d_set_deterministic(1, of, 64));
+    if (m3d_set_deterministic(0, nullptr, 0) != M3D_OK || m3d_get_deterministic() != 0) {
+        fprintf(stderr, "set_deterministic(0) failed\n");
+        return 1;
+    }
 
     // workspace sizing: pure host arithmetic over small .. huge shapes
     size_t acc = 0;

@@ -18,6 +18,13 @@ def close(got, ref, rtol=1e-4):
     assert err <= rtol * scale, f"max err {err:.3e} vs scale {scale:.3e}"
 
 
+def _join():
+    """Weight gradients run on the side stream (m3d.nn.WGRAD_STREAM): join it
+    before reading them, as RPNHead.finish_backward does in the model."""
+    from m3d.nn import join_wgrad
+    join_wgrad()
+
+
 class _Layer:
     """Minimal stand-in of params.ConvLayer over explicit tensors."""
 
@@ -101,6 +108,7 @@ def test_conv_block_fwd_bwd(cuda, case, wino, monkeypatch):
     close(y, yr)
     g = torch.tensor(rng.normal(size=yr.shape), dtype=torch.float32)
     y.backward(g.to(cuda))
+    _join()
     yr.backward(g.double())
     close(layer.kernel.grad, wr.grad)
     close(layer.bias.grad, br.grad)
@@ -130,6 +138,7 @@ def test_fpn_upsample_residual(cuda):
     close(y, yr)
     g = torch.randn(yr.shape)
     y.backward(g.to(cuda))
+    _join()
     yr.backward(g.double())
     close(r.grad, rr.grad)
     close(x.grad, xr.grad)
@@ -148,6 +157,7 @@ def test_maxpool_same_and_subsample(cuda, C):
     np.testing.assert_array_equal(y.detach().cpu().numpy(), yr.detach().float().numpy())
     g = torch.randn(yr.shape)
     y.backward(g.to(cuda))
+    _join()
     yr.backward(g.double())
     close(xg.grad, xr.grad, rtol=1e-6)
     if C % 4:
