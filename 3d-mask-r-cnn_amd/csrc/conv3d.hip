@@ -2409,6 +2409,27 @@ extern "C" int m3d_gemm_wgrad_f32(const float* A, const float* Bm, float* C, int
     return check_launch("m3d_gemm_wgrad_f32");
 }
 
+// The loaders address x / w / dz through 32-bit buffer offsets and the GEMM
+// row index m through 32-bit division: an operand the kernels read must stay
+// below 4 GiB and 2^31 voxels.  The conv entry points check that per batch item
+// and run a batch whose whole tensors pass it one item at a time (the
+// epilogues store through 64-bit pointers).  M3D_OPERAND_LIMIT (bytes) lowers
+// the bound, to exercise the per-item path at test sizes.
+static int64_t op_lim() {
+    static const int64_t v = [] {
+        const char* e = getenv("M3D_OPERAND_LIMIT");
+        const long long l = e ? atoll(e) : 0;
+        return (int64_t)((l > 0 && l < 0xFFFFFFF0LL) ? l : 0xFFFFFFF0LL) / 4;
+    }();
+    return v;
+}
+
+// batch of B items of in-voxels vin x cin and out-voxels vout x cout: one item at a time?
+static bool per_item(int64_t B, int64_t vin, int64_t cin, int64_t vout, int64_t cout) {
+    return B > 1 && (B * vin * cin >= op_lim() || B * vout * cout >= op_lim() || B * vin > 0x7FFFFFFF ||
+                     B * vout > 0x7FFFFFFF);
+}
+
 static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, int32_t kh,
                       int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
                       int32_t sy, int32_t sx, int32_t sz) {
@@ -2419,13 +2440,11 @@ static int conv_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, i
     if (OH <= 0 || OW <= 0 || OD <= 0) return einval("conv3d: output dimensions must be positive");
     if (Cout % 4) return einval("conv3d: Cout must be a multiple of 4");
     if ((int64_t)kh * kw * kd * Cin > 0x7FFFFFFF) return einval("conv3d: K too large");
-    if (B * H * W * D > 0x7FFFFFFF || B * OH * OW * OD > 0x7FFFFFFF)
-        return einval("conv3d: more than 2^31 voxels per tensor");
-    // 32-bit buffer addressing: every operand below 4 GiB
-    const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
-    if (B * H * W * D * Cin >= lim || B * OH * OW * OD * Cout >= lim ||
-        (int64_t)kh * kw * kd * Cin * Cout >= lim)
-        return einval("conv3d: operand larger than 4 GiB (32-bit buffer offsets)");
+    if (H * W * D > 0x7FFFFFFF || OH * OW * OD > 0x7FFFFFFF)
+        return einval("conv3d: more than 2^31 voxels per batch item");
+    const int64_t lim = op_lim();
+    if (H * W * D * Cin >= lim || OH * OW * OD * Cout >= lim || (int64_t)kh * kw * kd * Cin * Cout >= lim)
+        return einval("conv3d: operand of one batch item larger than 4 GiB (32-bit buffer offsets)");
     return M3D_OK;
 }
 
@@ -2537,6 +2556,19 @@ extern "C" int m3d_conv3d_fwd_dil(const float* x, int64_t B, int64_t H, int64_t 
     if (res_mode != 0 && residual == nullptr) return einval("conv3d: residual missing");
     if (res_mode == 2 && ((OH & 1) || (OW & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
     if (split_n > 0 && y2 == nullptr) return einval("conv3d: split output needs y2");
+    if (per_item(B, H * W * D, Cin, OH * OW * OD, Cout)) {
+        const int64_t xs = H * W * D * Cin, os = OH * OW * OD, ld = ldy > 0 ? ldy : Cout;
+        const int64_t rs = res_mode == 2 ? (OH / 2) * (OW / 2) * OD * Cout : os * ld;
+        for (int64_t b = 0; b < B; ++b) {
+            rc = m3d_conv3d_fwd_dil(x + b * xs, 1, H, W, D, Cin, w, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px,
+                                    pz, dly, dlx, dlz, bias, bn_scale, bn_shift,
+                                    residual ? residual + b * rs : nullptr, res_mode, act_code,
+                                    z_out ? z_out + b * os * Cout : nullptr, y + b * os * ld, ldy,
+                                    y2 ? y2 + b * os * ldy2 : nullptr, ldy2, split_n, s);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0, 0, 0, 0};
     p.dly = dly; p.dlx = dlx; p.dlz = dlz;
@@ -2572,6 +2604,14 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
     const bool unit = kh == 1 && kw == 1 && kd == 1;
     if (!unit && (sy != 1 || sx != 1 || sz != 1))
         return einval("conv3d bwd-data: strided convs supported for 1x1x1 kernels only");
+    if (per_item(B, H * W * D, Cin, OH * OW * OD, Cout)) {
+        for (int64_t b = 0; b < B; ++b) {
+            rc = m3d_conv3d_bwd_data(dz + b * OH * OW * OD * Cout, w, 1, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
+                                     sy, sx, sz, py, px, pz, dx + b * H * W * D * Cin, accumulate, s);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     ConvP p{};
     Epi e{};
     e.y = dx;
@@ -2617,6 +2657,14 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
                                      int32_t pz, float* dw, m3d_stream_t s) {
     int rc = conv_check(B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
     if (rc) return rc;
+    if (per_item(B, H * W * D, Cin, OH * OW * OD, Cout)) {      // dw accumulates over the items
+        for (int64_t b = 0; b < B; ++b) {
+            rc = m3d_conv3d_bwd_weight(x + b * H * W * D * Cin, dz + b * OH * OW * OD * Cout, 1, H, W, D, Cin, kh,
+                                       kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px, pz, dw, s);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
@@ -2651,11 +2699,16 @@ static int wino_check(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, in
     if (Cin % 32 || Cout % 32) return einval("conv3d winograd: Cin and Cout must be multiples of 32");
     if (pz < 0 || pz > 1 || D - OD < 0 || D - OD > 2)
         return einval("conv3d winograd: z geometry must be pz in {0,1} and 0 <= D - OD <= 2");
-    if (B * H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
-    // the input transform reads x / dz through 32-bit buffer offsets
-    if (B * H * W * (D > OD ? D : OD) * (Cin > Cout ? Cin : Cout) * 4 > 0xFFFFFFF0LL)
-        return einval("conv3d winograd: operand larger than 4 GiB (32-bit buffer offsets)");
+    if (H * W * (D > OD ? D : OD) > 0x7FFFFFFF) return einval("conv3d winograd: more than 2^31 voxels");
+    // the input transform reads x / dz through 32-bit buffer offsets (per batch
+    // item: a larger batch runs one item at a time, see op_lim)
+    if (H * W * (D > OD ? D : OD) * (Cin > Cout ? Cin : Cout) >= op_lim())
+        return einval("conv3d winograd: operand of one batch item larger than 4 GiB (32-bit buffer offsets)");
     return M3D_OK;
+}
+
+static bool wino_per_item(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD, int64_t Cin, int64_t Cout) {
+    return per_item(B, H * W * (D > OD ? D : OD), Cin > Cout ? Cin : Cout, 0, 0);
 }
 // Workspace: V [P][Cin][Cout] + U [P][T][C1] + M [P][T][C2] (P = 16*(NZ+2) points) with
 // {C1, C2} = {Cin, Cout} (fwd / wgrad) or {Cout, Cin} (bwd-data), T the larger
@@ -2673,6 +2726,7 @@ extern "C" int32_t m3d_conv3d_wino_tile_z(void) { return wino_nz(); }
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout)) B = 1;     // run one batch item at a time
     size_t best = 0;
     for (int nz : {wino_nz(), wino_wgrad_nz(), wino_dgrad_nz()}) {
         const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz);
@@ -2838,6 +2892,17 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {
+        if (u_keep) return einval("conv3d winograd: u_keep with a batch past the 32-bit operand bound");
+        const int64_t os = H * W * OD * Cout;
+        for (int64_t b = 0; b < B; ++b) {
+            rc = fwd_wino(x + b * H * W * D * Cin, 1, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift,
+                          residual ? residual + b * os : nullptr, relu, z_out ? z_out + b * os : nullptr, y + b * os,
+                          nullptr, workspace, ws_bytes, s, halo ? halo + b * H * W * 2 * Cin : nullptr, hlo, hhi);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     g.halo = halo; g.hlo = hlo; g.hhi = hhi;
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
@@ -2934,6 +2999,16 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {
+        const int64_t dxd = dx_halo ? OD : D;          // dx depth: the slab's interior, or the full grid
+        for (int64_t b = 0; b < B; ++b) {
+            rc = bwd_data_wino(dz + b * H * W * OD * Cout, w, 1, H, W, D, Cin, Cout, OD, pz, dx + b * H * W * dxd * Cin,
+                               accumulate, workspace, ws_bytes, hs,
+                               dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     const int nz = wino_dgrad_nz();
     const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
@@ -2973,6 +3048,16 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {           // dw accumulates over the items
+        if (u_in) return einval("conv3d winograd: kept U with a batch past the 32-bit operand bound");
+        for (int64_t b = 0; b < B; ++b) {
+            rc = bwd_weight_wino(x + b * H * W * D * Cin, nullptr, dz + b * H * W * OD * Cout, 1, H, W, D, Cin, Cout,
+                                 OD, pz, dw, workspace, ws_bytes, s, halo ? halo + b * H * W * 2 * Cin : nullptr, hlo,
+                                 hhi);
+            if (rc) return rc;
+        }
+        return M3D_OK;
+    }
     const int nz = wino_wgrad_nz();
     WinoGeom g = wino_geom(B, H, W, OD, D, pz, nz);
     g.halo = halo; g.hlo = hlo; g.hhi = hhi;

@@ -1,6 +1,7 @@
 """GPU parity of the conv / pooling / optimizer kernels against the float64
 PyTorch-CPU restatement of the Keras graph (oracle/model_ref.py).
 Tolerance (north_star): fp32 results within 1e-4 relative to the output scale."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -306,3 +307,35 @@ def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
     C = torch.empty((nb, M, N), device=cuda)
     _lib.check(L.m3d_gemm_x3(A3.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, M, K, N, _lib.stream()), "gemm_x3")
     close(C, torch.bmm(A.double(), Bt.double().transpose(1, 2)))
+
+
+def test_batch_items_past_operand_bound(tmp_path):
+    """Every conv entry point with a batch whose tensors pass the loaders'
+    32-bit operand bound runs one batch item at a time (M3D_OPERAND_LIMIT
+    lowers the 4 GiB bound to 500 KB so a 3 x 262 KB batch crosses it): the
+    forward and data gradients are bit-identical to the whole-batch launch,
+    the weight gradients (summed per item) within fp32 reassociation, and the
+    Winograd workspace shrinks to one item's."""
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(__file__), "operand_limit_worker.py")
+    res = {}
+    for tag, lim in (("whole", None), ("items", "500000")):
+        env = dict(os.environ)
+        env.pop("M3D_OPERAND_LIMIT", None)
+        if lim:
+            env["M3D_OPERAND_LIMIT"] = lim
+        out = str(tmp_path / f"{tag}.npz")
+        p = subprocess.run([sys.executable, worker, out], env=env, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res[tag] = np.load(out)
+    a, b = res["whole"], res["items"]
+    assert (b["ws_bytes"] < a["ws_bytes"]).all()
+    for k in a.files:
+        if k == "ws_bytes":
+            continue
+        if k.endswith("dw"):
+            scale = float(np.abs(a[k]).max())
+            assert float(np.abs(a[k] - b[k]).max()) <= 1e-5 * scale, k
+        else:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
