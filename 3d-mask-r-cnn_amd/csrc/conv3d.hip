@@ -923,7 +923,7 @@ static int num_cus() {
     return v;
 }
 
-// M3D_GEMM_X3 (bit mask, default 13): fp32 GEMMs on the exact 3-way bf16 split
+// M3D_GEMM_X3 (bit mask, default 29): fp32 GEMMs on the exact 3-way bf16 split
 // (6 bf16 MFMAs per product, see split3) instead of v_mfma_f32_32x32x2_f32.
 // bit 0: Winograd fwd / bwd-data point GEMMs on operands pre-split by the
 // transforms (x3_gemm_kernel; measured 39.9 -> 37.9 ms/step at 128^3, GEMM
@@ -932,9 +932,11 @@ static int num_cus() {
 // Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step);
 // bit 3: the weight gradients of 1x1x1 stride-1 convs on the same kernel;
 // bit 4: the Winograd input transform writes U as fp32 (4 B per point
-// instead of 3 x 2 B) and x3_gemm_kernel splits it in its LDS store.
+// instead of 3 x 2 B) and the point GEMM (x3_gemm256_af_kernel, or
+// x3_gemm_kernel<AF32>) splits it on its way into LDS: a third less HBM
+// traffic for U, 34.2 -> 32.9 ms/step at 128^3 (default on).
 static int x3_mask() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 13; }();
+    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 29; }();
     return v;
 }
 static int gemm_x3_env() { return x3_mask() & 1; }
@@ -2311,6 +2313,159 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
         }
 }
 
+// ---- x3_gemm256 with A in fp32 (4 B per point instead of three bf16 planes) --
+// The Winograd input transform is the step's largest HBM writer (6 B per point
+// of U, 12 GB per 128^3 step); with U in fp32 it writes and the GEMM reads a
+// third less.  A is loaded into registers two steps ahead (thread t: row t/2,
+// the 8 k of chunk t&1: two float4), split3 in registers and written into the
+// same swizzled x3_off16 image with one ds_write_b128 per plane (each 8-lane
+// write group covers 32 banks once); B (the weight planes) still moves by
+// LDS-DMA.  Per step and wave: A-load(kt+2) (2 ops) then B-DMA(kt+2) (3 ops),
+// always issued (out-of-range steps read zeros into unused stages), so the
+// counted waits are static: vmcnt(5) retires B-DMA(kt) at the top of step kt,
+// vmcnt(8) the A rows of step kt+1 before they are split into stage kt+1.
+// Every stage is its own __shared__ array and the k loop is unrolled by 6
+// (stage = kt % 3, register set = kt % 2, both static), so the compiler can see
+// that the DMA in flight and the ds_reads / ds_writes of other stages do not
+// alias and inserts no vmcnt(0) drain of the prefetch.  Same split, same MFMA
+// order: bit-identical to x3_gemm256_kernel.
+template <int N_> struct IC { static constexpr int v = N_; };
+__global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
+    __shared__ __attribute__((aligned(16))) char sA0[3 * G2_PL], sA1[3 * G2_PL], sA2[3 * G2_PL];
+    __shared__ __attribute__((aligned(16))) char sB0[3 * G2_PL], sB1[3 * G2_PL], sB2[3 * G2_PL];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
+    const int64_t nbx = (g.M + 255) / 256, nby = g.N / 256;
+    const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
+    const int64_t L = (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+    if (L >= total) return;
+    const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+    const int64_t bz = T / per_batch, Tt = T - bz * per_batch;
+    const int64_t m0 = (Tt / nby) * 256;
+    const int64_t n0 = (Tt % nby) * 256;
+    const int nk = g.K / G2_BK;
+    // A: fp32 rows from the tile's first row (rows past M and steps past nk read zeros)
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.af + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 4);
+    const int arow = tid >> 1, ach = tid & 1;
+    const uint32_t aoff0 = ((uint32_t)arow * (uint32_t)g.K + (uint32_t)ach * 8u) * 4u;
+    const int awr = x3_off16(arow, ach);
+    __amdgpu_buffer_rsrc_t rb[3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+        rb[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + n0 * g.K, (uint64_t)256 * g.K * 2);
+    const int lrow = 32 * wave + (lane >> 1);
+    const uint32_t lsrc = (uint32_t)lrow * (uint32_t)g.K * 2u + (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4);
+    auto stA = [&](auto st) -> char* {
+        if constexpr (decltype(st)::v == 0) return sA0;
+        else if constexpr (decltype(st)::v == 1) return sA1;
+        else return sA2;
+    };
+    auto stB = [&](auto st) -> char* {
+        if constexpr (decltype(st)::v == 0) return sB0;
+        else if constexpr (decltype(st)::v == 1) return sB1;
+        else return sB2;
+    };
+    auto load_a = [&](int kt, float4 (&v)[2]) {
+        const bool in = kt < nk;
+        const uint32_t o = aoff0 + (uint32_t)kt * (G2_BK * 4);
+        v[0] = bload4(ra, in ? o : M3D_OOB);
+        v[1] = bload4(ra, in ? o + 16u : M3D_OOB);
+    };
+    auto dma_b = [&](auto st, int kt) {
+        char* S = stB(st) + wave * 1024;
+        const uint32_t off = kt < nk ? lsrc + (uint32_t)kt * (G2_BK * 2) : M3D_OOB;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G2_PL, off);
+    };
+    auto split_a = [&](auto st, const float4 (&v)[2]) {
+        char* S = stA(st) + awr;
+        uint2 lo4[3], hi4[3];
+        split3x4(v[0], lo4);
+        split3x4(v[1], hi4);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<uint4*>(S + q * G2_PL) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
+    };
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    float4 xa[2], ya[2];            // A rows of the even / odd steps
+    load_a(0, xa);
+    dma_b(IC<0>{}, 0);
+    load_a(1, ya);
+    dma_b(IC<1>{}, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A(0)
+    split_a(IC<0>{}, xa);
+    // step kt on stage st = kt % 3: cur holds A(kt+1) (loaded at step kt-1), nxt
+    // receives A(kt+2) (its A(kt) was split at step kt-1)
+    auto step = [&](auto st, int kt, float4 (&cur)[2], float4 (&nxt)[2]) {
+        constexpr int s0 = decltype(st)::v;
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // B(kt); own A(kt) writes
+        __builtin_amdgcn_s_barrier();
+        load_a(kt + 2, nxt);
+        dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");              // A(kt+1)
+        split_a(IC<(s0 + 1) % 3>{}, cur);        // stage last read at step kt-2
+        const char* SA = stA(st);
+        const char* SB = stB(st);
+        bf16x8 bfr[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int off = x3_off16(wn * 64 + j * 32 + l32, h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                bfr[j][pl] = *reinterpret_cast<const bf16x8*>(SB + pl * G2_PL + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int off = x3_off16(wm * 128 + i * 32 + l32, h);
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                floatx16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+            }
+        }
+    };
+    // stage kt % 3 and register set kt % 2 static: six steps per trip
+    for (int kt = 0;;) {
+        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
+        step(IC<2>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<0>{}, kt, xa, ya); if (++kt >= nk) break;
+        step(IC<1>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<2>{}, kt, xa, ya); if (++kt >= nk) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = (int)n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = acc[i][j][r];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                      (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u),
+                                                      0, 0);
+            }
+        }
+}
+
 // M3D_X3_256 (default 1): the Winograd point GEMMs with N % 256 == 0 on
 // x3_gemm256_kernel; 0 keeps x3_gemm_kernel everywhere (A/B)
 static int x3_256_env() {
@@ -2809,6 +2964,12 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
     q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
     q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
+    if (af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
+        const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
+        const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
+        hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
+        return;
+    }
     if (!af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
@@ -2874,6 +3035,22 @@ extern "C" int m3d_gemm_x3(const uint16_t* A3, const uint16_t* B3, float* C, int
     ws.WT = nullptr;
     wino_gemm_x3(ws, M, (int)K, (int)N, (int)batch, st(s));
     return check_launch("m3d_gemm_x3");
+}
+
+extern "C" int m3d_gemm_x3_af(const float* A, const uint16_t* B3, float* C, int64_t batch, int64_t M, int64_t K,
+                              int64_t N, m3d_stream_t s) {
+    if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm_x3_af: dimensions must be positive");
+    if (K % 32 || N % 4) return einval("gemm_x3_af: K must be a multiple of 32 and N of 4");
+    if (!A || !B3 || !C) return einval("gemm_x3_af: null operand");
+    if (M > 0x7FFFFFFF || M * K * 4 >= 0xFFFFFFF0LL || N * K * 2 >= 0xFFFFFFF0LL || M * N * 4 >= 0xFFFFFFF0LL)
+        return einval("gemm_x3_af: operand larger than 4 GiB (32-bit buffer offsets)");
+    WinoWs ws;
+    ws.U = const_cast<float*>(A);
+    ws.V = (float*)const_cast<uint16_t*>(B3);
+    ws.M = C;
+    ws.WT = nullptr;
+    wino_gemm_x3(ws, M, (int)K, (int)N, (int)batch, st(s), true);
+    return check_launch("m3d_gemm_x3_af");
 }
 
 

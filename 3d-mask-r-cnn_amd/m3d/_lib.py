@@ -64,6 +64,7 @@ _SIGS = {
     "m3d_gemm_wgrad_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
     "m3d_split3_f32": [c_p, c_i64, c_p, c_p],
     "m3d_gemm_x3": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
+    "m3d_gemm_x3_af": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
     "m3d_conv3d_wino_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64],
     "m3d_conv3d_fwd_wino": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
                             c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_sz, c_p],

@@ -93,37 +93,37 @@ def wino_gemm_shape(S):
 
 
 def time_wino_gemm(S, reps=5):
-    """x3_gemm_kernel (the step's second kernel) on its largest launch through
-    m3d_gemm_x3 (operands split once, untimed, as the Winograd transforms do in
-    the step)."""
+    """The Winograd point GEMMs of rpn_conv_shared1 on P2 in the form the step
+    runs them (M3D_GEMM_X3 bit 4): U in fp32 split inside x3_gemm256_af_kernel,
+    the weight planes split once, untimed, as the weight transform does in the
+    step (m3d_gemm_x3_af)."""
     from m3d import _lib
     L = _lib.load()
     nb, T, K, N = wino_gemm_shape(S)
     g = torch.Generator(device="cuda").manual_seed(5)
     A = torch.randn((nb, T, K), device="cuda", generator=g)
     Bt = torch.randn((nb, N, K), device="cuda", generator=g) * 0.05
-    A3 = torch.empty(3 * A.numel(), dtype=torch.int16, device="cuda")
     B3 = torch.empty(3 * Bt.numel(), dtype=torch.int16, device="cuda")
-    _lib.check(L.m3d_split3_f32(A.data_ptr(), A.numel(), A3.data_ptr(), _lib.stream()), "split3")
     _lib.check(L.m3d_split3_f32(Bt.data_ptr(), Bt.numel(), B3.data_ptr(), _lib.stream()), "split3")
-    del A, Bt
+    del Bt
     C = torch.empty((nb, T, N), device="cuda")
 
     def launch():
-        _lib.check(L.m3d_gemm_x3(A3.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, T, K, N, _lib.stream()),
-                   "gemm_x3")
+        _lib.check(L.m3d_gemm_x3_af(A.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, T, K, N, _lib.stream()),
+                   "gemm_x3_af")
     t = _event_time(launch, reps)
     flops = 2.0 * nb * T * K * N
-    key = f"wino_gemm_x3_rpn_shared1_S{S}"
+    key = f"wino_gemm_x3af_rpn_shared1_S{S}"
     return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": X3_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4),
             "traffic": _pmc_traffic(key),
-            "kernel": f"x3_gemm_kernel (fp32 GEMM as 6 bf16 MFMAs per product on the exact 3-way split): "
+            "kernel": f"x3_gemm256_af_kernel (fp32 GEMM as 6 bf16 MFMAs per product on the exact 3-way split, "
+                      f"A in fp32 split in registers): "
                       f"{nb} batched Winograd point GEMMs of rpn_conv_shared1 on P2, M={T} K={K} N={N}",
             "peak_note": "bf16 MFMA dense peak 2516.6 TFLOP/s / 6; achieved counts fp32 FLOPs 2*M*K*N",
             "f32_mfma_peak_frac": round(flops / t / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
             "flop_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
-            "algorithmic_bytes_per_launch": nb * (6.0 * (T * K + N * K) + 4.0 * T * N),
+            "algorithmic_bytes_per_launch": nb * (4.0 * T * K + 6.0 * N * K + 4.0 * T * N),
             "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
 
 

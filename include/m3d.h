@@ -276,6 +276,12 @@ int m3d_split3_f32(const float* x, int64_t n, uint16_t* x3, m3d_stream_t s);
  * bench.py prices the RPN head's largest launch with it. */
 int m3d_gemm_x3(const uint16_t* A3, const uint16_t* B3, float* C, int64_t batch, int64_t M, int64_t K,
                 int64_t N, m3d_stream_t s);
+/* m3d_gemm_x3 with A as fp32 [batch][M][K], split in the GEMM on its way into
+ * LDS (x3_gemm256_af_kernel for N % 256 == 0, else x3_gemm_kernel<AF32>): the
+ * form the Winograd point GEMMs run in the step (M3D_GEMM_X3 bit 4, default),
+ * bit-identical to m3d_gemm_x3 on the split planes of the same A. */
+int m3d_gemm_x3_af(const float* A, const uint16_t* B3, float* C, int64_t batch, int64_t M, int64_t K,
+                   int64_t N, m3d_stream_t s);
 
 /* Strided batched GEMM: for b < batch, C + b*bsc [M][N] (+)= act(A[b] B[b] + bias)
  * with A[b] = A + b*bsa (rows of stride lda >= K), B[b] = B + b*bsb [K][N]; act

@@ -1,6 +1,6 @@
 """Runs ONE priced launch of bench.py a few times for the rocprofv3 --pmc
 passes of scripts/gpu_prof.sh:  kernels_for_pmc.py LEG [S]
-  gemm    x3_gemm_kernel's largest launch (batched Winograd GEMM of rpn_conv_shared1)
+  gemm    the Winograd point GEMM launch of rpn_conv_shared1 (x3_gemm256_af_kernel)
   wgrad   the dominant kernel's largest launch: batched Winograd weight-gradient GEMM of rpn_conv_shared1 (x3_wgrad_kernel)
   direct  rpn_conv_shared1 as a direct implicit-GEMM conv on P2
   roi7 / roi14  PyramidROIAlign 7^3 / 14^3 at configs[2] shapes

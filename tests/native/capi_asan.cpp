@@ -95,6 +95,9 @@ int main() {
     EXPECT_EINVAL(m3d_split3_f32(nf, 0, nullptr, s));
     EXPECT_EINVAL(m3d_gemm_x3(nullptr, nullptr, of, 1, 64, 48, 64, s));        // K % 32
     EXPECT_EINVAL(m3d_gemm_x3(nullptr, nullptr, of, 1, 1LL << 40, 64, 64, s)); // > 4 GiB operand
+    EXPECT_EINVAL(m3d_gemm_x3_af(nf, nullptr, of, 1, 64, 48, 64, s));           // K % 32
+    EXPECT_EINVAL(m3d_gemm_x3_af(nullptr, nullptr, of, 1, 64, 64, 64, s));      // null A
+    EXPECT_EINVAL(m3d_gemm_x3_af(nf, nullptr, of, 1, 1LL << 40, 64, 64, s));    // > 4 GiB operand
     EXPECT_EINVAL(m3d_gemm_f32_ex(nf, 4, 16, nf, 16, of, 16, 1, 4, 0, 4, nf, 0, 0, s));
     EXPECT_EINVAL(m3d_splitk_reduce(nf, 0, 4, 4, nf, nf, nf, 0, of, s));
 

@@ -290,7 +290,7 @@ def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
     """m3d_split3_f32: hi + mid + lo == x exactly (float64 sum of the bf16
     planes); m3d_gemm_x3 (the Winograd point-GEMM kernels: x3_gemm_kernel,
     and x3_gemm256_kernel for N % 256 == 0, M >= 256) against float64, ragged
-    M tiles."""
+    M tiles; m3d_gemm_x3_af (fp32 A) bit-identical to it."""
     from m3d import _lib
     L = _lib.load()
     g = torch.Generator().manual_seed(13)
@@ -307,6 +307,12 @@ def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
     C = torch.empty((nb, M, N), device=cuda)
     _lib.check(L.m3d_gemm_x3(A3.data_ptr(), B3.data_ptr(), C.data_ptr(), nb, M, K, N, _lib.stream()), "gemm_x3")
     close(C, torch.bmm(A.double(), Bt.double().transpose(1, 2)))
+    # the step's form: A in fp32, split inside the GEMM (x3_gemm256_af_kernel /
+    # x3_gemm_kernel<AF32>): the same split and MFMA order, bit-identical
+    C2 = torch.full((nb, M, N), float("nan"), device=cuda)
+    _lib.check(L.m3d_gemm_x3_af(Ad.data_ptr(), B3.data_ptr(), C2.data_ptr(), nb, M, K, N, _lib.stream()),
+               "gemm_x3_af")
+    assert torch.equal(C, C2)
 
 
 def test_batch_items_past_operand_bound(tmp_path):
