@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libm3d.so")
+# M3D_LIB_FILE: another build of the same sources in this directory (A/B runs)
+LIB_PATH = os.path.join(_HERE, os.environ.get("M3D_LIB_FILE", "libm3d.so"))
 
 _lib = None
 

@@ -27,7 +27,14 @@ def init_from_env(backend=None):
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
+        if backend == "nccl":
+            # bind this rank to its GPU before the communicator exists (eager
+            # RCCL init on that device; barriers need not guess the device)
+            local = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend=backend, device_id=local)
+        else:
+            dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
 
 

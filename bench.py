@@ -11,6 +11,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -34,6 +35,34 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICRO
 # fp32-FLOP ceiling is a sixth of it
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 X3_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
+
+
+class LegWatchdog:
+    """Bounds a multi-rank leg whose collectives have no timeout of their own:
+    if the leg is still running after `seconds`, rank 0 prints the result line
+    gathered so far (the leg reported as timed out) and every rank leaves with
+    status 0, so one hung leg cannot cost the bench line of the whole run."""
+
+    def __init__(self, seconds, rank, out, key):
+        import threading
+        self.rank, self.out, self.key = rank, out, key
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+
+    def _fire(self):
+        if self.rank == 0:
+            self.out[self.key] = {"error": "timeout: the leg did not finish (watchdog)"}
+            print(json.dumps(self.out), flush=True)
+        log(f"[bench] watchdog: {self.key} timed out on rank {self.rank}, exiting")
+        os._exit(0)
+
+    def __enter__(self):
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.cancel()
+        return False
 
 
 def log(*a):
@@ -758,8 +787,12 @@ def main():
         del r
         torch.cuda.empty_cache()
         try:
-            out["depth_slab"] = depth_slab_leg(args.slab_size, args.steps, args.warmup, rank, world, dev,
-                                               proposals=props)
+            # N > 1: the halo exchanges and merged proposals run over RCCL P2P /
+            # all-gathers that have no timeout of their own
+            with LegWatchdog(float(os.environ.get("M3D_SLAB_LEG_TIMEOUT", "300")), rank, out, "depth_slab") \
+                    if world > 1 else contextlib.nullcontext():
+                out["depth_slab"] = depth_slab_leg(args.slab_size, args.steps, args.warmup, rank, world, dev,
+                                                   proposals=props)
         except Exception as e:  # report, never hide
             out["depth_slab"] = {"error": repr(e)}
     if world == 1 and not args.no_extras:

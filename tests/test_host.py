@@ -165,3 +165,24 @@ def test_gradlink_is_bound_and_checked():
     buf, acc = _link_take(link, x)
     assert acc == 1 and link.buf is None
     check_links(reg)
+
+
+def test_bench_leg_watchdog_prints_line_and_exits():
+    """bench.LegWatchdog: a leg still running after its limit makes rank 0
+    print the result line gathered so far (the leg marked timed out) and the
+    process leave with status 0."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import time, bench\n"
+            "out = {'metric': 'm', 'value': 1.0}\n"
+            "with bench.LegWatchdog(0.5, 0, out, 'depth_slab'):\n"
+            "    time.sleep(30)\n"
+            "print('not reached')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and "timeout" in d["depth_slab"]["error"]
