@@ -267,6 +267,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
             }
         }
     }
+    if (!part) return;          // elementwise only (block-uniform): no channel sums
     __shared__ float red[3][256][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -688,9 +689,10 @@ extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, i
     const bool sums = sum_dpre || sum_dpre_xhat || sum_dz;
     if (sums && ws_bytes < sizeof(float) * 3 * (size_t)gx * (size_t)C)
         return einval("bn_act_bwd: workspace too small");
+    if (!sums && !dz && !dres) return M3D_OK;
     hipLaunchKernelGGL(bn_act_bwd_kernel, dim3((unsigned)gx, (unsigned)groups), dim3(256), 0, st(s),
                        dy, y, z, M, (int)C, T, relu, scale, mean, rstd, dz, dres, accumulate_res,
-                       sum_dpre_xhat ? 1 : 0, (float*)workspace);
+                       sum_dpre_xhat ? 1 : 0, sums ? (float*)workspace : nullptr);
     int rc = check_launch("bn_act_bwd_kernel");
     if (rc || !sums) return rc;
     hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 15) / 16), 3), dim3(256), 0, st(s),

@@ -427,6 +427,8 @@ int m3d_bn_affine(const float* gamma, const float* beta, const float* mean, cons
  * non-NULL, in a fixed order (deterministic, no float atomics):
  *   sum_dpre[c] += sum dpre, sum_dpre_xhat[c] += sum dpre*(z-mean)*rstd,
  *   sum_dz[c] += sum dz.
+ * With all three sums NULL it is elementwise only (no workspace needed); with
+ * dz and dres NULL it computes the sums only.
  * workspace: m3d_bn_act_bwd_workspace_bytes(M, C) bytes of device scratch. */
 size_t m3d_bn_act_bwd_workspace_bytes(int64_t M, int64_t C);
 int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, int64_t C,

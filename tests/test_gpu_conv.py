@@ -345,3 +345,44 @@ def test_batch_items_past_operand_bound(tmp_path):
             assert float(np.abs(a[k] - b[k]).max()) <= 1e-5 * scale, k
         else:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, True)])
+def test_bn_act_bwd_modes(relu, res):
+    """m3d_bn_act_bwd against the float64 formulas (include/m3d.h), and its
+    elementwise-only (no sums, no workspace) and sums-only (no dz / dres)
+    calls equal to the fused one bit for bit."""
+    from m3d import nn as mnn
+    torch.manual_seed(5)
+    dev = torch.device("cuda")
+    M, C = 3000, 96
+    dy, z = torch.randn(M, C, device=dev), torch.randn(M, C, device=dev)
+    gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    mean, var = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
+    rstd = 1.0 / torch.sqrt(var + 1e-3)
+    scale, shift = gamma * rstd, beta - mean * gamma * rstd
+    y = z * scale + shift
+    if relu:
+        y = torch.relu(y)
+
+    def run(with_dz, with_sums):
+        dz = torch.full_like(dy, 7.0) if with_dz else None
+        dres = torch.full_like(dy, 7.0) if with_dz and res else None
+        sums = [torch.zeros(C, device=dev) for _ in range(3)] if with_sums else [None] * 3
+        mnn.bn_act_bwd(dy, y, z, M, C, relu, scale, mean, rstd, dz, dres, *sums)
+        torch.cuda.synchronize()
+        return dz, dres, sums
+
+    dz, dres, sums = run(True, True)
+    g = dy.double() * ((y > 0).double() if relu else 1.0)
+    xhat = (z.double() - mean.double()) * rstd.double()
+    close(dz, g * scale.double())
+    if res:
+        close(dres, g)
+    close(sums[0], g.sum(0))
+    close(sums[1], (g * xhat).sum(0))
+    close(sums[2], (g * scale.double()).sum(0))
+    dz1, dres1, _ = run(True, False)
+    _, _, sums2 = run(False, True)
+    assert torch.equal(dz1, dz) and (not res or torch.equal(dres1, dres))
+    assert all(torch.equal(a, b) for a, b in zip(sums2, sums))
