@@ -272,6 +272,37 @@ __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t
     st4(dst, v);
 }
 
+// epi_store4 of a simple (y row == m) store whose same-shape residual
+// (res_mode 1, no accumulate) or accumulated destination (res_mode 0) was loaded beforehand
+// into `pre` -- the epilogue issues all of a thread's loads before its first
+// store (the res / y pointers may alias, so the compiler cannot hoist a load
+// over an earlier store: one HBM round trip per float4 otherwise).
+__device__ __forceinline__ void epi_store4_pre(const ConvP& p, const Epi& e, int64_t m, int n, float4 v,
+                                               const float4& pre) {
+    const int64_t zrow = m * p.N + n;
+    if (e.bias) {
+        const float4 bb = ld4(e.bias + n);
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+    }
+    if (e.z) st4(e.z + zrow, v);
+    if (e.scale) {
+        const float4 sc = ld4(e.scale + n), sh = ld4(e.shift + n);
+        v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
+        v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
+    }
+    if (e.res_mode == 1) {
+        v.x += pre.x; v.y += pre.y; v.z += pre.z; v.w += pre.w;
+    }
+    if (e.relu) {
+        v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
+    }
+    float* dst = e.y + m * e.ldy + n;
+    if (e.accumulate) {      // (res_mode 0 here: pre holds the old destination)
+        v.x += pre.x; v.y += pre.y; v.z += pre.z; v.w += pre.w;
+    }
+    st4(dst, v);
+}
+
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
@@ -514,7 +545,13 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
         }
     };
 
-    const int nk = (p.K + BK - 1) / BK;
+#ifndef M3D_EPI_PREFETCH
+#define M3D_EPI_PREFETCH 1   // 0: the epilogue loads its residual / accumulated rows one store at a time
+#endif
+#ifndef M3D_CONV_DBG
+#define M3D_CONV_DBG 0   // timing probes (debug builds): 1 no epilogue, 2 no k-loop (epilogue only)
+#endif
+    const int nk = M3D_CONV_DBG == 2 ? 0 : (p.K + BK - 1) / BK;
     const int h = lane >> 5, l32 = lane & 31;
     load_tile(0);
     store_tile(0);
@@ -626,6 +663,19 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     // PERSIST: once the accumulators are staged in LDS (acc dead), map the
     // next tile and put its first k-tile loads in flight behind this tile's
     // global epilogue stores.
+#if M3D_CONV_DBG == 1
+    if constexpr (!PERSIST) {
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        if (t == 1.2345f) e.y[0] = t;
+        return;
+    }
+#endif
     const int64_t m0c = m0;
     const int n0c = n0;
     const int64_t Ln = L + Lstep;
@@ -637,6 +687,10 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     static_assert(HALVES == 1 || (TM * 32) % HR == 0 || HR % (TM * 32) == 0, "wave rows vs halves");
     float* Ts = smem;
     constexpr int C4T = BN / 4;
+    constexpr int QN = (HR * C4T + 255) / 256;
+    // residual / accumulated-destination rows loaded before the staging (block-uniform)
+    const bool pf = !PERSIST && M3D_EPI_PREFETCH && e.simple && e.split <= 0 && !(e.ldy & 3) &&
+                    ((e.res_mode == 1 && !e.accumulate) || (e.res_mode == 0 && e.accumulate));
     for (int hf = 0; hf < HALVES; ++hf) {
         if (hf) __syncthreads();                 // previous half fully read
         if ((wm * TM * 32) / HR == hf) {
@@ -659,19 +713,41 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
             setup_rows();
             load_tile(0);
         }
+        // PB float4 per thread per batch: with pf, the batch's residual /
+        // destination loads are all issued before its first store
+        constexpr int PB = QN < 4 ? QN : 4;
+        static_assert(QN % PB == 0, "epilogue batches");
 #pragma unroll
-        for (int q = 0; q < (HR * C4T + 255) / 256; ++q) {
-            const int idx = tid + 256 * q;
-            if (HR * C4T % 256 && idx >= HR * C4T) break;
-            const int row = idx / C4T, c4 = idx % C4T;
-            const int64_t m = m0c + hf * HR + row;
-            const int n = n0c + c4 * 4;
-            if (m < p.M && n < p.N) {
-                const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
-                if (PERSIST)   // plain C store (host-checked: simple epilogue, nothing fused)
-                    st4(e.y + m * e.ldy + n, v);
-                else
-                    epi_store4(p, e, m, n, v);
+        for (int q0 = 0; q0 < QN; q0 += PB) {
+            float4 pre[PB];
+            if (pf) {
+                const float* src = e.res_mode == 1 ? e.res : e.y;
+#pragma unroll
+                for (int u = 0; u < PB; ++u) {
+                    const int idx = tid + 256 * (q0 + u);
+                    const int row = idx / C4T, c4 = idx % C4T;
+                    const int64_t m = m0c + hf * HR + row;
+                    const int n = n0c + c4 * 4;
+                    pre[u] = (idx < HR * C4T && m < p.M && n < p.N) ? ld4(src + m * e.ldy + n)
+                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+                const int idx = tid + 256 * (q0 + u);
+                if (HR * C4T % 256 && idx >= HR * C4T) break;
+                const int row = idx / C4T, c4 = idx % C4T;
+                const int64_t m = m0c + hf * HR + row;
+                const int n = n0c + c4 * 4;
+                if (m < p.M && n < p.N) {
+                    const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
+                    if (PERSIST)   // plain C store (host-checked: simple epilogue, nothing fused)
+                        st4(e.y + m * e.ldy + n, v);
+                    else if (pf)
+                        epi_store4_pre(p, e, m, n, v, pre[u]);
+                    else
+                        epi_store4(p, e, m, n, v);
+                }
             }
         }
         e.y = y_next;
