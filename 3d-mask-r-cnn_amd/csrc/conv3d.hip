@@ -395,7 +395,9 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
             }
         }
         rsA = make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
-        rsB = make_rsrc(p.w, (uint64_t)p.K * p.N * 4);
+        // BT rows are (tap, n) of p.C channels; a split-K slice (p.K < taps * p.C) reads a
+        // channel window of every row, so the range is the whole weight
+        rsB = make_rsrc(p.w, BT ? (uint64_t)ntaps * p.N * p.C * 4 : (uint64_t)p.K * p.N * 4);
     };
     setup_rows();
 
@@ -735,11 +737,10 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
 #pragma unroll
             for (int u = 0; u < PB; ++u) {
                 const int idx = tid + 256 * (q0 + u);
-                if (HR * C4T % 256 && idx >= HR * C4T) break;
                 const int row = idx / C4T, c4 = idx % C4T;
                 const int64_t m = m0c + hf * HR + row;
                 const int n = n0c + c4 * 4;
-                if (m < p.M && n < p.N) {
+                if ((HR * C4T % 256 == 0 || idx < HR * C4T) && m < p.M && n < p.N) {
                     const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
                     if (PERSIST)   // plain C store (host-checked: simple epilogue, nothing fused)
                         st4(e.y + m * e.ldy + n, v);
@@ -2899,6 +2900,137 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
     p.M = (int64_t)p.B * p.OH * p.OW * p.OD;
     dispatch_gemm<true, true>(p, e, st(s));
     return check_launch("conv_gemm_kernel(bwd-data)");
+}
+
+// ---- split-K form of the 1x1x1 direct convs whose tiles do not fill the chip --
+// The deep stages' 1x1x1 convs have few output rows (res5: 2048 voxels at
+// 128^3), so their 128x128 output tiles occupy a quarter of the CUs, each
+// walking K = Cin (up to 2048) alone.  Split-K: `splits` K-slices run as the
+// batch of one launch (the slice's channels are an offset into the rows of x /
+// dz and of w), each writing its partial tile plainly into the workspace; one
+// reduce kernel sums the slices in slice order (deterministic) and applies the
+// conv's epilogue (bias, z, BN, residual, ReLU, strided or accumulated store)
+// through the same epi_store4 as the one-pass kernel.
+__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict__ ws, int splits,
+                                                         ConvP p, Epi e) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int N4 = p.N >> 2;
+    if (i >= p.M * N4) return;
+    const int64_t m = i / N4;
+    const int n = (int)(i - m * N4) * 4;
+    const int64_t plane = p.M * p.N;
+    float4 v = ld4(ws + m * p.N + n);
+    for (int z = 1; z < splits; ++z) {
+        const float4 t = ld4(ws + z * plane + m * p.N + n);
+        v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+    }
+    epi_store4(p, e, m, n, v);
+}
+
+// K-slices for a 1x1x1 conv GEMM of M rows, reduction K, N columns (1: no split).
+// Only where the 128x128 tiles leave CUs idle AND each walks a long K (>= 1024),
+// or the tiles are very few (<= 32); doubled while the tiles times the slices
+// stay under two per CU and a slice keeps >= 128 channels (4 k-tiles).
+// Measured per layer at 128^3 (scripts/conv_layers.py): res5 2048 -> 512
+// 117 -> 67 us, the P5 lateral 2048 -> 256 106 -> 39 us; K = 512 with 128-256
+// tiles lost 10-25 % (the extra partial-sum traffic, no idle CUs to gain).
+static int splitk_count(int64_t M, int64_t K, int64_t N) {
+    if (N % 4 || K % 32) return 1;
+    const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    if (tiles >= num_cus() || (K < 1024 && tiles > 32)) return 1;
+    int s = 1;
+    while (s < 8 && tiles * s < 2 * num_cus() && K % (64 * s) == 0 && K / (2 * s) >= 128) s *= 2;
+    return s;
+}
+
+extern "C" int32_t m3d_conv3d_splitk_count(int64_t M, int64_t K, int64_t N) {
+    if (M <= 0 || K <= 0 || N <= 0) return 1;
+    return splitk_count(M, K, N);
+}
+
+// fwd: x [B,H,W,D,Cin] (strided rows), w [Cin][Cout]; the epilogue of m3d_conv3d_fwd
+extern "C" int m3d_conv3d_fwd_splitk(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                                     const float* w, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
+                                     int32_t sy, int32_t sx, int32_t sz, const float* bias, const float* bn_scale,
+                                     const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,
+                                     float* z_out, float* y, int32_t splits, void* workspace, size_t ws_bytes,
+                                     m3d_stream_t s) {
+    const int64_t M = B * OH * OW * OD;
+    if (splits <= 1 || per_item(B, H * W * D, Cin, OH * OW * OD, Cout))
+        return m3d_conv3d_fwd(x, B, H, W, D, Cin, w, 1, 1, 1, Cout, OH, OW, OD, sy, sx, sz, 0, 0, 0, bias,
+                              bn_scale, bn_shift, residual, res_mode, relu, z_out, y, Cout, nullptr, 0, 0, s);
+    int rc = conv_check(B, H, W, D, Cin, 1, 1, 1, Cout, OH, OW, OD, sy, sx, sz);
+    if (rc) return rc;
+    if ((bn_scale == nullptr) != (bn_shift == nullptr))
+        return einval("conv3d: bn_scale and bn_shift must be given together");
+    if (res_mode < 0 || res_mode > 3) return einval("conv3d: res_mode must be 0..3");
+    if (relu < 0 || relu > 2) return einval("conv3d: activation must be 0 (none), 1 (relu), 2 (sigmoid)");
+    if (res_mode != 0 && residual == nullptr) return einval("conv3d: residual missing");
+    if (res_mode == 2 && ((OH & 1) || (OW & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
+    if (splits > 64 || Cin % (32 * splits)) return einval("conv3d split-K: Cin must be a multiple of 32 * splits");
+    if (!workspace || ws_bytes < sizeof(float) * (size_t)splits * (size_t)M * (size_t)Cout)
+        return einval("conv3d split-K: workspace smaller than splits * M * Cout floats");
+    const int sp = splits;
+    const int64_t slice = Cin / sp;
+    float* part = static_cast<float*>(workspace);
+    // the K-slices as the batch: channel offset into x's rows and w's rows
+    ConvP q{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, 1, 1, 1,
+            sy, sx, sz, 0, 0, 0, M, (int)slice, w, (int)Cout, 0, slice, slice * Cout, M * Cout};
+    Epi pe{};
+    pe.y = part; pe.ldy = Cout; pe.simple = 1; pe.YH = (int)OH; pe.YW = (int)OW; pe.YD = (int)OD;
+    pe.ysy = pe.ysx = pe.ysz = 1;
+    dispatch_gemm<false, true>(q, pe, st(s), sp);
+    rc = check_launch("conv_gemm_kernel(fwd split-K)");
+    if (rc) return rc;
+    ConvP p{x, (int)B, (int)H, (int)W, (int)D, (int)Cin, (int)OH, (int)OW, (int)OD, 1, 1, 1,
+            sy, sx, sz, 0, 0, 0, M, (int)Cin, w, (int)Cout, 0, 0, 0, 0};
+    Epi e{bias, bn_scale, bn_shift, residual, res_mode, relu, z_out, y, Cout,
+          nullptr, 0, 0, (int)OH, (int)OW, (int)OD, 1, 1, 1, 0, 1};
+    hipLaunchKernelGGL(splitk_epi_kernel, dim3(grid_for(M * Cout / 4, 256)), dim3(256), 0, st(s), part, sp, p, e);
+    return check_launch("splitk_epi_kernel(fwd)");
+}
+
+// bwd-data of a 1x1x1 conv: dx (+)= dz w^T, dz [B,OH,OW,OD,Cout]; the store of m3d_conv3d_bwd_data
+extern "C" int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                          int64_t D, int64_t Cin, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
+                                          int32_t sy, int32_t sx, int32_t sz, float* dx, int32_t accumulate,
+                                          int32_t splits, void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    const int64_t M = B * OH * OW * OD;
+    if (splits <= 1 || per_item(B, H * W * D, Cin, OH * OW * OD, Cout))
+        return m3d_conv3d_bwd_data(dz, w, B, H, W, D, Cin, 1, 1, 1, Cout, OH, OW, OD, sy, sx, sz, 0, 0, 0, dx,
+                                   accumulate, s);
+    int rc = conv_check(B, H, W, D, Cin, 1, 1, 1, Cout, OH, OW, OD, sy, sx, sz);
+    if (rc) return rc;
+    if (Cout % 32) return einval("conv3d bwd-data: Cout must be a multiple of 32");
+    if (Cin % 4) return einval("conv3d bwd-data: Cin must be a multiple of 4");
+    if (splits > 64 || Cout % (32 * splits)) return einval("conv3d split-K: Cout must be a multiple of 32 * splits");
+    if (!workspace || ws_bytes < sizeof(float) * (size_t)splits * (size_t)M * (size_t)Cin)
+        return einval("conv3d split-K: workspace smaller than splits * M * Cin floats");
+    const int sp = splits;
+    const int64_t slice = Cout / sp;
+    float* part = static_cast<float*>(workspace);
+    // M grid = dz grid; B(k = c', n) = w[n][c'] (Keras [Cin][Cout]), slice = channel offset of dz and w
+    ConvP q{};
+    q.a = dz; q.B = (int)B; q.H = (int)OH; q.W = (int)OW; q.D = (int)OD; q.C = (int)Cout;
+    q.OH = (int)OH; q.OW = (int)OW; q.OD = (int)OD;
+    q.kh = q.kw = q.kd = 1; q.sy = q.sx = q.sz = 1;
+    q.M = M; q.K = (int)slice; q.w = w; q.N = (int)Cin; q.flip = 1;
+    q.bsa = slice; q.bsw = slice; q.bsy = M * Cin;
+    Epi pe{};
+    pe.y = part; pe.ldy = Cin; pe.simple = 1; pe.YH = (int)OH; pe.YW = (int)OW; pe.YD = (int)OD;
+    pe.ysy = pe.ysx = pe.ysz = 1;
+    dispatch_gemm<true, true>(q, pe, st(s), sp);
+    rc = check_launch("conv_gemm_kernel(bwd-data split-K)");
+    if (rc) return rc;
+    ConvP p = q;
+    p.K = (int)Cout; p.bsa = p.bsw = p.bsy = 0;
+    Epi e{};
+    e.y = dx; e.ldy = Cin; e.accumulate = accumulate;
+    e.YH = (int)H; e.YW = (int)W; e.YD = (int)D;
+    e.ysy = sy; e.ysx = sx; e.ysz = sz;
+    e.simple = (sy == 1 && sx == 1 && sz == 1 && H == OH && W == OW && D == OD);
+    hipLaunchKernelGGL(splitk_epi_kernel, dim3(grid_for(M * Cin / 4, 256)), dim3(256), 0, st(s), part, sp, p, e);
+    return check_launch("splitk_epi_kernel(bwd-data)");
 }
 
 extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,

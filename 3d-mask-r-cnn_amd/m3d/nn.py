@@ -92,6 +92,9 @@ def _L():
 # halo-extended copy of every z-window input instead (torch.cat, the old path)
 SLAB_HALO_PLANES = os.environ.get("M3D_SLAB_HALO_PLANES", "1") != "0"
 
+# split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
+SPLITK = os.environ.get("M3D_SPLITK", "1") != "0"
+
 # Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
 WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
 WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
@@ -110,6 +113,20 @@ def use_winograd(geo, cin, cout, in_sp):
             and tuple(geo.out[:2]) == tuple(in_sp[:2]) and geo.pad[2] in (0, 1)
             and 0 <= in_sp[2] - geo.out[2] <= 2
             and cin % 32 == 0 and cout % 32 == 0 and min(cin, cout) >= WINO_MIN_C)
+
+
+def _splitk(xshape, geo, cin, cout, bwd_data):
+    """K-slices of the split-K form of a 1x1x1 conv (m3d_conv3d_splitk_count; 1: one pass).
+    Under depth-slab sharding the count is the whole volume's (depth is never
+    strided), so every slab sums its K slices exactly as the unsharded run."""
+    if geo.k != (1, 1, 1) or geo.pad != (0, 0, 0) or not SPLITK:
+        return 1
+    B, (OH, OW, OD) = xshape[0], geo.out
+    sg = slab.current()
+    if sg is not None:
+        OD = sg.D
+    K, N = (cout, cin) if bwd_data else (cin, cout)
+    return int(_L().m3d_conv3d_splitk_count(B * OH * OW * OD, K, N))
 
 
 def _wino_ws(B, H, W, D, OD, cin, cout, dev):
@@ -273,10 +290,18 @@ class _ConvBNAct(torch.autograd.Function):
                                                ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
                                                ptr(ws), wsb, stream()), "conv3d_fwd_wino")
         else:
-            check(_L().m3d_conv3d_fwd(ptr(x), *x.shape, ptr(w), *geo.k, Cout, OH, OW, OD,
-                                      *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
-                                      ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
-                                      None, 0, 0, stream()), "conv3d_fwd")
+            nsk = _splitk(x.shape, geo, Cin, Cout, 0)
+            if nsk > 1:
+                wsk = torch.empty((nsk, y.numel()), device=x.device, dtype=torch.float32)
+                check(_L().m3d_conv3d_fwd_splitk(ptr(x), *x.shape, ptr(w), Cout, OH, OW, OD, *geo.stride,
+                                                 ptr(b), ptr(scale), ptr(shift), ptr(residual), res_mode,
+                                                 1 if relu else 0, ptr(z), ptr(y), nsk, ptr(wsk),
+                                                 wsk.numel() * 4, stream()), "conv3d_fwd_splitk")
+            else:
+                check(_L().m3d_conv3d_fwd(ptr(x), *x.shape, ptr(w), *geo.k, Cout, OH, OW, OD,
+                                          *geo.stride, *geo.pad, ptr(b), ptr(scale), ptr(shift),
+                                          ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y), Cout,
+                                          None, 0, 0, stream()), "conv3d_fwd")
         if LAYER_LOG is not None:
             direct = 2.0 * (y.numel() // Cout) * kh * kw * kd * Cin * Cout
             exe = direct
@@ -400,9 +425,16 @@ class _ConvBNAct(torch.autograd.Function):
                 wd[..., :Cout] = w
                 dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
                 dzd[..., :Cout] = dz
-            check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
-                                        OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
-                  "conv3d_bwd_data")
+            nsk = _splitk(x.shape, geo, Cin, cpad, 1)
+            if nsk > 1:
+                wsk = torch.empty((nsk, M * Cin), device=x.device, dtype=torch.float32)
+                check(L.m3d_conv3d_bwd_data_splitk(ptr(dzd), ptr(wd), B, H, W, D, Cin, cpad, OH, OW, OD,
+                                                   *geo.stride, ptr(dx), acc, nsk, ptr(wsk), wsk.numel() * 4,
+                                                   stream()), "conv3d_bwd_data_splitk")
+            else:
+                check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
+                                            OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
+                      "conv3d_bwd_data")
             dx = _link_park(link, dx, acc)
         _grad_done(grads, side)
         dr = None

@@ -179,6 +179,27 @@ int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, int64_t H, i
                         int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
                         int32_t py, int32_t px, int32_t pz, float* dx, int32_t accumulate,
                         m3d_stream_t s);
+/* Split-K forms of the 1x1x1 convs whose output tiles do not fill the chip
+ * (deep stages: few voxels, Cin up to 2048).  m3d_conv3d_splitk_count gives
+ * the K-slices for a GEMM of M output rows, reduction K and N columns (1: one
+ * pass); the caller passes `splits` (so a depth slab can use the count of the
+ * whole volume and stay bit-identical to it) and a workspace of
+ * splits * M * N floats (M = B*OH*OW*OD; N = Cout fwd, Cin bwd-data).  The
+ * K-slices are summed in slice order (deterministic) and the conv's epilogue
+ * applied once: the result equals m3d_conv3d_fwd / _bwd_data up to the order
+ * of the K sum.  splits <= 1 runs the one-pass kernels.  Conv3D(1,1,1) of
+ * core/models.py (a TF builtin in the reference). */
+int32_t m3d_conv3d_splitk_count(int64_t M, int64_t K, int64_t N);
+int m3d_conv3d_fwd_splitk(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                          const float* w, int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
+                          int32_t sx, int32_t sz, const float* bias, const float* bn_scale,
+                          const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,
+                          float* z_out, float* y, int32_t splits, void* workspace, size_t ws_bytes,
+                          m3d_stream_t s);
+int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                               int64_t Cin, int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
+                               int32_t sx, int32_t sz, float* dx, int32_t accumulate, int32_t splits,
+                               void* workspace, size_t ws_bytes, m3d_stream_t s);
 int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
                           int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd,
                           int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,

@@ -386,3 +386,62 @@ def test_bn_act_bwd_modes(relu, res):
     _, _, sums2 = run(False, True)
     assert torch.equal(dz1, dz) and (not res or torch.equal(dres1, dres))
     assert all(torch.equal(a, b) for a, b in zip(sums2, sums))
+
+
+@pytest.mark.parametrize("shape,cout,stride,res,acc", [
+    ((1, 4, 4, 16, 1024), 512, (1, 1, 1), True, 0),      # res5-like: 32 rows of tiles, K = 1024
+    ((1, 8, 8, 16, 512), 256, (2, 2, 1), False, 1),      # strided shortcut, accumulated dgrad
+])
+def test_splitk_1x1_matches_one_pass(cuda, shape, cout, stride, res, acc):
+    """m3d_conv3d_fwd_splitk / _bwd_data_splitk (K-slices summed in slice order,
+    then the full epilogue: bias, z, BN, residual, ReLU; strided and accumulated
+    stores) against the one-pass kernels, within the f32 summation-order bound."""
+    from m3d import _lib
+    L = _lib.load()
+    torch.manual_seed(3)
+    assert L.m3d_conv3d_splitk_count(1 << 20, 1024, 512) == 1     # enough tiles: one pass
+    B, H, W, D, Cin = shape
+    OH, OW, OD = -(-H // stride[0]), -(-W // stride[1]), -(-D // stride[2])
+    M = B * OH * OW * OD
+    sp = L.m3d_conv3d_splitk_count(M, Cin, cout)
+    assert sp > 1, "shape expected to take the split-K path"
+    x = torch.randn(shape, device=cuda)
+    w = torch.randn((1, 1, 1, Cin, cout), device=cuda) / Cin ** 0.5
+    b, sc, sh = torch.randn(cout, device=cuda), torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
+    r = torch.randn((B, OH, OW, OD, cout), device=cuda) if res else None
+    outs = []
+    for split in (False, True):
+        y = torch.empty((B, OH, OW, OD, cout), device=cuda)
+        z = torch.empty_like(y)
+        p = _lib.ptr
+        if split:
+            ws = torch.empty(sp * M * cout, device=cuda)
+            _lib.check(L.m3d_conv3d_fwd_splitk(p(x), *shape, p(w), cout, OH, OW, OD, *stride, p(b), p(sc), p(sh),
+                                               p(r), 1 if res else 0, 1, p(z), p(y), sp, p(ws), ws.numel() * 4,
+                                               _lib.stream()), "fwd")
+        else:
+            _lib.check(L.m3d_conv3d_fwd(p(x), *shape, p(w), 1, 1, 1, cout, OH, OW, OD, *stride, 0, 0, 0, p(b),
+                                        p(sc), p(sh), p(r), 1 if res else 0, 1, p(z), p(y), cout, None, 0, 0,
+                                        _lib.stream()), "fwd")
+        outs.append((y, z))
+    close(outs[1][0], outs[0][0], 1e-5)
+    close(outs[1][1], outs[0][1], 1e-5)
+    # data gradient: dx (+)= conv^T dz, strided scatter / accumulate
+    dz = torch.randn((B, OH, OW, OD, cout), device=cuda)
+    spd = L.m3d_conv3d_splitk_count(M, cout, Cin)
+    dxs = []
+    for split in (False, True):
+        dx = torch.randn(shape, device=cuda) if acc else torch.zeros(shape, device=cuda)
+        if acc:
+            torch.manual_seed(9)
+            dx = torch.randn(shape, device=cuda)
+        p = _lib.ptr
+        if split and spd > 1:
+            ws = torch.empty(spd * M * Cin, device=cuda)
+            _lib.check(L.m3d_conv3d_bwd_data_splitk(p(dz), p(w), B, H, W, D, Cin, cout, OH, OW, OD, *stride, p(dx),
+                                                    acc, spd, p(ws), ws.numel() * 4, _lib.stream()), "bwd_data")
+        else:
+            _lib.check(L.m3d_conv3d_bwd_data(p(dz), p(w), B, H, W, D, Cin, 1, 1, 1, cout, OH, OW, OD, *stride,
+                                             0, 0, 0, p(dx), acc, _lib.stream()), "bwd_data")
+        dxs.append(dx)
+    close(dxs[1], dxs[0], 1e-5)
