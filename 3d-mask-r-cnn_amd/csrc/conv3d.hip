@@ -2911,7 +2911,7 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
 // reduce kernel sums the slices in slice order (deterministic) and applies the
 // conv's epilogue (bias, z, BN, residual, ReLU, strided or accumulated store)
 // through the same epi_store4 as the one-pass kernel.
-__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict__ ws, int splits,
+__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* ws, int splits,   // (may be e.y: in place)
                                                          ConvP p, Epi e) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int N4 = p.N >> 2;
@@ -3281,6 +3281,90 @@ extern "C" int m3d_gemm_x3_af(const float* A, const uint16_t* B3, float* C, int6
     return check_launch("m3d_gemm_x3_af");
 }
 
+
+// ---- 1x1x1 stride-1 convs as one GEMM on the exact bf16 split --------------
+// The big-K 1x1x1 convs at the finest level (rpn_conv_shared2 512 -> 256, the
+// P2 lateral 256 -> 256 and their data gradients) are f32-MFMA-bound in the
+// direct kernel; as a GEMM rows = voxels, A = x (or dz) rows of K fp32
+// channels split in registers, B = the weight as split planes, they run on
+// x3_gemm256_af_kernel, the conv epilogue applied by a second pass.
+// planes[p][n][k] = split3_p(w[k][n]) (transpose = 1: the forward, K = Cin,
+// N = Cout) or split3_p(w[n][k]) (transpose = 0: the data gradient, N = Cin,
+// K = Cout); w is the Keras [Cin][Cout] kernel.
+__global__ __launch_bounds__(256) void x3_wplanes_kernel(const float* __restrict__ w, int Cin, int Cout,
+                                                         int transpose, unsigned short* __restrict__ pl) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_el = (int64_t)Cin * Cout;
+    if (i >= n_el) return;
+    const int c = (int)(i / Cout), o = (int)(i % Cout);   // w[c][o]
+    uint32_t h, m, l;
+    split3(w[i], h, m, l);
+    const int64_t at = transpose ? (int64_t)o * Cin + c : i;
+    pl[at] = (unsigned short)h;
+    pl[n_el + at] = (unsigned short)m;
+    pl[2 * n_el + at] = (unsigned short)l;
+}
+
+extern "C" int m3d_conv1_x3_planes(const float* w, int64_t Cin, int64_t Cout, int32_t transpose, uint16_t* planes,
+                                   m3d_stream_t s) {
+    if (Cin <= 0 || Cout <= 0 || !w || !planes) return einval("conv1_x3_planes: bad arguments");
+    hipLaunchKernelGGL(x3_wplanes_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, st(s), w, (int)Cin,
+                       (int)Cout, transpose ? 1 : 0, reinterpret_cast<unsigned short*>(planes));
+    return check_launch("x3_wplanes_kernel");
+}
+
+// the GEMM on x3_gemm256_af_kernel (plain C = out [M][N]), then -- when the
+// conv has an epilogue -- splitk_epi_kernel over `out` in place (one slice):
+// each element read once and rewritten through epi_store4.  (The epilogue
+// inside the GEMM kernel spilled: its 222 VGPRs leave no room.)
+static int conv1_x3_launch(const float* a, const uint16_t* planes, int64_t M, int64_t K, int64_t N, int64_t H,
+                           int64_t W, int64_t D, float* out, const Epi* e, hipStream_t s) {
+    if (M <= 0 || K <= 0 || N <= 0) return einval("conv1 x3: dimensions must be positive");
+    if (K % 32 || N % 256) return einval("conv1 x3: K must be a multiple of 32 and N of 256");
+    if (M > 0x7FFFFFFF || M * K >= op_lim() || M * N >= op_lim() || N * K * 2 >= 0xFFFFFFF0LL)
+        return einval("conv1 x3: operand larger than 4 GiB (32-bit buffer offsets)");
+    X3G q{};
+    q.af = a;
+    q.b = reinterpret_cast<const unsigned short*>(planes);
+    q.c = out;
+    q.M = M; q.K = (int)K; q.N = (int)N; q.nbatch = 1;
+    q.psb = K * N;
+    const int64_t t256 = ((M + 255) / 256) * (N / 256);
+    const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
+    hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
+    int rc = check_launch("x3_gemm256_af_kernel(conv1)");
+    if (rc || !e) return rc;
+    ConvP p{};
+    p.M = M; p.N = (int)N; p.K = (int)K; p.OH = (int)H; p.OW = (int)W; p.OD = (int)D;
+    hipLaunchKernelGGL(splitk_epi_kernel, dim3(grid_for(M * N / 4, 256)), dim3(256), 0, s, out, 1, p, *e);
+    return check_launch("splitk_epi_kernel(conv1 x3)");
+}
+
+extern "C" int m3d_conv3d_fwd_x3(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                                 const uint16_t* planes, int64_t Cout, const float* bias, const float* bn_scale,
+                                 const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,
+                                 float* z_out, float* y, m3d_stream_t s) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0) return einval("conv3d x3: tensor dimensions must be positive");
+    if ((bn_scale == nullptr) != (bn_shift == nullptr))
+        return einval("conv3d: bn_scale and bn_shift must be given together");
+    if (res_mode < 0 || res_mode > 2) return einval("conv3d x3: res_mode must be 0..2");
+    if (relu < 0 || relu > 2) return einval("conv3d: activation must be 0 (none), 1 (relu), 2 (sigmoid)");
+    if (res_mode != 0 && residual == nullptr) return einval("conv3d: residual missing");
+    if (res_mode == 2 && ((H & 1) || (W & 1))) return einval("conv3d: upsampled residual needs even OH/OW");
+    Epi e{};
+    e.bias = bias; e.scale = bn_scale; e.shift = bn_shift; e.res = residual; e.res_mode = res_mode;
+    e.relu = relu; e.z = z_out; e.y = y; e.ldy = Cout; e.simple = 1;
+    e.YH = (int)H; e.YW = (int)W; e.YD = (int)D; e.ysy = e.ysx = e.ysz = 1;
+    const bool plain = !bias && !bn_scale && !residual && !relu && !z_out;
+    return conv1_x3_launch(x, planes, B * H * W * D, Cin, Cout, H, W, D, y, plain ? nullptr : &e, st(s));
+}
+
+// dx = dz w^T (accumulate = 0 only: the GEMM's plain store)
+extern "C" int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W,
+                                      int64_t D, int64_t Cin, int64_t Cout, float* dx, m3d_stream_t s) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0) return einval("conv3d x3: tensor dimensions must be positive");
+    return conv1_x3_launch(dz, planes, B * H * W * D, Cout, Cin, H, W, D, dx, nullptr, st(s));
+}
 
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
     if (wino_nz() != wino_wgrad_nz()) return 0;       // forward tiles differ from the wgrad's: nothing to keep

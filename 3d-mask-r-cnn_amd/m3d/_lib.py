@@ -54,6 +54,10 @@ _SIGS = {
                               c_i32, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_data_splitk": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                    c_i32, c_i32, c_i32, c_p, c_i32, c_i32, c_p, c_sz, c_p],
+    "m3d_conv1_x3_planes": [c_p, c_i64, c_i64, c_i32, c_p, c_p],
+    "m3d_conv3d_fwd_x3": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_i32,
+                          c_p, c_p, c_p],
+    "m3d_conv3d_bwd_data_x3": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_conv3d_bwd_data": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
                             c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                             c_p, c_i32, c_p],

@@ -92,6 +92,8 @@ def _L():
 # halo-extended copy of every z-window input instead (torch.cat, the old path)
 SLAB_HALO_PLANES = os.environ.get("M3D_SLAB_HALO_PLANES", "1") != "0"
 
+# big-K 1x1x1 stride-1 convs on the bf16-split GEMM (M3D_CONV1_X3=0: the f32 direct kernel)
+CONV1_X3 = os.environ.get("M3D_CONV1_X3", "1") != "0"
 # split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
 SPLITK = os.environ.get("M3D_SPLITK", "1") != "0"
 
@@ -127,6 +129,31 @@ def _splitk(xshape, geo, cin, cout, bwd_data):
         OD = sg.D
     K, N = (cout, cin) if bwd_data else (cin, cout)
     return int(_L().m3d_conv3d_splitk_count(B * OH * OW * OD, K, N))
+
+
+def _conv1_x3(xshape, geo, K, N):
+    """Run a 1x1x1 stride-1 conv (forward: K = Cin, N = Cout; data gradient:
+    K = Cout, N = Cin) as one GEMM on the exact bf16 split (m3d_conv3d_fwd_x3 /
+    _bwd_data_x3)?  Only the big-K convs whose 256x256 tiles fill the chip
+    (rpn_conv_shared2 and the lateral at P2; the other 1x1x1 convs are bound by
+    their epilogue or a short K, where the split costs more than it saves).
+    The choice uses the whole volume's depth under depth-slab sharding, so
+    every slab runs the same kernel as the unsharded volume."""
+    if not CONV1_X3 or geo.k != (1, 1, 1) or geo.stride != (1, 1, 1) or geo.pad != (0, 0, 0):
+        return False
+    B, H, W, D = xshape[:4]
+    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < 256:
+        return False
+    sg = slab.current()
+    Dg = sg.D if sg is not None else D
+    return -(-B * H * W * Dg // 256) * (N // 256) >= 256
+
+
+def _x3_planes(w, cin, cout, transpose):
+    planes = torch.empty(3 * cin * cout, device=w.device, dtype=torch.int16)
+    check(_L().m3d_conv1_x3_planes(ptr(w), cin, cout, 1 if transpose else 0, ptr(planes), stream()),
+          "conv1_x3_planes")
+    return planes
 
 
 def _wino_ws(B, H, W, D, OD, cin, cout, dev):
@@ -289,6 +316,11 @@ class _ConvBNAct(torch.autograd.Function):
                                                ptr(b), ptr(scale),
                                                ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
                                                ptr(ws), wsb, stream()), "conv3d_fwd_wino")
+        elif res_mode <= 2 and _conv1_x3(x.shape, geo, Cin, Cout):
+            planes = _x3_planes(w, Cin, Cout, True)
+            check(_L().m3d_conv3d_fwd_x3(ptr(x), B, H, W, D, Cin, ptr(planes), Cout, ptr(b), ptr(scale),
+                                         ptr(shift), ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y),
+                                         stream()), "conv3d_fwd_x3")
         else:
             nsk = _splitk(x.shape, geo, Cin, Cout, 0)
             if nsk > 1:
@@ -426,7 +458,11 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
-            if nsk > 1:
+            if cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin):
+                planes = _x3_planes(w, Cin, Cout, False)
+                check(L.m3d_conv3d_bwd_data_x3(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), stream()),
+                      "conv3d_bwd_data_x3")
+            elif nsk > 1:
                 wsk = torch.empty((nsk, M * Cin), device=x.device, dtype=torch.float32)
                 check(L.m3d_conv3d_bwd_data_splitk(ptr(dzd), ptr(wd), B, H, W, D, Cin, cpad, OH, OW, OD,
                                                    *geo.stride, ptr(dx), acc, nsk, ptr(wsk), wsk.numel() * 4,

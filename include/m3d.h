@@ -200,6 +200,24 @@ int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64_t B, int64
                                int64_t Cin, int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
                                int32_t sx, int32_t sz, float* dx, int32_t accumulate, int32_t splits,
                                void* workspace, size_t ws_bytes, m3d_stream_t s);
+/* 1x1x1 stride-1 convs as one GEMM on the exact bf16 split (the big-K convs
+ * of the finest level: rpn_conv_shared2, the P2 lateral, their data
+ * gradients).  m3d_conv1_x3_planes splits the Keras kernel w [Cin][Cout] into
+ * planes uint16 [3][N][K] (transpose = 1: forward, N = Cout, K = Cin;
+ * transpose = 0: data gradient, N = Cin, K = Cout).  Then the forward (epilogue
+ * of m3d_conv3d_fwd: bias, z, BN, same-shape or (2,2,1)-upsampled residual,
+ * activation; applied by a second in-place pass over y) or the data gradient
+ * (dx = dz w^T, no accumulate).  K % 32 == 0, N % 256 == 0.
+ * Error vs fp64 at or below the f32 MFMA's (exact split, 6 bf16 MFMAs per
+ * product). */
+int m3d_conv1_x3_planes(const float* w, int64_t Cin, int64_t Cout, int32_t transpose, uint16_t* planes,
+                        m3d_stream_t s);
+int m3d_conv3d_fwd_x3(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                      const uint16_t* planes, int64_t Cout, const float* bias, const float* bn_scale,
+                      const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,
+                      float* z_out, float* y, m3d_stream_t s);
+int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
+                           int64_t Cin, int64_t Cout, float* dx, m3d_stream_t s);
 int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
                           int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd,
                           int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,

@@ -445,3 +445,49 @@ def test_splitk_1x1_matches_one_pass(cuda, shape, cout, stride, res, acc):
                                              0, 0, 0, p(dx), acc, _lib.stream()), "bwd_data")
         dxs.append(dx)
     close(dxs[1], dxs[0], 1e-5)
+
+
+@pytest.mark.parametrize("res_mode", [0, 1, 2])
+def test_conv1_x3_matches_direct(cuda, res_mode):
+    """1x1x1 stride-1 convs on the bf16-split GEMM (m3d_conv3d_fwd_x3 with the
+    conv epilogue: bias, z, BN, residual same-shape / (2,2,1)-upsampled, ReLU;
+    m3d_conv3d_bwd_data_x3) against the f32 direct
+    kernels and a float64 evaluation."""
+    from m3d import _lib
+    L = _lib.load()
+    p = _lib.ptr
+    torch.manual_seed(11 + res_mode)
+    B, H, W, D, Cin, Cout = 1, 16, 16, 64, 512, 256
+    x = torch.randn((B, H, W, D, Cin), device=cuda)
+    w = torch.randn((Cin, Cout), device=cuda) / Cin ** 0.5
+    b, sc, sh = torch.randn(Cout, device=cuda), torch.rand(Cout, device=cuda) + 0.5, torch.randn(Cout, device=cuda)
+    rshape = (B, H // 2, W // 2, D, Cout) if res_mode == 2 else (B, H, W, D, Cout)
+    r = torch.randn(rshape, device=cuda) if res_mode else None
+    planes = torch.empty(3 * Cin * Cout, device=cuda, dtype=torch.int16)
+    _lib.check(L.m3d_conv1_x3_planes(p(w), Cin, Cout, 1, p(planes), _lib.stream()), "planes")
+    y1, z1 = torch.empty((B, H, W, D, Cout), device=cuda), torch.empty((B, H, W, D, Cout), device=cuda)
+    _lib.check(L.m3d_conv3d_fwd_x3(p(x), B, H, W, D, Cin, p(planes), Cout, p(b), p(sc), p(sh), p(r), res_mode, 1,
+                                   p(z1), p(y1), _lib.stream()), "fwd_x3")
+    y0, z0 = torch.empty_like(y1), torch.empty_like(z1)
+    _lib.check(L.m3d_conv3d_fwd(p(x), B, H, W, D, Cin, p(w), 1, 1, 1, Cout, H, W, D, 1, 1, 1, 0, 0, 0, p(b), p(sc),
+                                p(sh), p(r), res_mode, 1, p(z0), p(y0), Cout, None, 0, 0, _lib.stream()), "fwd")
+    zr = x.double().reshape(-1, Cin) @ w.double() + b.double()
+    yr = zr * sc.double() + sh.double()
+    if res_mode == 1:
+        yr = yr + r.double().reshape(-1, Cout)
+    elif res_mode == 2:
+        up = r.double().repeat_interleave(2, 1).repeat_interleave(2, 2)
+        yr = yr + up.reshape(-1, Cout)
+    yr = torch.relu(yr)
+    close(z1.reshape(-1, Cout), zr)
+    close(y1.reshape(-1, Cout), yr)
+    close(y1, y0, 1e-5)
+    # data gradient: N = Cin, K = Cout
+    dz = torch.randn((B, H, W, D, Cout), device=cuda)
+    _lib.check(L.m3d_conv1_x3_planes(p(w), Cin, Cout, 0, p(planes), _lib.stream()), "planes_t")
+    d1, d0 = torch.full((B, H, W, D, Cin), 7.0, device=cuda), torch.empty((B, H, W, D, Cin), device=cuda)
+    _lib.check(L.m3d_conv3d_bwd_data_x3(p(dz), p(planes), B, H, W, D, Cin, Cout, p(d1), _lib.stream()), "bwd_x3")
+    _lib.check(L.m3d_conv3d_bwd_data(p(dz), p(w), B, H, W, D, Cin, 1, 1, 1, Cout, H, W, D, 1, 1, 1, 0, 0, 0,
+                                     p(d0), 0, _lib.stream()), "bwd")
+    close(d1.reshape(-1, Cin), dz.double().reshape(-1, Cout) @ w.double().t())
+    close(d1, d0, 1e-5)
