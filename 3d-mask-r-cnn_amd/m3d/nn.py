@@ -633,18 +633,22 @@ class _RPNOut(torch.autograd.Function):
             dlogits = torch.zeros((B, sum(rows) * apl, 2), device=dev)
         if dbbox is None:
             dbbox = torch.zeros((B, sum(rows) * apl, 6), device=dev)
-        w_pad = torch.zeros((Cin, npad), device=dev, dtype=torch.float32)
-        w_pad[:, :n_out] = w24.reshape(Cin, n_out)
+        w_pad = torch.nn.functional.pad(w24.reshape(Cin, n_out), (0, npad - n_out))
         dshared = [torch.empty_like(s) for s in shared]
         L = _L()
+        R = sum(rows)
         for b in range(B):
+            # all levels' output gradients as one [R, npad] matrix (row = voxel,
+            # level-concatenated like the outputs): one cat + one pad instead of
+            # a zero fill and two slice copies per level
+            dz_all = torch.nn.functional.pad(
+                torch.cat([dlogits[b].reshape(R, 2 * apl), dbbox[b].reshape(R, 6 * apl)], dim=1),
+                (0, npad - n_out))
             off = 0
             for li, (s, r) in enumerate(zip(shared, rows)):
                 xb = s[b:b + 1]
                 _, H, W, D, _ = xb.shape
-                dz = torch.zeros((r, npad), device=dev, dtype=torch.float32)
-                dz[:, :2 * apl] = dlogits[b, off * apl:(off + r) * apl].reshape(r, 2 * apl)
-                dz[:, 2 * apl:n_out] = dbbox[b, off * apl:(off + r) * apl].reshape(r, 6 * apl)
+                dz = dz_all[off:off + r]
                 if grads.get("bias") is not None:
                     bn_act_bwd(dz, None, None, r, npad, False, None, None, None, None, None, None,
                                None, grads["bias"])

@@ -97,8 +97,8 @@ def _pmc_traffic(kernel_key):
 
 
 def wgrad_gemm_shape(S):
-    """The largest launch of the step's dominant kernel (x3_wgrad_kernel, 21 %
-    of the step's kernel time, profiles/r01s_bench_kernels_128.txt): the 64
+    """The largest launch of the step's second kernel, x3_wgrad_tr_kernel (15.7 %
+    of the step's kernel time, profiles/r02i_bench_kernels_128.txt): the 64
     batched Winograd weight-gradient GEMMs of rpn_conv_shared1 (3x3x3, 256->512)
     on P2 [S/4, S/4, S] -- F(2x2x2) tiles (the weight gradient keeps NZ = 2,
     conv3d.hip wino_wgrad_nz), reduction over M = T tiles, K = 256, N = 512."""
@@ -109,8 +109,8 @@ def wgrad_gemm_shape(S):
 
 
 def wino_gemm_shape(S):
-    """The step's largest launch of x3_gemm_kernel (19 % of the step's kernel
-    time, profiles/r01s_bench_kernels_128.txt): the
+    """The largest launch of the step's dominant kernel, x3_gemm256_af_kernel
+    (17.7 % of the step's kernel time, profiles/r02i_bench_kernels_128.txt): the
     16*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
     256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles, K = 256,
     N = 512 (NZ = 4 by default: 96 GEMMs)."""
@@ -812,10 +812,11 @@ def main():
         with torch.no_grad():
             fmaps = model.features(image)
         try:
-            # dominant kernel of the step: x3_wgrad_kernel (21 % of the step's kernel
-            # time, profiles/r01s_bench_kernels_128.txt), then x3_gemm_kernel (19 %)
-            out["roofline"] = time_wgrad_gemm(S)
-            out["roofline"]["wino_gemm"] = time_wino_gemm(S)
+            # dominant kernel of the step: x3_gemm256_af_kernel (17.7 % of the step's
+            # kernel time: the Winograd point GEMMs plus the big-K 1x1x1 convs,
+            # profiles/r02i_bench_kernels_128.txt), then x3_wgrad_tr_kernel (15.7 %)
+            out["roofline"] = time_wino_gemm(S)
+            out["roofline"]["wgrad_gemm"] = time_wgrad_gemm(S)
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
             out["roofline"]["wino_fwd_conv"] = time_wino_fwd(S)
         except Exception as e:  # report, never hide
