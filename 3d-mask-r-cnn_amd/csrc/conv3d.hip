@@ -2563,6 +2563,160 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         }
 }
 
+// ---- the same GEMM with 256x128 tiles, 4 waves, two workgroups per CU -------
+// x3_gemm256_af_kernel holds one workgroup per CU (144 KB of LDS), so while it
+// stores its tile (the fp32 C it writes is 2/3 of its HBM traffic) the CU's
+// MFMA pipes idle.  Here a workgroup is 4 waves on a 256x128 tile (each wave
+// the same 128x64 block, fragments and MFMA order: bit-identical results) with
+// two 36-KB LDS stages, so two workgroups fit a CU and one's stores overlap the
+// other's main loop.  Per step and wave: B-DMA(kt+1) (3 ops, the stage read at
+// step kt-1), then A-load(kt+2) (4 ops, two rows per thread); vmcnt(4) at the
+// top retires B(kt), vmcnt(7) the A rows of step kt+1 before they are split.
+constexpr int G3_PLA = 256 * G2_BK * 2;   // one A plane of a stage: 8 KB
+constexpr int G3_PLB = 128 * G2_BK * 2;   // one B plane of a stage: 4 KB
+__global__ __launch_bounds__(256, 2) void x3_gemm_af128_kernel(X3G g) {
+    __shared__ __attribute__((aligned(16))) char sA0[3 * G3_PLA], sA1[3 * G3_PLA];
+    __shared__ __attribute__((aligned(16))) char sB0[3 * G3_PLB], sB1[3 * G3_PLB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+    const int64_t nbx = (g.M + 255) / 256, nby = g.N / 128;
+    const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
+    const int64_t L = (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+    if (L >= total) return;
+    const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+    const int64_t bz = T / per_batch, Tt = T - bz * per_batch;
+    const int64_t m0 = (Tt / nby) * 256;
+    const int64_t n0 = (Tt % nby) * 128;
+    const int nk = g.K / G2_BK;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.af + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 4);
+    const int arow = tid >> 1, ach = tid & 1;             // rows arow and arow + 128, k chunk ach
+    const uint32_t aoff0 = ((uint32_t)arow * (uint32_t)g.K + (uint32_t)ach * 8u) * 4u;
+    const uint32_t aoff1 = aoff0 + 128u * (uint32_t)g.K * 4u;
+    const int awr0 = x3_off16(arow, ach), awr1 = x3_off16(arow + 128, ach);
+    __amdgpu_buffer_rsrc_t rb[3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+        rb[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + n0 * g.K, (uint64_t)128 * g.K * 2);
+    const int lrow = 32 * wave + (lane >> 1);
+    const uint32_t lsrc = (uint32_t)lrow * (uint32_t)g.K * 2u + (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4);
+    auto stA = [&](auto st) -> char* {
+        if constexpr (decltype(st)::v == 0) return sA0;
+        else return sA1;
+    };
+    auto stB = [&](auto st) -> char* {
+        if constexpr (decltype(st)::v == 0) return sB0;
+        else return sB1;
+    };
+    auto load_a = [&](int kt, float4 (&v)[4]) {
+        const bool in = kt < nk;
+        const uint32_t o = (uint32_t)kt * (G2_BK * 4);
+        v[0] = bload4(ra, in ? aoff0 + o : M3D_OOB);
+        v[1] = bload4(ra, in ? aoff0 + o + 16u : M3D_OOB);
+        v[2] = bload4(ra, in ? aoff1 + o : M3D_OOB);
+        v[3] = bload4(ra, in ? aoff1 + o + 16u : M3D_OOB);
+    };
+    auto dma_b = [&](auto st, int kt) {
+        char* S = stB(st) + wave * 1024;
+        const uint32_t off = kt < nk ? lsrc + (uint32_t)kt * (G2_BK * 2) : M3D_OOB;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G3_PLB, off);
+    };
+    auto split_a = [&](auto st, const float4 (&v)[4]) {
+        char* S = stA(st);
+        uint2 lo4[3], hi4[3];
+        split3x4(v[0], lo4);
+        split3x4(v[1], hi4);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<uint4*>(S + awr0 + q * G3_PLA) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
+        split3x4(v[2], lo4);
+        split3x4(v[3], hi4);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<uint4*>(S + awr1 + q * G3_PLA) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
+    };
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    float4 xa[4], ya[4];            // A rows of the even / odd steps
+    load_a(0, xa);
+    dma_b(IC<0>{}, 0);
+    load_a(1, ya);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");   // A(0)
+    split_a(IC<0>{}, xa);
+    // step kt on stage kt % 2: cur holds A(kt+1) (loaded at step kt-1), nxt
+    // receives A(kt+2) (its A(kt) was split at step kt-1)
+    auto step = [&](auto st, int kt, float4 (&cur)[4], float4 (&nxt)[4]) {
+        constexpr int s0 = decltype(st)::v;
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");   // B(kt); own A(kt) writes
+        __builtin_amdgcn_s_barrier();
+        dma_b(IC<1 - s0>{}, kt + 1);            // stage last read at step kt-1
+        load_a(kt + 2, nxt);
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");              // A(kt+1)
+        split_a(IC<1 - s0>{}, cur);
+        const char* SA = stA(st);
+        const char* SB = stB(st);
+        bf16x8 bfr[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int off = x3_off16(wn * 64 + j * 32 + l32, h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                bfr[j][pl] = *reinterpret_cast<const bf16x8*>(SB + pl * G3_PLB + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int off = x3_off16(wm * 128 + i * 32 + l32, h);
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G3_PLA + off);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                floatx16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+            }
+        }
+    };
+    for (int kt = 0;;) {
+        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
+        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = (int)n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = acc[i][j][r];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                      (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u),
+                                                      0, 0);
+            }
+        }
+}
+
+// M3D_X3_AF128=1: the fp32-A point GEMMs on x3_gemm_af128_kernel (A/B)
+static int x3_af128_env() {
+    static int v = [] { const char* e = getenv("M3D_X3_AF128"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
 // M3D_X3_256 (default 1): the Winograd point GEMMs with N % 256 == 0 on
 // x3_gemm256_kernel; 0 keeps x3_gemm_kernel everywhere (A/B)
 static int x3_256_env() {
@@ -3192,6 +3346,12 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
     q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
     q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
+    if (af32 && x3_256_env() && x3_af128_env() && N % 128 == 0 && T >= 256) {
+        const int64_t t128 = ((T + 255) / 256) * (N / 128) * P;
+        const dim3 grid((unsigned)(t128 < 65536 ? t128 : 65536), (unsigned)((t128 + 65535) / 65536));
+        hipLaunchKernelGGL(x3_gemm_af128_kernel, grid, dim3(256), 0, s, q);
+        return;
+    }
     if (af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
