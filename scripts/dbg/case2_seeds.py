@@ -44,18 +44,22 @@ for seed in range(nseeds):
         yr = MR.batchnorm(yr, gr, ber, bn.moving_mean.cpu().double(), bn.moving_variance.cpu().double())
     if use_res:
         rr = res.double().requires_grad_(True); yr = yr + rr
+    flips = 0
     if relu:
+        flips = int(((yr > 0) != (y.detach().double().cpu() > 0)).sum())
         yr = torch.relu(yr)
     e_y = rel(y, yr)
     g = torch.tensor(rng.normal(size=yr.shape), dtype=torch.float32)
     y.backward(g.to(cuda))
     join_wgrad()
     yr.backward(g.double())
-    e = [e_y, rel(layer.kernel.grad, wr.grad), rel(layer.bias.grad, br.grad), rel(xg.grad, xr.grad)]
+    e = [e_y, rel(layer.kernel.grad, wr.grad), rel(layer.bias.grad, br.grad)]
+    if cin != 1:
+        e.append(rel(xg.grad, xr.grad))
     if use_bn:
         e += [rel(bn.gamma.grad, gr.grad), rel(bn.beta.grad, ber.grad)]
     flag = max(e) > 1e-4
     bad += flag
     if flag or seed < 3:
-        print(seed, " ".join(f"{v:.2e}" for v in e), "BAD" if flag else "", flush=True)
+        print(seed, " ".join(f"{v:.2e}" for v in e), "BAD" if flag else "", "relu flips", flips, flush=True)
 print("bad", bad, "of", nseeds)
