@@ -622,11 +622,14 @@ extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64
     return check_launch("subsample221_kernel(bwd)");
 }
 
-// total bn_act_bwd blocks (M3D_BN_BLOCKS, default 2048 = 8 per CU: enough
-// loads in flight to stream dy/y/z at HBM rate; 512 reached ~2.7 TB/s)
+// total bn_act_bwd blocks (M3D_BN_BLOCKS, default 1024 = 4 per CU).  Alone the
+// kernel streams best at 2048 (512 reached ~2.7 TB/s); inside the training
+// step, beside the weight-gradient stream, 1024 is faster (step 32.1 -> 31.9 ms
+// at 128^3, 512: 32.4 ms; scripts/gpu_step_ab.sh, round 2) and halves the
+// partial rows bn_sums_reduce_kernel folds.
 static int bn_blocks_env() {
-    static int v = [] { const char* e = getenv("M3D_BN_BLOCKS"); return e ? atoi(e) : 2048; }();
-    return v > 0 ? v : 2048;
+    static int v = [] { const char* e = getenv("M3D_BN_BLOCKS"); return e ? atoi(e) : 1024; }();
+    return v > 0 ? v : 1024;
 }
 static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {
     const int quads = (int)(C / 4);
