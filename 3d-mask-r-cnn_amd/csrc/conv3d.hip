@@ -3536,7 +3536,8 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
                     const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
                     const float* bn_scale, const float* bn_shift, const float* residual,
                     int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
-                    size_t ws_bytes, hipStream_t s, const float* halo = nullptr, int hlo = 0, int hhi = 0) {
+                    size_t ws_bytes, hipStream_t s, const float* halo = nullptr, int hlo = 0, int hhi = 0,
+                    bool v_ready = false) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -3547,7 +3548,8 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
         for (int64_t b = 0; b < B; ++b) {
             rc = fwd_wino(x + b * H * W * D * Cin, 1, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift,
                           residual ? residual + b * os : nullptr, relu, z_out ? z_out + b * os : nullptr, y + b * os,
-                          nullptr, workspace, ws_bytes, s, halo ? halo + b * H * W * 2 * Cin : nullptr, hlo, hhi);
+                          nullptr, workspace, ws_bytes, s, halo ? halo + b * H * W * 2 * Cin : nullptr, hlo, hhi,
+                          v_ready || b > 0);
             if (rc) return rc;
         }
         return M3D_OK;
@@ -3557,10 +3559,12 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
     if (gemm_x3_env() && !u_keep) {
         float* wt = ws.WT;
-        hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
-                           dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
-        WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
-                          (int)Cin, (int)Cout, 0, ws.V);
+        if (!v_ready) {     // v_ready: V already holds this w's transform (an earlier call, same workspace)
+            hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
+                               dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
+            WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
+                              (int)Cin, (int)Cout, 0, ws.V);
+        }
         const bool af32 = x3_af32_env();
         WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
         wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s, af32);
@@ -3617,7 +3621,28 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t s, float* dx_halo = nullptr,
-                         int hlo = 0);
+                         int hlo = 0, bool v_ready = false);
+
+// The same two entry points for convs that share one kernel across calls (the
+// RPN head's rpn_conv_shared1 on P2..P6, core/models.py:512-557): with
+// v_ready = 1 the workspace's V region already holds this w's transform from
+// an earlier call on the same stream (same Cin, Cout, workspace), and the
+// weight transform is skipped.
+extern "C" int m3d_conv3d_fwd_wino_v(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                                     const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                                     const float* bn_scale, const float* bn_shift, const float* residual,
+                                     int32_t relu, float* z_out, float* y, void* workspace, size_t ws_bytes,
+                                     int32_t v_ready, m3d_stream_t s) {
+    return fwd_wino(x, B, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift, residual, relu, z_out, y,
+                    nullptr, workspace, ws_bytes, st(s), nullptr, 0, 0, v_ready != 0);
+}
+extern "C" int m3d_conv3d_bwd_data_wino_v(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                          int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
+                                          int32_t accumulate, void* workspace, size_t ws_bytes, int32_t v_ready,
+                                          m3d_stream_t s) {
+    return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s), nullptr,
+                         0, v_ready != 0);
+}
 
 extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H,
                                         int64_t W, int64_t D, int64_t Cin, int64_t Cout,
@@ -3643,7 +3668,7 @@ static void wino_dgrad_out(const float* Mt, const WinoGeom& g, int C, float* dx,
 
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
-                         void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo) {
+                         void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo, bool v_ready) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -3653,7 +3678,7 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
         for (int64_t b = 0; b < B; ++b) {
             rc = bwd_data_wino(dz + b * H * W * OD * Cout, w, 1, H, W, D, Cin, Cout, OD, pz, dx + b * H * W * dxd * Cin,
                                accumulate, workspace, ws_bytes, hs,
-                               dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo);
+                               dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo, v_ready || b > 0);
             if (rc) return rc;
         }
         return M3D_OK;
@@ -3663,8 +3688,9 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
     WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz);
     if (gemm_x3_env()) {
-        WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
-                          (int)Cin, (int)Cout, 1, ws.V);
+        if (!v_ready)
+            WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
+                              (int)Cin, (int)Cout, 1, ws.V);
         const bool af32 = x3_af32_env();
         if (af32)
             WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,

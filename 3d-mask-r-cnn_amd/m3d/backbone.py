@@ -9,10 +9,16 @@ trainable gamma/beta (TRAIN_BN=False), every conv has a bias.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .nn import GradLink, _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
 from .params import BNLayer, ConvLayer
+
+# the RPN head's shared conv transforms its weights once per pass for all
+# pyramid levels (M3D_SHARE_WINO_WEIGHTS=0: once per level, A/B)
+SHARE_WINO_WEIGHTS = os.environ.get("M3D_SHARE_WINO_WEIGHTS", "1") != "0"
 
 
 class _Unit:
@@ -150,11 +156,16 @@ class RPNHead:
 
     def __call__(self, feature_maps):
         shared = []
+        # rpn_conv_shared1 is one kernel on every level: its Winograd weight
+        # transform is done once per pass (forward and data gradient) and reused
+        wshare = {} if SHARE_WINO_WEIGHTS else None
         for p in feature_maps:
             g1 = conv_geom(tuple(p.shape[1:4]), (3, 3, 3), (1, 1, 1), "same")
-            s = conv_bn_act(p, self.shared1, g1, relu=True)
+            s = conv_bn_act(p, self.shared1, g1, relu=True, wshare=wshare)
             g2 = conv_geom(tuple(s.shape[1:4]), (1, 1, 1), (1, 1, 1), "valid")
             shared.append(conv_bn_act(s, self.shared2, g2, relu=True))
+        if wshare is not None:
+            wshare.pop("fwd", None)        # the forward's workspace is not needed past the loop
         apl = self.apl
         cin = 256
         w24 = torch.cat([self.cls.kernel.data.reshape(cin, 2 * apl),

@@ -156,6 +156,28 @@ def _x3_planes(w, cin, cout, transpose):
     return planes
 
 
+def _shared_wino_ws(wshare, role, ws, wsb):
+    """Workspace of a Winograd conv whose kernel is shared across calls
+    (``wshare``: one dict per shared kernel and forward pass, e.g. the RPN
+    head's rpn_conv_shared1 on P2..P6).  The first call of a role ("fwd" /
+    "bwd") transforms the weights into its workspace, sized for the largest
+    level, and keeps it; later calls of that role reuse the workspace with
+    v_ready = 1 (no weight transform).  Returns (ws, ws_bytes, v_ready)."""
+    if wshare is None:
+        return ws, wsb, 0
+    if role == "fwd":
+        wshare["max_bytes"] = max(wshare.get("max_bytes", 0), wsb)
+    held = wshare.get(role)
+    if held is not None and held[1] >= wsb:
+        return held[0], held[1], 1
+    nb = max(wsb, wshare.get("max_bytes", 0))
+    if nb > wsb:
+        ws = torch.empty(nb // 4 + 1, device=ws.device, dtype=torch.float32)
+        wsb = nb
+    wshare[role] = (ws, wsb)
+    return ws, wsb, 0
+
+
 def _wino_ws(B, H, W, D, OD, cin, cout, dev):
     n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, cin, cout))
     return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
@@ -265,7 +287,8 @@ class _ConvBNAct(torch.autograd.Function):
     source of y (FPN top-down add, core/models.py:3193-3204)."""
 
     @staticmethod
-    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, halo=None):
+    def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, halo=None,
+                wshare=None):
         B, H, W, D, Cin = x.shape
         # depth slab (m3d.slab): halo = (planes [B,H,W,2,C], has_lo, has_hi) read by the
         # Winograd kernels beside x instead of a halo-extended copy of x
@@ -312,10 +335,11 @@ class _ConvBNAct(torch.autograd.Function):
                                                     1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u),
                                                     ptr(ws), wsb, stream()), "conv3d_fwd_wino_keep")
             else:
-                check(_L().m3d_conv3d_fwd_wino(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
-                                               ptr(b), ptr(scale),
-                                               ptr(shift), ptr(residual), 1 if relu else 0, ptr(z), ptr(y),
-                                               ptr(ws), wsb, stream()), "conv3d_fwd_wino")
+                ws, wsb, v_ready = _shared_wino_ws(wshare, "fwd", ws, wsb)
+                check(_L().m3d_conv3d_fwd_wino_v(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
+                                                 ptr(b), ptr(scale), ptr(shift), ptr(residual), 1 if relu else 0,
+                                                 ptr(z), ptr(y), ptr(ws), wsb, v_ready, stream()),
+                      "conv3d_fwd_wino")
         elif res_mode <= 2 and _conv1_x3(x.shape, geo, Cin, Cout):
             planes = _x3_planes(w, Cin, Cout, True)
             check(_L().m3d_conv3d_fwd_x3(ptr(x), B, H, W, D, Cin, ptr(planes), Cout, ptr(b), ptr(scale),
@@ -344,6 +368,7 @@ class _ConvBNAct(torch.autograd.Function):
             nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
             _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
         ctx.save_for_backward(x, w, y, z)
+        ctx.wshare = wshare
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -430,13 +455,14 @@ class _ConvBNAct(torch.autograd.Function):
                           "conv3d_bwd_data_wino_halo")
                     slab.return_halo_grads(dx, dh)
                 else:
-                    check(L.m3d_conv3d_bwd_data_wino(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
-                                                     geo.pad[2], ptr(dx), acc, ptr(ws), wsb, stream()),
+                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb)
+                    check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                       geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, stream()),
                           "conv3d_bwd_data_wino")
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             ctx.halo = None
-            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None
+            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None, None
         if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
@@ -484,7 +510,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
-        return dx, dr, None, None, None, None, None, None, None, None, None, None
+        return dx, dr, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _slab_extend(x, geo):
@@ -499,10 +525,12 @@ def _slab_extend(x, geo):
     return xe, ConvGeom(geo.k, geo.stride, (geo.pad[0], geo.pad[1], r - nlo), geo.out)
 
 
-def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None):
+def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None,
+                wshare=None):
     """Functional entry: ``layer`` is a Conv3D parameter group from params.py.
     ``link``: a GradLink shared by the residual conv and the input conv of an
-    identity block (see GradLink)."""
+    identity block (see GradLink).  ``wshare``: a dict shared by the calls of
+    one kernel within a pass (see _shared_wino_ws)."""
     w = layer.kernel.data
     b = layer.bias.data if layer.bias is not None else None
     grads = layer.grad_dict(bn) if torch.is_grad_enabled() else None   # inference: no z / grads
@@ -524,7 +552,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                            need_dx and x.requires_grad, link, halo)
+                            need_dx and x.requires_grad, link, halo, wshare)
 
 
 class _MaxPool(torch.autograd.Function):

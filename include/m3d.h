@@ -218,6 +218,19 @@ int m3d_conv3d_fwd_x3(const float* x, int64_t B, int64_t H, int64_t W, int64_t D
                       float* z_out, float* y, m3d_stream_t s);
 int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
                            int64_t Cin, int64_t Cout, float* dx, m3d_stream_t s);
+/* m3d_conv3d_fwd_wino / m3d_conv3d_bwd_data_wino for a kernel shared across
+ * calls (rpn_conv_shared1 on P2..P6, core/models.py:512-557): v_ready = 1 means
+ * the workspace's transformed-weight region already holds this w's transform
+ * from an earlier call on the same stream with the same Cin, Cout and
+ * workspace, and the weight transform is skipped (results bit-identical). */
+int m3d_conv3d_fwd_wino_v(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                          const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                          const float* bn_scale, const float* bn_shift, const float* residual, int32_t relu,
+                          float* z_out, float* y, void* workspace, size_t ws_bytes, int32_t v_ready,
+                          m3d_stream_t s);
+int m3d_conv3d_bwd_data_wino_v(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                               int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                               void* workspace, size_t ws_bytes, int32_t v_ready, m3d_stream_t s);
 int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
                           int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd,
                           int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,

@@ -494,3 +494,44 @@ def test_conv1_x3_matches_direct(cuda, res_mode):
                                      p(d0), 0, _lib.stream()), "bwd")
     close(d1.reshape(-1, Cin), dz.double().reshape(-1, Cout) @ w.double().t())
     close(d1, d0, 1e-5)
+
+
+def test_wino_shared_weight_transform_bit_identical(cuda):
+    """m3d_conv3d_fwd_wino_v / _bwd_data_wino_v with v_ready = 1 (the RPN
+    head's shared kernel on several levels: the weight transform of the first
+    call reused from the workspace) give the same bits as a fresh transform."""
+    from m3d import _lib
+    L = _lib.load()
+    p = _lib.ptr
+    torch.manual_seed(21)
+    Cin, Cout = 128, 256
+    w = torch.randn((3, 3, 3, Cin, Cout), device=cuda) / (27 * Cin) ** 0.5
+    b = torch.randn(Cout, device=cuda)
+    shapes = [(1, 8, 8, 16), (1, 4, 4, 8), (1, 2, 2, 4)]
+    nbs = [L.m3d_conv3d_wino_workspace_bytes(*s, s[3], Cin, Cout) for s in shapes]
+    shared = torch.empty(max(nbs) // 4 + 1, device=cuda)
+    for i, s in enumerate(shapes):
+        x = torch.randn((*s, Cin), device=cuda)
+        dz = torch.randn((*s, Cout), device=cuda)
+        outs = []
+        for reuse in (False, True):
+            ws = shared if reuse else torch.empty(nbs[i] // 4 + 1, device=cuda)
+            nb = shared.numel() * 4 if reuse else nbs[i]
+            v = 1 if (reuse and i > 0) else 0
+            y = torch.empty((*s, Cout), device=cuda)
+            _lib.check(L.m3d_conv3d_fwd_wino_v(p(x), *s, Cin, p(w), Cout, s[3], 1, p(b), None, None, None, 1, None,
+                                               p(y), p(ws), nb, v, _lib.stream()), "fwd_v")
+            outs.append(y)
+        assert torch.equal(outs[0], outs[1])
+    for i, s in enumerate(shapes):          # the data gradient, its own shared workspace
+        dz = torch.randn((*s, Cout), device=cuda)
+        outs = []
+        for reuse in (False, True):
+            ws = shared if reuse else torch.empty(nbs[i] // 4 + 1, device=cuda)
+            nb = shared.numel() * 4 if reuse else nbs[i]
+            v = 1 if (reuse and i > 0) else 0
+            dx = torch.empty((*s, Cin), device=cuda)
+            _lib.check(L.m3d_conv3d_bwd_data_wino_v(p(dz), p(w), *s, Cin, Cout, s[3], 1, p(dx), 0, p(ws), nb, v,
+                                                    _lib.stream()), "bwd_v")
+            outs.append(dx)
+        assert torch.equal(outs[0], outs[1])
