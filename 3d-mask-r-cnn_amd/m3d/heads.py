@@ -283,4 +283,4 @@ class MaskRCNN:
         mrcnn_mask = self.mask_head(mpooled)
         return {"detections": detections, "mrcnn_class": mrcnn_class, "mrcnn_bbox": mrcnn_bbox,
                 "mrcnn_mask": mrcnn_mask, "rpn_rois": rpn_rois, "feature_maps": fmaps,
-                "pooled": pooled, "mask_pooled": mpooled}
+                "pooled": pooled, "mask_pooled": mpooled, "rpn_class": rpn_probs, "rpn_bbox": rpn_bbox}

@@ -158,13 +158,15 @@ def _x3_planes(w, cin, cout, transpose):
     return planes
 
 
-def _shared_wino_ws(wshare, role, ws, wsb):
+def _shared_wino_ws(wshare, role, ws, wsb, tag=None):
     """Workspace of a Winograd conv whose kernel is shared across calls
     (``wshare``: one dict per shared kernel and forward pass, e.g. the RPN
     head's rpn_conv_shared1 on P2..P6).  The first call of a role ("fwd" /
     "bwd") transforms the weights into its workspace, sized for the largest
     level, and keeps it; later calls of that role reuse the workspace with
-    v_ready = 1 (no weight transform).  Returns (ws, ws_bytes, v_ready)."""
+    v_ready = 1 (no weight transform).  ``tag`` (weight pointer, Cin, Cout)
+    guards the reuse: a held workspace transformed from other weights is never
+    passed with v_ready = 1.  Returns (ws, ws_bytes, v_ready)."""
     if wshare is None:
         return ws, wsb, 0
     if role == "fwd":
@@ -175,14 +177,26 @@ def _shared_wino_ws(wshare, role, ws, wsb):
         # workspaces as before (measured 204 -> 306 ms/step at 256^3 held)
         return ws, wsb, 0
     held = wshare.get(role)
-    if held is not None and held[1] >= wsb:
+    if held is not None and held[1] >= wsb and held[2] == tag:
         return held[0], held[1], 1
     nb = max(wsb, wshare.get("max_bytes", 0))
     if nb > wsb:
         ws = torch.empty(nb // 4 + 1, device=ws.device, dtype=torch.float32)
         wsb = nb
-    wshare[role] = (ws, wsb)
+    wshare[role] = (ws, wsb, tag)
     return ws, wsb, 0
+
+
+def _shared_wino_release(wshare):
+    """After a shared kernel's data-gradient call: the last pending call of
+    the pass drops the held 'bwd' workspace (it would otherwise live until the
+    autograd graph is destroyed, through the rest of the backbone backward)."""
+    if wshare is None or "pending_bwd" not in wshare:
+        return
+    wshare["pending_bwd"] -= 1
+    if wshare["pending_bwd"] <= 0:
+        wshare.pop("bwd", None)
+        wshare.pop("pending_bwd", None)
 
 
 def _wino_ws(B, H, W, D, OD, cin, cout, dev):
@@ -342,7 +356,7 @@ class _ConvBNAct(torch.autograd.Function):
                                                     1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u),
                                                     ptr(ws), wsb, stream()), "conv3d_fwd_wino_keep")
             else:
-                ws, wsb, v_ready = _shared_wino_ws(wshare, "fwd", ws, wsb)
+                ws, wsb, v_ready = _shared_wino_ws(wshare, "fwd", ws, wsb, (w.data_ptr(), Cin, Cout))
                 check(_L().m3d_conv3d_fwd_wino_v(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
                                                  ptr(b), ptr(scale), ptr(shift), ptr(residual), 1 if relu else 0,
                                                  ptr(z), ptr(y), ptr(ws), wsb, v_ready, stream()),
@@ -376,6 +390,9 @@ class _ConvBNAct(torch.autograd.Function):
             _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
         ctx.save_for_backward(x, w, y, z)
         ctx.wshare = wshare
+        if wshare is not None and ctx.wino and halo is None and need_dx:
+            # data-gradient calls still to come: the last one releases the held workspace
+            wshare["pending_bwd"] = wshare.get("pending_bwd", 0) + 1
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -462,10 +479,11 @@ class _ConvBNAct(torch.autograd.Function):
                           "conv3d_bwd_data_wino_halo")
                     slab.return_halo_grads(dx, dh)
                 else:
-                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb)
+                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout))
                     check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                        geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, stream()),
                           "conv3d_bwd_data_wino")
+                    _shared_wino_release(ctx.wshare)
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             ctx.halo = None

@@ -116,7 +116,7 @@ def build_rpn_targets(anchors, gt_class_ids, gt_boxes, config, seed=0, list_cap=
     gtd = torch.from_numpy(np.ascontiguousarray(gt)).to(dev)
     match8 = torch.empty((A,), device=dev, dtype=torch.int8)
     bbox = torch.empty((total, 6), device=dev, dtype=torch.float32)
-    cap = int(list_cap or min(A, 1 << 20))
+    cap = int(list_cap or A)                          # a GT's IoU > 0 list never exceeds A
     wsb = int(L.m3d_rpn_targets_workspace_bytes(A, G, cap))
     ws = torch.empty(max(wsb, 1), device=dev, dtype=torch.uint8)
     sd = (_lib.c_f * 6)(*[float(np.float32(v)) for v in config.RPN_BBOX_STD_DEV])
@@ -142,7 +142,14 @@ class RPNTargetBuilder:
     builder(gt_boxes, seed) with gt_boxes a normalised [G,6] DEVICE tensor
     returns m3d.model.DeviceRPNTargets (rpn_match int8 [A], rpn_bbox
     [RPN_TRAIN_ANCHORS_PER_IMAGE, 6]); ``counts`` (device int32[3]) holds the
-    last call's positives, negatives and list-overflow flag."""
+    last call's positives, negatives and list-overflow flag.
+
+    Same contract as the synchronous builder, which returns M3D_EINVAL when a
+    GT's IoU > 0 candidate list passes ``list_cap``: by default the cap is A,
+    so no list can be truncated.  With a smaller explicit cap, each call queues
+    a copy of its flag to pinned host memory, and the next call (or
+    ``check()``, which waits for it) raises RuntimeError when it was set --
+    truncated lists would label from an atomic-order-dependent subset."""
 
     def __init__(self, anchors, config, max_gt=64, list_cap=None):
         ops._dev(anchors)
@@ -158,12 +165,28 @@ class RPNTargetBuilder:
         self.topk = int(getattr(config, "ATSS_TOPK", 24))
         self.min_pos = int(getattr(config, "ATSS_MIN_POS_PER_GT", 4))
         self.sd = (_lib.c_f * 6)(*[float(np.float32(v)) for v in config.RPN_BBOX_STD_DEV])
-        self.cap = int(list_cap or min(self.A, 1 << 20))
+        self.cap = int(list_cap or self.A)
         self.wsb = int(self.L.m3d_rpn_targets_workspace_bytes(self.A, self.max_gt, self.cap))
         self.ws = torch.empty(max(self.wsb, 1), device=dev, dtype=torch.uint8)
         self.match = torch.empty((self.A,), device=dev, dtype=torch.int8)
         self.bbox = torch.empty((self.total, 6), device=dev, dtype=torch.float32)
         self.counts = torch.zeros((3,), device=dev, dtype=torch.int32)
+        self._flag_host = torch.zeros((3,), dtype=torch.int32, pin_memory=True) if self.cap < self.A else None
+        self._flag_event = None
+
+    def check(self, wait=True):
+        """Raise if the last call's candidate lists overflowed ``list_cap``.
+        wait=False only looks at a flag whose copy has already landed."""
+        ev = self._flag_event
+        if ev is None:
+            return
+        if not wait and not ev.query():
+            return
+        ev.synchronize()
+        self._flag_event = None
+        if int(self._flag_host[2]) != 0:
+            raise RuntimeError(f"rpn_targets_async: a GT overlaps more than list_cap={self.cap} anchors "
+                               f"(its ATSS candidate list was truncated); raise list_cap (A = {self.A})")
 
     def __call__(self, gt_boxes, seed=0):
         from .model import DeviceRPNTargets
@@ -172,9 +195,14 @@ class RPNTargetBuilder:
         G = int(gt.shape[0])
         if G > self.max_gt:
             raise ValueError(f"{G} GT boxes, builder sized for max_gt={self.max_gt}")
+        self.check()                                  # the previous call's flag (copy landed long ago)
         check(self.L.m3d_rpn_targets_async(ptr(self.anchors), self.A, ptr(gt), G, self.pos_iou, self.neg_iou,
                                            self.total, self.ratio, self.topk, self.min_pos, self.sd,
                                            int(seed) & 0xFFFFFFFF, ptr(self.match), ptr(self.bbox), self.cap,
                                            ptr(self.ws), self.wsb, ptr(self.counts), stream()),
               "rpn_targets_async")
+        if self._flag_host is not None:
+            self._flag_host.copy_(self.counts, non_blocking=True)
+            self._flag_event = torch.cuda.Event()
+            self._flag_event.record()
         return DeviceRPNTargets(self.match, self.bbox)

@@ -41,7 +41,8 @@ class LegWatchdog:
     """Bounds a multi-rank leg whose collectives have no timeout of their own:
     if the leg is still running after `seconds`, rank 0 prints the result line
     gathered so far (the leg reported as timed out) and every rank leaves with
-    status 0, so one hung leg cannot cost the bench line of the whole run."""
+    status 3: one hung leg cannot cost the bench line of the whole run, and
+    the hang stays visible to the launcher (the legs after it are missing)."""
 
     def __init__(self, seconds, rank, out, key):
         import threading
@@ -53,8 +54,8 @@ class LegWatchdog:
         if self.rank == 0:
             self.out[self.key] = {"error": "timeout: the leg did not finish (watchdog)"}
             print(json.dumps(self.out), flush=True)
-        log(f"[bench] watchdog: {self.key} timed out on rank {self.rank}, exiting")
-        os._exit(0)
+        log(f"[bench] watchdog: {self.key} timed out on rank {self.rank}, exiting with status 3")
+        os._exit(3)
 
     def __enter__(self):
         self.timer.start()

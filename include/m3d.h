@@ -52,7 +52,7 @@ int32_t m3d_get_deterministic(void);
 /* ---------------------------------------------------------------------------
  * CropAndResize3D family.  Replaces the TF custom ops of the vendored wheel
  * tensorflow_nms_car_3d==0.1.0 imported at core/custom_op/custom_op.py:22-24:
- *   crop_and_resize_3d(image, boxes, box_ind, crop_size,
+ *   crop_and_resize_3d(image, boxes, box_index, crop_size,
  *                      method_name='trilinear', extrapolation_value=0)
  *   crop_and_resize_3d_grad_image(grads, boxes, box_ind, image_size, T, method_name)
  *   crop_and_resize_3d_grad_boxes(grads, image, boxes, box_ind, method_name)

@@ -59,7 +59,7 @@ int32 method_code(const string& m) { return m == "nearest" ? 1 : 0; }
 REGISTER_OP("CropAndResize3D")
     .Input("image: T")
     .Input("boxes: float")
-    .Input("box_ind: int32")
+    .Input("box_index: int32")     // the wheel's name (its grad ops say box_ind)
     .Input("crop_size: int32")
     .Output("crops: float")
     .Attr("T: {uint8, uint16, int8, int16, int32, int64, half, float, double}")

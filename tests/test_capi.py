@@ -84,3 +84,22 @@ def test_tf_binding_matches_header():
                "NonMaxSuppression3D"):
         assert f'REGISTER_OP("{op}")' in src
         assert re.search(r'Name\("' + op + r'"\)\.Device\(DEVICE_GPU\)', src), op
+
+
+def test_tf_op_defs_match_the_wheel():
+    """Every REGISTER_OP of the TF binding declares exactly the wheel's op-def:
+    the same .Input / .Output / .Attr specs in the same order, compared with
+    the strings extracted statically from the reference's vendored op
+    libraries (tests/golden/wheel_opdefs.json, tests/golden/extract_opdefs.py)
+    -- e.g. CropAndResize3D's third input is `box_index`, its grad ops'
+    `box_ind`."""
+    import json
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "wheel_opdefs.json")))
+    src = open(os.path.join(ROOT, "integration", "tf", "m3d_tf_ops.cc")).read()
+    src = re.sub(r"//[^\n]*", "", src)
+    assert len(want) == 4
+    for op, d in want.items():
+        i = src.index(f'REGISTER_OP("{op}")')
+        j = src.index(".SetShapeFn", i)
+        got = re.findall(r'\.(?:Input|Output|Attr)\("([^"]*)"\)', src[i:j])
+        assert got == d["specs"], (op, got, d["specs"])

@@ -129,3 +129,44 @@ def test_train_steps_bitwise_repeatable(det, cuda):
     d = _train(cuda, 4)
     assert abs(a[0] - d[0]) <= 1e-5 * abs(a[0])
     assert float((a[2] - d[2]).abs().max()) <= 1e-5 * float(a[2].abs().max())
+
+
+def test_rpn_head_shared_wino_policy_bit_identical(det, cuda, monkeypatch):
+    """The RPN head's shared Winograd weight transform as the model drives it
+    (m3d.nn._shared_wino_ws): forward + backward of the whole RPN with sharing
+    on, off (M3D_SHARE_WINO_WEIGHTS=0) and on with a 0-byte cap
+    (M3D_SHARE_WINO_MAX_GB=0: every level falls back to its own workspace) give
+    bit-identical outputs and gradients (deterministic mode), and the held
+    data-gradient workspace is released after the last level's call."""
+    from m3d import backbone as BB
+    from m3d import nn as NN
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
+    _lib = det
+    _lib.set_deterministic(True)
+    cfg = synthetic_rpn_config(64, depth=16, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=200)
+    image = synthetic_volume(64, 16, seed=3).to(cuda)
+    seen = []
+    real_release = NN._shared_wino_release
+
+    def spy(wshare):
+        real_release(wshare)
+        if wshare is not None:
+            seen.append("bwd" in wshare)
+    monkeypatch.setattr(NN, "_shared_wino_release", spy)
+    res = []
+    for share, cap in ((True, NN.SHARE_WINO_MAX_BYTES), (False, NN.SHARE_WINO_MAX_BYTES), (True, 0)):
+        monkeypatch.setattr(BB, "SHARE_WINO_WEIGHTS", share)
+        monkeypatch.setattr(NN, "SHARE_WINO_MAX_BYTES", cap)
+        model = RPN(cfg, device=cuda, seed=7)
+        match, bbox = synthetic_rpn_targets(model.anchors.shape[1], 256, seed=2)
+        seen.clear()
+        r = model.forward_backward(image, RPNTargets(match, bbox, cuda), proposals=False)
+        torch.cuda.synchronize()
+        if share and cap > 0:
+            assert len(seen) >= 2 and seen[-1] is False and all(seen[:-1]), seen
+        res.append((r["loss"].clone(), model.store.grad_flat.clone()))
+        del model
+    for loss, grad in res[1:]:
+        assert torch.equal(loss, res[0][0])
+        assert torch.equal(grad, res[0][1])

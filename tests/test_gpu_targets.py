@@ -128,3 +128,33 @@ def test_rpn_targets_async_in_step_form(cuda, S, D, G, total):
     for fn, x in ((rpn_class_loss, logits), (rpn_bbox_loss, deltas)):
         a, b = float(fn(t, x)), float(fn(host, x))
         assert abs(a - b) <= 1e-6 * max(1.0, abs(b)), (fn.__name__, a, b)
+
+
+def test_rpn_targets_list_cap_overflow_raises(cuda):
+    """A GT whose IoU > 0 candidate list passes list_cap: the synchronous
+    builder returns M3D_EINVAL (ValueError); the in-step builder raises at its
+    next call / check() instead of labelling from a truncated, atomic-order
+    dependent list.  The default cap (A) cannot overflow."""
+    from m3d.anchors import get_anchors
+    from m3d.config import synthetic_rpn_config
+    from m3d.targets import RPNTargetBuilder, build_rpn_targets
+    cfg = synthetic_rpn_config(64, depth=16, RPN_POSITIVE_IOU=0.3, RPN_NEGATIVE_IOU=0.1,
+                               RPN_TRAIN_ANCHORS_PER_IMAGE=256, ATSS_TOPK=24, ATSS_MIN_POS_PER_GT=4)
+    anchors = torch.from_numpy(get_anchors(cfg)).to(cuda)
+    gt = np.array([[0.1, 0.1, 0.1, 0.9, 0.9, 0.9]], np.float32)     # overlaps most anchors
+    with pytest.raises(ValueError):
+        build_rpn_targets(anchors, np.ones(1, np.int32), gt, cfg, seed=1, list_cap=64)
+    small = RPNTargetBuilder(anchors, cfg, max_gt=4, list_cap=64)
+    gtd = torch.from_numpy(gt).to(cuda)
+    small(gtd, seed=1)
+    with pytest.raises(RuntimeError, match="list_cap"):
+        small.check()
+    small(gtd, seed=2)
+    with pytest.raises(RuntimeError, match="list_cap"):
+        small(gtd, seed=3)                            # raised for the previous call's flag
+    full = RPNTargetBuilder(anchors, cfg, max_gt=4)
+    t = full(gtd, seed=1)
+    full.check()
+    assert int(full.counts[2]) == 0
+    m_sync, _ = build_rpn_targets(anchors, np.ones(1, np.int32), gt, cfg, seed=1)
+    assert torch.equal(t.match.to(torch.int32), m_sync)
