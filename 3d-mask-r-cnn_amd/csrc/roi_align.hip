@@ -275,6 +275,156 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(LineArgs a, Pyr P) {
     }
 }
 
+// ---- PyramidROIAlign forward, region-major --------------------------------------
+// The ROI-major line kernel reads each ROI's own corner rows once, but rows
+// shared by overlapping ROIs are fetched again for every ROI (PMC traffic 2x
+// the globally unique bytes at 256^3, 512 ROIs).  Here a workgroup owns a
+// TY x TX x TZ block of one pyramid level's voxels and produces every ROI
+// sample whose floor corner lies in the block (samples outside the map are
+// assigned by the clamped coordinate, so every sample has exactly one owner):
+// the block's rows are read by all ROIs within the workgroup's short lifetime
+// and stay in L2, and the blocks are issued XCD-contiguously with z fastest,
+// so the z-neighbour's halo plane is in the same L2.  Per sample the
+// arithmetic is line_fwd_kernel's (bit-identical).  The sample coordinate is
+// monotone in the sample index (boxes_adj has y2 > y1 etc.), so the samples of
+// a box in a block are one contiguous index range per axis: lanes evaluate the
+// 64 sample coordinates of an axis and one ballot gives the range.
+struct RegionGrid {
+    int64_t off[5];              // first block of each level
+    int gy[4], gx[4], gz[4];     // blocks per axis and level
+};
+
+// owner voxel index of a sample coordinate along an axis of S voxels
+__device__ __forceinline__ int owner_idx(float in, int S) {
+    return in >= 0.0f ? (in <= (float)(S - 1) ? (int)floorf(in) : S - 1) : 0;
+}
+
+template <int TY, int TX, int TZ>
+__global__ __launch_bounds__(256) void region_fwd_kernel(LineArgs a, Pyr P, RegionGrid G) {
+    const int64_t blk = xcd_block();
+    if (blk >= G.off[4]) return;
+    int l = 0;
+    while (l < 3 && blk >= G.off[l + 1]) ++l;
+    int64_t r = blk - G.off[l];
+    const int bz = (int)(r % G.gz[l]); r /= G.gz[l];
+    const int bx = (int)(r % G.gx[l]); r /= G.gx[l];
+    const int by = (int)(r % G.gy[l]);
+    const int64_t b = r / G.gy[l];
+    const int H = P.H[l], W = P.W[l], D = P.D[l];
+    const int Y0 = by * TY, X0 = bx * TX, Z0 = bz * TZ;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int C4 = a.C >> 2;
+    const float4* base = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)b * H * W * D * a.C);
+    const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
+    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
+    int64_t k = 0;                                   // running work-unit counter (wave-uniform)
+    for (int64_t n0 = 0; n0 < a.N; n0 += 64) {
+        bool rel = false;
+        const int64_t nl = n0 + lane;
+        if (nl < a.N && a.levels[b * a.N + nl] == l + 2) {
+            const float* bx6 = a.boxes + (b * a.N + nl) * 6;
+            auto hit = [](float b1, float b2, int S, int n, int A0, int T) {
+                const float sc = axis_scale(b1, b2, S, n);
+                const int lo = owner_idx(axis_coord(b1, b2, S, n, 0, sc), S);
+                const int hi = owner_idx(axis_coord(b1, b2, S, n, n - 1, sc), S);
+                return hi >= A0 && lo < A0 + T;
+            };
+            rel = hit(bx6[0], bx6[3], H, a.ch, Y0, TY) && hit(bx6[1], bx6[4], W, a.cw, X0, TX) &&
+                  hit(bx6[2], bx6[5], D, a.cd, Z0, TZ);
+        }
+        for (uint64_t rm = __ballot(rel); rm; rm &= rm - 1) {
+            const int64_t n = b * a.N + n0 + __builtin_ctzll(rm);
+            const float* box = a.boxes + n * 6;
+            const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
+            const float ysc = axis_scale(y1, y2, H, a.ch), xsc = axis_scale(x1, x2, W, a.cw);
+            const float zsc = axis_scale(z1, z2, D, a.cd);
+            const int oy = owner_idx(axis_coord(y1, y2, H, a.ch, lane, ysc), H);
+            const int ox = owner_idx(axis_coord(x1, x2, W, a.cw, lane, xsc), W);
+            const int oz = owner_idx(axis_coord(z1, z2, D, a.cd, lane, zsc), D);
+            const uint64_t my = __ballot(lane < a.ch && oy >= Y0 && oy < Y0 + TY);
+            const uint64_t mx = __ballot(lane < a.cw && ox >= X0 && ox < X0 + TX);
+            const uint64_t mz = __ballot(lane < a.cd && oz >= Z0 && oz < Z0 + TZ);
+            if (!my || !mx || !mz) continue;
+            const int ny = __builtin_popcountll(my), nx = __builtin_popcountll(mx);
+            const int y0 = __builtin_ctzll(my), x0 = __builtin_ctzll(mx);
+            const int z0 = __builtin_ctzll(mz), z1e = z0 + __builtin_popcountll(mz);
+            const int64_t units = (int64_t)ny * nx;
+            // this wave's units: global unit index (k + u) == wave (mod 4)
+            for (int64_t u = (wave - k % 4 + 4) % 4; u < units; u += 4) {
+                const int y = y0 + (int)(u / nx), x = x0 + (int)(u % nx);
+                const float in_y = axis_coord(y1, y2, H, a.ch, y, ysc);
+                const float in_x = axis_coord(x1, x2, W, a.cw, x, xsc);
+                float4* o = reinterpret_cast<float4*>(a.out + ((n * a.ch + y) * a.cw + x) * (int64_t)a.cd * a.C);
+                const bool yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
+                if (yx_oob) {
+                    for (int z = z0; z < z1e; ++z)
+                        for (int c = lane; c < C4; c += 64) st_nt(o + (int64_t)z * C4 + c, ex);
+                    continue;
+                }
+                const int ty = (int)floorf(in_y), byy = (int)ceilf(in_y);
+                const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+                const float yl = in_y - (float)ty, xl = in_x - (float)lx;
+                const float4* col[4] = {base + ty * rowW + lx * rowD, base + ty * rowW + rx * rowD,
+                                        base + byy * rowW + lx * rowD, base + byy * rowW + rx * rowD};
+                for (int c = lane; c < C4; c += 64) {
+                    int pk = -1;
+                    float4 kv[4];
+                    for (int z = z0; z < z1e; ++z) {
+                        const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
+                        float4 rv;
+                        if (in_z < 0 || in_z > (float)(D - 1)) {
+                            rv = ex;
+                        } else {
+                            const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+                            const float zl = in_z - (float)fz;
+                            float4 fv[4];
+                            if (fz == pk) {
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) fv[q] = kv[q];
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
+                            }
+                            if (kz != fz) {
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) kv[q] = fv[q];
+                            }
+                            pk = kz;
+                            rv = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
+                            rv.x = scrub(rv.x); rv.y = scrub(rv.y); rv.z = scrub(rv.z); rv.w = scrub(rv.w);
+                        }
+                        st_nt(o + (int64_t)z * C4 + c, rv);
+                    }
+                }
+            }
+            k += units;
+        }
+    }
+}
+
+// block shape of the region-major forward: M3D_ROI_REGION = 0 (off: line kernel),
+// 1 (2x2x8, default), 2 (4x4x4), 3 (2x2x16), 4 (4x4x8)
+static int roi_region_mode() {
+    static const int env = [] { const char* e = getenv("M3D_ROI_REGION"); return e ? atoi(e) : 1; }();
+    return env;
+}
+
+template <int TY, int TX, int TZ>
+static void launch_region_fwd(const LineArgs& a, const Pyr& P, int64_t B, hipStream_t s) {
+    RegionGrid G;
+    G.off[0] = 0;
+    for (int l = 0; l < 4; ++l) {
+        G.gy[l] = (P.H[l] + TY - 1) / TY;
+        G.gx[l] = (P.W[l] + TX - 1) / TX;
+        G.gz[l] = (P.D[l] + TZ - 1) / TZ;
+        G.off[l + 1] = G.off[l] + B * G.gy[l] * G.gx[l] * G.gz[l];
+    }
+    hipLaunchKernelGGL((region_fwd_kernel<TY, TX, TZ>), dim3((unsigned)G.off[4]), dim3(256), 0, s, a, P, G);
+}
+
 // ---- trilinear backward in gather form ----------------------------------------
 // The 8-corner scatter of A.2 is separable: the gradient of voxel (Y,X,Z) is
 // sum_{i,j,k} g[i][j][k] * ((wy(Y,i) * wx(X,j)) * wz(Z,k)), where wy(Y,i) is
@@ -479,6 +629,171 @@ __global__ __launch_bounds__(256) void crop_bwd_serial_kernel(
                                     gv * w;
                             }
                 }
+    }
+}
+
+// Deterministic grad_image, segmented by destination: every voxel row of the
+// output is owned by one thread (its channels by a float4 / float lane), which
+// walks the contributions it receives in the reference order and keeps the
+// running fp32 sum in a register -- so no atomics, no zero fill (every voxel is
+// stored once) and the same bits as crop_bwd_serial_kernel's sequential replay.
+//
+// Why the order is the replay's: restricted to one destination voxel, the
+// replay adds terms in (box n, y, x, z, corner) order.  Per sample at most ONE
+// corner with a nonzero weight lands on a given voxel (two corners coincide
+// only when floor == ceil, i.e. the lerp is exactly 0 and the second corner's
+// weight is 0), and adding a zero term to the running sum never changes it
+// (the sum starts at +0 and round-to-nearest never produces -0 from +0, so
+// x + (+-0) == x for every reachable x; non-finite gradients still propagate
+// because every term is still added).  The thread therefore enumerates
+// n ascending, then (y sample, corner side), (x sample, side), (z sample,
+// side) ascending, which visits every nonzero term in replay order.
+//
+// Mapping: block = (image b, row Y, column X, 256 consecutive (Z, channel
+// vector) destinations); lanes test 64 boxes at a time against the column
+// (conservative per-axis voxel ranges from the end samples: the sample
+// coordinate is monotone in the sample index), then per relevant box the
+// exact hit masks come from one ballot per axis (lane = sample index).  The
+// terms g * ((wy * wx) * wz) are formed exactly as the replay forms them
+// (-ffp-contract=off).  Needs crop sizes <= 64 (one lane per sample).
+template <int VEC>
+__global__ __launch_bounds__(256) void crop_bwd_det_kernel(
+    const float* __restrict__ grads, const float* __restrict__ boxes,
+    const int32_t* __restrict__ box_ind, int64_t N, int ch, int cw, int cd, int B, int H, int W,
+    int D, int C, int method, int64_t blocks_per_col, float* __restrict__ gimg) {
+    const int CV = C / VEC;
+    const int lane = threadIdx.x & 63;
+    const int64_t ncols = (int64_t)B * H * W;
+    auto rdl = [](float v, int l) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    };
+    for (int64_t blk = blockIdx.x; blk < ncols * blocks_per_col; blk += gridDim.x) {
+        const int64_t col = blk / blocks_per_col;
+        const int64_t idx = (blk - col * blocks_per_col) * 256 + threadIdx.x;
+        const bool active = idx < (int64_t)D * CV;
+        const int Z = active ? (int)(idx / CV) : 0;
+        const int cv = active ? (int)(idx - (int64_t)Z * CV) : 0;
+        const int X = (int)(col % W);
+        const int Y = (int)((col / W) % H);
+        const int b = (int)(col / ((int64_t)H * W));
+        // this wave's destination Z range (for the conservative box test)
+        const int64_t wbase = (blk - col * blocks_per_col) * 256 + (threadIdx.x & ~63);
+        const int zw0 = (int)min<int64_t>(wbase / CV, D - 1);
+        const int zw1 = (int)min<int64_t>((wbase + 63) / CV, D - 1);
+        float acc[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
+        for (int64_t n0 = 0; n0 < N; n0 += 64) {
+            bool rel = false;
+            const int64_t nl = n0 + lane;
+            if (nl < N && box_ind[nl] == b) {
+                const float* bx = boxes + nl * 6;
+                auto cover = [](float b1, float b2, int S, int n, float lo_v, float hi_v) {
+                    const float sc = axis_scale(b1, b2, S, n);
+                    const float e0 = axis_coord(b1, b2, S, n, 0, sc);
+                    const float e1 = axis_coord(b1, b2, S, n, n - 1, sc);
+                    const float lo = fminf(e0, e1), hi = fmaxf(e0, e1);
+                    // NaN coordinates keep the box (the exact test then finds no sample)
+                    return !(hi_v < floorf(lo) || lo_v > ceilf(hi));
+                };
+                rel = cover(bx[0], bx[3], H, ch, (float)Y, (float)Y) &&
+                      cover(bx[1], bx[4], W, cw, (float)X, (float)X) &&
+                      cover(bx[2], bx[5], D, cd, (float)zw0, (float)zw1);
+            }
+            for (uint64_t rm = __ballot(rel); rm; rm &= rm - 1) {
+                const int64_t n = n0 + __builtin_ctzll(rm);
+                const float* bx = boxes + n * 6;
+                const float y1 = bx[0], x1 = bx[1], z1 = bx[2], y2 = bx[3], x2 = bx[4], z2 = bx[5];
+                // lane i: sample i of the y and x axes (make_sample's maths)
+                const float in_y = axis_coord(y1, y2, H, ch, lane, axis_scale(y1, y2, H, ch));
+                const float in_x = axis_coord(x1, x2, W, cw, lane, axis_scale(x1, x2, W, cw));
+                const bool vy = lane < ch && !(in_y < 0 || in_y > (float)(H - 1));
+                const bool vx = lane < cw && !(in_x < 0 || in_x > (float)(W - 1));
+                const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
+                const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+                const float yl = in_y - (float)ty, xl = in_x - (float)lx;
+                uint64_t myt, myb, mxl, mxr;
+                if (method == 1) {
+                    myt = __ballot(vy && (int)roundf(in_y) == Y);
+                    mxl = __ballot(vx && (int)roundf(in_x) == X);
+                    myb = mxr = 0;
+                } else {
+                    myt = __ballot(vy && ty == Y);
+                    myb = __ballot(vy && by == Y);
+                    mxl = __ballot(vx && lx == X);
+                    mxr = __ballot(vx && rx == X);
+                }
+                // (uniform from here to the per-thread z loops: the readlanes below
+                // must run with every lane active, or a value the compiler sinks into
+                // a divergent block is missing in the lanes that skipped it)
+                if (!(myt | myb) || !(mxl | mxr)) continue;
+                // this thread's z samples / corner sides (per thread: Z varies across lanes)
+                const float zsc = axis_scale(z1, z2, D, cd);
+                uint64_t mzf = 0, mzk = 0;
+                for (int i = 0; i < cd && active; ++i) {
+                    const float in_z = axis_coord(z1, z2, D, cd, i, zsc);
+                    if (in_z < 0 || in_z > (float)(D - 1)) continue;
+                    if (method == 1) {
+                        if ((int)roundf(in_z) == Z) mzf |= 1ull << i;
+                        continue;
+                    }
+                    if ((int)floorf(in_z) == Z) mzf |= 1ull << i;
+                    if ((int)ceilf(in_z) == Z) mzk |= 1ull << i;
+                }
+                const float* gn = grads + (size_t)n * ch * cw * cd * C + (size_t)cv * VEC;
+                if (method == 1) {                          // nearest: img[ny,nx,nz] += g
+                    for (uint64_t m1 = myt; m1; m1 &= m1 - 1)
+                        for (uint64_t m2 = mxl; m2; m2 &= m2 - 1) {
+                            const float* gyx = gn + ((size_t)__builtin_ctzll(m1) * cw + __builtin_ctzll(m2)) * cd * C;
+                            for (uint64_t m3 = mzf; m3; m3 &= m3 - 1) {
+                                const float* gr = gyx + (size_t)__builtin_ctzll(m3) * C;
+#pragma unroll
+                                for (int q = 0; q < VEC; ++q) acc[q] += gr[q];
+                            }
+                        }
+                    continue;
+                }
+                for (uint64_t m1 = myt | myb; m1; m1 &= m1 - 1) {
+                    const int iy = __builtin_ctzll(m1);
+                    const float yli = rdl(yl, iy);
+                    for (int a = 0; a < 2; ++a) {
+                        if (!(((a ? myb : myt) >> iy) & 1)) continue;
+                        const float wy = a ? yli : 1.0f - yli;
+                        for (uint64_t m2 = mxl | mxr; m2; m2 &= m2 - 1) {
+                            const int ix = __builtin_ctzll(m2);
+                            const float xli = rdl(xl, ix);
+                            for (int bb = 0; bb < 2; ++bb) {
+                                if (!(((bb ? mxr : mxl) >> ix) & 1)) continue;
+                                const float wyx = wy * (bb ? xli : 1.0f - xli);
+                                const float* gyx = gn + ((size_t)iy * cw + ix) * cd * C;
+                                for (uint64_t m3 = mzf | mzk; m3; m3 &= m3 - 1) {
+                                    const int iz = __builtin_ctzll(m3);
+                                    const float in_z = axis_coord(z1, z2, D, cd, iz, zsc);
+                                    const float zli = in_z - floorf(in_z);
+                                    const float* gr = gyx + (size_t)iz * C;
+                                    float gv[VEC];
+#pragma unroll
+                                    for (int q = 0; q < VEC; ++q) gv[q] = gr[q];
+                                    for (int cc = 0; cc < 2; ++cc) {
+                                        if (!(((cc ? mzk : mzf) >> iz) & 1)) continue;
+                                        const float w = wyx * (cc ? zli : 1.0f - zli);
+#pragma unroll
+                                        for (int q = 0; q < VEC; ++q) acc[q] += gv[q] * w;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (active) {
+            float* dst = gimg + ((((size_t)b * H + Y) * W + X) * D + Z) * C + (size_t)cv * VEC;
+            if constexpr (VEC == 4)
+                *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            else
+                dst[0] = acc[0];
+        }
     }
 }
 
@@ -758,10 +1073,26 @@ extern "C" int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* 
                                                m3d_stream_t s) {
     int rc = check_crop_args(B, H, W, D, C, ch, cw, cd, method);
     if (rc) return rc;
+    if (deterministic < 0 || deterministic > 2) return einval("deterministic must be 0, 1 or 2");
+    const int64_t total = N * ch * cw * cd;
+    if (deterministic == 1 && B > 0 && ch <= 64 && cw <= 64 && cd <= 64) {
+        // destination-owned sums in the replay order: writes every voxel (no zero fill)
+        const bool v4 = (C & 3) == 0;
+        const int64_t cvn = v4 ? C / 4 : C;
+        const int64_t bpc = (D * cvn + 255) / 256;
+        const int64_t nblk = B * H * W * bpc;
+        const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);
+        if (v4)
+            hipLaunchKernelGGL(crop_bwd_det_kernel<4>, dim3(grid), dim3(256), 0, st(s), grads, boxes, box_ind,
+                               N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, grad_image);
+        else
+            hipLaunchKernelGGL(crop_bwd_det_kernel<1>, dim3(grid), dim3(256), 0, st(s), grads, boxes, box_ind,
+                               N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, grad_image);
+        return check_launch("crop_bwd_det_kernel");
+    }
     if (hipMemsetAsync(grad_image, 0, sizeof(float) * (size_t)(B * H * W * D * C), st(s)) !=
         hipSuccess)
         return check_launch("memset grad_image");
-    const int64_t total = N * ch * cw * cd;
     if (total == 0 || B == 0) return M3D_OK;
     if (deterministic) {
         hipLaunchKernelGGL(crop_bwd_serial_kernel, dim3(grid_for(B * C, 256)), dim3(256), 0,
@@ -828,6 +1159,16 @@ extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
     if ((C & 3) == 0) {
         LineArgs a{nullptr, nullptr, boxes_adj, levels, N, B * N * ph * pw, 0, 0, 0, (int)C, ph, pw, pd,
                    0.0f, out};
+        const int mode = roi_region_mode();
+        if (mode && ph <= 64 && pw <= 64 && pd <= 64) {
+            switch (mode) {
+                case 2: launch_region_fwd<4, 4, 4>(a, P, B, st(s)); break;
+                case 3: launch_region_fwd<2, 2, 16>(a, P, B, st(s)); break;
+                case 4: launch_region_fwd<4, 4, 8>(a, P, B, st(s)); break;
+                default: launch_region_fwd<2, 2, 8>(a, P, B, st(s));
+            }
+            return check_launch("region_fwd_kernel");
+        }
         hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, st(s), a, P);
         return check_launch("line_fwd_kernel");
     }

@@ -25,6 +25,15 @@ from ._lib import check, ptr, stream
 LAYER_LOG = None
 
 
+# ReLU branch record for parity tests: when set to a dict, every conv unit
+# with a ReLU appends its output's sign mask (y > 0, on the host) under its
+# Keras layer name, in call order.  The float64 restatement can then take the
+# branches the GPU forward took (oracle/model_ref.RefRPN relu_masks): a
+# pre-activation within fp32 rounding of 0 otherwise flips the branch and moves
+# every gradient upstream of it.
+RELU_CAPTURE = None
+
+
 # Gradient-ready hook of the data-parallel path (m3d.parallel.OverlappedAllReduce):
 # when set, every conv unit registers its gradient tensors in forward
 # (use(key, tensors)) and reports them final once its backward has enqueued
@@ -576,8 +585,11 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     else:
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
-    return _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                            need_dx and x.requires_grad, link, halo, wshare)
+    y = _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
+                         need_dx and x.requires_grad, link, halo, wshare)
+    if RELU_CAPTURE is not None and relu:
+        RELU_CAPTURE.setdefault(layer.name, []).append((y.detach() > 0).cpu())
+    return y
 
 
 class _MaxPool(torch.autograd.Function):

@@ -64,7 +64,13 @@ def _crop_fwd(image, boxes, box_ind, crop_size, method, extrap):
 
 def crop_and_resize_3d_grad_image(grads, boxes, box_ind, image_size, T=torch.float32,
                                   method_name="trilinear", deterministic=False):
-    """grads [N,ch,cw,cd,C] -> d image [B,H,W,D,C] (zero-filled, then scatter)."""
+    """grads [N,ch,cw,cd,C] -> d image [B,H,W,D,C].
+
+    deterministic: False / 0 -- fp32 atomics (fast, last bits vary with arrival
+    order); True / 1 -- destination-owned sums in the reference's sequential
+    summation order (bit-identical to the wheel's CPU scatter, parallel over
+    voxels); 2 -- the single-thread-per-channel sequential replay (the same
+    bits, slow; kept as the in-library check of mode 1)."""
     _dev(grads, boxes, box_ind)
     if method_name not in _METHODS:
         raise ValueError("method must be 'trilinear' or 'nearest'")
@@ -74,7 +80,7 @@ def crop_and_resize_3d_grad_image(grads, boxes, box_ind, image_size, T=torch.flo
     out = torch.empty((B, H, W, D, C), device=grads.device, dtype=torch.float32)
     check(_L().m3d_crop_and_resize3d_bwd_image(ptr(grads), ptr(boxes), ptr(box_ind), N, ch, cw, cd,
                                                B, H, W, D, C, _METHODS[method_name],
-                                               1 if deterministic else 0, ptr(out), stream()),
+                                               int(deterministic), ptr(out), stream()),
           "crop_and_resize_3d_grad_image")
     return out.to(T) if T != torch.float32 else out
 

@@ -210,6 +210,34 @@ class SlabRPN:
         return {"rpn_class_logits": logits, "rpn_class": probs, "rpn_bbox": bbox, "rpn_rois": rois,
                 "feature_maps": fmaps}
 
+    def _proposals_async(self, out):
+        """The slab ProposalLayer (local top-k, candidate all-gather on the
+        group's own communicator, decode, 3-D NMS) launched right after the
+        forward on a side HIP stream, as RPN.proposals_async does for one
+        volume: it overlaps the backward.  Returns join() -> rpn_rois on the
+        current stream.  Host-staged (gloo) groups run it in line."""
+        m = self.model
+        probs, bbox = out["rpn_class"].detach(), out["rpn_bbox"].detach()
+        args = ([probs, bbox, m.anchors], self.sg, self.local_index)
+        if not probs.is_cuda or self.sg.host_staging:
+            rois = m.proposal_layer.call_slab(*args)
+            return lambda: rois
+        main = torch.cuda.current_stream(probs.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(probs.device)
+        side = self._side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            rois = m.proposal_layer.call_slab(*args)
+        probs.record_stream(side)
+        bbox.record_stream(side)
+
+        def join():
+            main.wait_stream(side)
+            rois.record_stream(main)
+            return rois
+        return join
+
     def train_step(self, image_slab, proposals=True, apply=True, overlap=True):
         """One sharded step.  The weight gradients (partial sums of one
         gradient) are SUM-all-reduced in buckets DURING the backward
@@ -229,6 +257,7 @@ class SlabRPN:
             mnn.GRAD_HOOK = hook
         try:
             out = self.forward(image_slab, proposals=False)
+            join = self._proposals_async(out) if proposals else None     # overlaps the backward
             lc, lb = m.losses(out, self.targets)
             total = lc * m.LOSS_WEIGHTS["rpn_class_loss"] + lb * m.LOSS_WEIGHTS["rpn_bbox_loss"]
             with slab.active(self.sg):          # halo gradients flow during backward
@@ -240,9 +269,8 @@ class SlabRPN:
             hook.finish()
         else:
             self.sg.all_reduce_sum_(m.store.grad_flat)
-        if proposals:
-            out["rpn_rois"] = m.proposal_layer.call_slab([out["rpn_class"], out["rpn_bbox"], m.anchors],
-                                                         self.sg, self.local_index)
+        if join is not None:
+            out["rpn_rois"] = join()
         if apply:
             m.optimizer_step()
         parts = torch.stack([total.detach(), lc.detach(), lb.detach()])

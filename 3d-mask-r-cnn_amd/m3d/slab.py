@@ -72,6 +72,16 @@ class SlabGroup:
         if host_staging is None:
             host_staging = self.world > 1 and dist.is_initialized() and dist.get_backend() == "gloo"
         self.host_staging = host_staging
+        # Own communicators (collective: every rank builds its SlabGroup): the
+        # halo P2P of the backward never queues behind the gradient buckets the
+        # overlapped all-reduce (default group) has in flight, and the proposal
+        # candidates' all-gather (launched on a side stream beside the backward)
+        # never sits between a halo exchange and its partner.
+        self.halo_group = self.coll_group = None
+        if self.world > 1 and dist.is_initialized():
+            ranks = list(range(self.world))
+            self.halo_group = dist.new_group(ranks)
+            self.coll_group = dist.new_group(ranks)
 
     @property
     def Dl(self):
@@ -93,12 +103,12 @@ class SlabGroup:
         ops, recv = [], [None, None]
         if self.lo is not None:
             recv[0] = self._buf(shape, like)
-            ops += [dist.P2POp(dist.isend, self._out(to_lo), self.lo),
-                    dist.P2POp(dist.irecv, recv[0], self.lo)]
+            ops += [dist.P2POp(dist.isend, self._out(to_lo), self.lo, self.halo_group),
+                    dist.P2POp(dist.irecv, recv[0], self.lo, self.halo_group)]
         if self.hi is not None:
             recv[1] = self._buf(shape, like)
-            ops += [dist.P2POp(dist.isend, self._out(to_hi), self.hi),
-                    dist.P2POp(dist.irecv, recv[1], self.hi)]
+            ops += [dist.P2POp(dist.isend, self._out(to_hi), self.hi, self.halo_group),
+                    dist.P2POp(dist.irecv, recv[1], self.hi, self.halo_group)]
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
@@ -112,7 +122,7 @@ class SlabGroup:
             return t[None]
         src = self._out(t)
         parts = [torch.empty_like(src) for _ in range(self.world)]
-        dist.all_gather(parts, src)
+        dist.all_gather(parts, src, group=self.coll_group)
         out = torch.stack(parts)
         return out.to(t.device) if out.device != t.device else out
 

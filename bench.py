@@ -342,6 +342,19 @@ def time_roi_align_bwd(fmaps, S, n_rois=128, reps=5, pools=(7, 14), hi=128):
                            "note": "bytes = 4|grads| + 4|P2..P5| + 8*C*touched voxel rows (per ROI); "
                                    "scatter_bytes = the per-sample 8-corner atomic form (4|grads| + 32|grads| "
                                    "+ 4|P2..P5|)"}
+        # CropAndResize3DGradImage itself (the op the TF binding calls) on P2 with
+        # all the ROIs: fast (atomic) mode vs deterministic mode 1 (destination-
+        # owned sums in the reference's order, bit-identical to the wheel)
+        g0 = grad[0].contiguous()
+        bi = torch.zeros(n_rois, dtype=torch.int32, device=g0.device)
+        bx = badj.reshape(-1, 6).contiguous()
+        shape2 = tuple(maps[0].shape)
+        tf = _event_time(lambda: ops.crop_and_resize_3d_grad_image(g0, bx, bi, shape2, deterministic=0), reps)
+        td = _event_time(lambda: ops.crop_and_resize_3d_grad_image(g0, bx, bi, shape2, deterministic=1), reps)
+        res[f"pool{p}"]["crop_grad_image_P2"] = {
+            "fast_atomic_ms": round(tf * 1e3, 4), "deterministic_ms": round(td * 1e3, 4),
+            "note": f"CropAndResize3DGradImage of {n_rois} ROIs x {p}^3 x C={C} into P2 {list(shape2)}; "
+                    "deterministic = mode 1 (bit-identical to the reference's sequential scatter)"}
     return res
 
 

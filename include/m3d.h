@@ -66,9 +66,14 @@ int m3d_crop_and_resize3d_fwd(const float* image, int64_t B, int64_t H, int64_t 
                               float extrapolation, float* crops /*[N,ch,cw,cd,C]*/,
                               m3d_stream_t s);
 
-/* grad_image is zero-filled by the callee.  deterministic=0: fp32 atomics;
- * deterministic=1: per-(image,channel) sequential replay in the reference's
- * box->y->x->z order (bit-exact vs the reference summation order, slow). */
+/* grad_image: every voxel written by the callee.  deterministic=0: zero fill +
+ * fp32 atomics (fast; the last bits vary with arrival order);
+ * deterministic=1: every output voxel row owned by one thread that adds its
+ * terms in the reference's sequential box->y->x->z->corner order (bit-identical
+ * to the wheel's CPU scatter, parallel over voxels, no atomics; crops <= 64
+ * per axis, larger crops fall back to mode 2); deterministic=2: the
+ * per-(image,channel) sequential replay of the same order (slow, the check of
+ * mode 1). */
 int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* boxes,
                                     const int32_t* box_ind, int64_t N, int32_t ch, int32_t cw,
                                     int32_t cd, int64_t B, int64_t H, int64_t W, int64_t D,

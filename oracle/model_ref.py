@@ -80,11 +80,17 @@ def upsample221(x):
 class RefRPN:
     """Functional restatement driven by a {keras_name: tensor} dict."""
 
-    def __init__(self, params, architecture="resnet50", dtype=torch.float64, apl=3):
+    def __init__(self, params, architecture="resnet50", dtype=torch.float64, apl=3, relu_masks=None):
+        """relu_masks: {layer name: [bool mask per call]} (m3d.nn.RELU_CAPTURE of
+        a GPU forward): each ReLU then takes the branches recorded there
+        (y * mask) instead of deciding them in this precision, so gradients
+        are compared on the same piecewise-linear branch."""
         self.p = {k: torch.as_tensor(np.asarray(v)).to(dtype) for k, v in params.items()}
         self.dtype = dtype
         self.arch = architecture
         self.apl = apl
+        self.relu_masks = relu_masks
+        self._calls = {}
 
     def _cb(self, x, conv, bn, stride=(1, 1, 1), padding="valid", relu=True, res=None):
         p = self.p
@@ -94,6 +100,13 @@ class RefRPN:
                           p[f"{bn}/moving_variance:0"])
         if res is not None:
             y = y + res
+        if relu and self.relu_masks is not None:
+            i = self._calls.get(conv, 0)
+            self._calls[conv] = i + 1
+            m = self.relu_masks[conv][i]
+            if tuple(m.shape) != tuple(y.shape):
+                raise ValueError(f"relu mask of {conv} call {i}: {tuple(m.shape)} vs {tuple(y.shape)}")
+            return y * m.to(y.dtype)
         return torch.relu(y) if relu else y
 
     def _block(self, x, stage, block, strides, shortcut):
@@ -138,6 +151,7 @@ class RefRPN:
         return logits, torch.softmax(logits, -1), torch.cat(bbox, 1)
 
     def forward(self, image):
+        self._calls = {}
         _, C2, C3, C4, C5 = self.backbone(image)
         fm = self.fpn(C2, C3, C4, C5)
         logits, probs, bbox = self.rpn_head(fm)

@@ -8,24 +8,18 @@ ToyDataset normalisation core/data_generators.py:1603-1630).
     same seed: rpn_match bit-exact, rpn_bbox to float32 log rounding;
   * the step's losses on those targets within 1e-4 of the float64 restatement
     of the Keras graph (oracle/model_ref.py) and its weight gradients held to
-    the bars of test_gpu_model.py (core/models.py:3320-3387);
+    gradparity.grad_parity's bars (core/models.py:3320-3387);
   * one full train_step (SGD) runs and moves the weights.
 The reference's own TF CPU path cannot run here."""
 import numpy as np
 import pytest
 import torch
 
+from gradparity import grad_parity, ref_grads
 from oracle import heads_ref as HR
-from oracle import model_ref as MR
 
 pytestmark = pytest.mark.gpu
 S = 64
-
-
-def rel_err(got, ref):
-    got = torch.as_tensor(got).detach().double().cpu()
-    ref = torch.as_tensor(ref).detach().double().cpu()
-    return float((got - ref).abs().max()) / (float(ref.abs().max()) + 1e-30)
 
 
 @pytest.fixture(scope="module")
@@ -69,41 +63,32 @@ def test_config0_rpn_targets_on_gpu(toy):
 
 
 def test_config0_step_losses_and_gradients(toy, cuda):
+    """The step on the GPU-built targets: losses within 1e-4 of the float64
+    restatement on the oracle's targets, gradients held to
+    gradparity.grad_parity's bars (the reference forward takes the GPU's
+    ReLU branches: the toy volume's 94 distinct input values put many
+    pre-activations within rounding of 0 -- a flipped branch in res5 moves
+    that block's gradients by 2 % for any fp32 implementation)."""
+    import m3d.nn as mnn
     cfg, model, image, gt, builder, t, rm, rb = toy
     model.store.zero_grad()
-    out = model.forward(image.to(cuda), proposals=False)
+    mnn.RELU_CAPTURE = {}
+    try:
+        out = model.forward(image.to(cuda), proposals=False)
+        masks = mnn.RELU_CAPTURE
+    finally:
+        mnn.RELU_CAPTURE = None
     lc, lb = model.losses(out, t)                      # device-resident targets, mask form
     (lc * 1.0 + lb * 1.5).backward()
     model.rpn.finish_backward()
     torch.cuda.synchronize()
-
-    def ref(dtype):
-        r = MR.RefRPN(model.store.state_dict(), dtype=dtype)
-        for p in model.store.params:
-            r.p[p.name].requires_grad_(True)
-        o = r.forward(image.to(dtype))
-        match = torch.from_numpy(rm.reshape(1, -1, 1))
-        rlc = MR.rpn_class_loss(match, o["rpn_class_logits"])
-        rlb = MR.rpn_bbox_loss(torch.from_numpy(rb[None]).to(dtype), match, o["rpn_bbox"])
-        (rlc * 1.0 + rlb * 1.5).backward()
-        return float(rlc), float(rlb), {k: v.grad for k, v in r.p.items()}
-    rlc, rlb, g64 = ref(torch.float64)
-    _, _, g32 = ref(torch.float32)
+    match, bbox = rm.reshape(1, -1, 1), rb[None]
+    rlc, rlb, g64 = ref_grads(model, image, match, bbox, torch.float64, masks)
+    _, _, g32 = ref_grads(model, image, match, bbox, torch.float32, masks)
     print(f"configs[0] losses GPU ({float(lc):.6f}, {float(lb):.6f}) fp64 ({rlc:.6f}, {rlb:.6f})", flush=True)
     assert abs(float(lc) - rlc) <= 1e-4 * abs(rlc)
     assert abs(float(lb) - rlb) <= 1e-4 * abs(rlb)
-    gpu, cpu32 = [], []
-    for p in model.store.params:
-        g_ref = g64[p.name]
-        if g_ref is None or float(g_ref.abs().max()) == 0.0:
-            continue
-        gpu.append((rel_err(p.grad, g_ref), p.name))
-        cpu32.append(rel_err(g32[p.name], g_ref))
-    gpu.sort(reverse=True)
-    med, med32 = float(np.median([e for e, _ in gpu])), float(np.median(cpu32))
-    print(f"configs[0] gradients: GPU median {med:.2e} worst {gpu[0]}, CPU fp32 median {med32:.2e}", flush=True)
-    assert med < 2e-4 and med <= 0.25 * med32, (med, med32)
-    assert gpu[0][0] <= max(1e-3, 4 * max(cpu32)), (gpu[:5], max(cpu32))
+    grad_parity(model, g64, g32, "configs[0]")
 
 
 def test_config0_train_step(toy, cuda):

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 import torch
 
+from gradparity import grad_parity, ref_grads
 from oracle import heads_ref as HR
 from oracle import model_ref as MR
 from oracle import ops_ref as R
@@ -203,32 +204,28 @@ def test_config2_pyramid_roi_align_and_grad_image(e2e128, cuda, pool):
     print(f"configs[2] pool {pool}: levels {np.bincount(lvl, minlength=6)[2:].tolist()}")
 
 
-def _ref_grads(model, image, match, bbox, dtype):
-    ref = MR.RefRPN(model.store.state_dict(), dtype=dtype)
-    for p in model.store.params:
-        ref.p[p.name].requires_grad_(True)
-    o = ref.forward(image.to(dtype))
-    m = torch.from_numpy(match)
-    rlc = MR.rpn_class_loss(m, o["rpn_class_logits"])
-    rlb = MR.rpn_bbox_loss(torch.from_numpy(bbox).to(dtype), m, o["rpn_bbox"])
-    (rlc * 1.0 + rlb * 1.5).backward()
-    return float(rlc), float(rlb), {k: (v.grad.clone() if v.grad is not None else None) for k, v in ref.p.items()}
-
-
 def test_config1_gradients_full_size(fwd128, cuda):
-    """configs[1]'s backward at its own shape (128^3, 1536 selected anchors):
-    the GPU step's two losses within 1e-4 of the float64 restatement, and every
-    weight gradient held to the bars of test_gpu_model.py at 64x64x8 -- the
-    median tensor error below a quarter of the CPU-fp32 restatement's median
-    (and below 2e-4), the worst tensor within 4x the CPU-fp32 worst
-    (core/models.py:3320-3387; fp32 itself drifts through ~60 layers of
-    relu-mask flips, so float64 is the truth and CPU fp32 the yardstick)."""
+    """configs[1]'s backward at its own shape (128^3, 1536 selected anchors,
+    core/models.py:3320-3387): the two losses within 1e-4 of the float64
+    restatement and every weight gradient held to grad_parity's bars.  The
+    float64 (and the CPU fp32 yardstick) forward takes the GPU's ReLU branches
+    (m3d.nn.RELU_CAPTURE): through ~60 layers a pre-activation within fp32
+    rounding of 0 flips its branch in any fp32 implementation and moves every
+    gradient upstream of it by up to 1e-2 (measured: the CPU fp32 restatement
+    against plain float64 has median 1.3e-4, worst 1.9e-3), which would hide
+    real errors behind branch noise."""
     import time
+    import m3d.nn as mnn
     from m3d.model import RPNTargets, synthetic_rpn_targets
     cfg, model, image, _ = fwd128
     match, bbox = synthetic_rpn_targets(model.anchors.shape[1], cfg.RPN_TRAIN_ANCHORS_PER_IMAGE, seed=2)
     model.store.zero_grad()
-    out = model.forward(image.to(cuda), proposals=False)
+    mnn.RELU_CAPTURE = {}
+    try:
+        out = model.forward(image.to(cuda), proposals=False)
+        masks = mnn.RELU_CAPTURE
+    finally:
+        mnn.RELU_CAPTURE = None
     lc, lb = model.losses(out, RPNTargets(match, bbox, cuda))
     (lc * 1.0 + lb * 1.5).backward()
     model.rpn.finish_backward()
@@ -236,23 +233,11 @@ def test_config1_gradients_full_size(fwd128, cuda):
     del out
     torch.set_num_threads(min(16, torch.get_num_threads()))
     t0 = time.time()
-    rlc, rlb, g64 = _ref_grads(model, image, match, bbox, torch.float64)
+    rlc, rlb, g64 = ref_grads(model, image, match, bbox, torch.float64, masks)
     print(f"configs[1] fp64 reference fwd+bwd {time.time() - t0:.1f} s", flush=True)
     t0 = time.time()
-    _, _, g32 = _ref_grads(model, image, match, bbox, torch.float32)
+    _, _, g32 = ref_grads(model, image, match, bbox, torch.float32, masks)
     print(f"configs[1] fp32 reference fwd+bwd {time.time() - t0:.1f} s", flush=True)
     assert abs(float(lc) - rlc) <= 1e-4 * abs(rlc), (float(lc), rlc)
     assert abs(float(lb) - rlb) <= 1e-4 * abs(rlb), (float(lb), rlb)
-    gpu, cpu32 = [], []
-    for p in model.store.params:
-        g_ref = g64[p.name]
-        if g_ref is None or float(g_ref.abs().max()) == 0.0:
-            continue
-        gpu.append((rel_err(p.grad.cpu().numpy(), g_ref.numpy()), p.name))
-        cpu32.append(rel_err(g32[p.name].numpy(), g_ref.numpy()))
-    gpu.sort(reverse=True)
-    med, med32 = float(np.median([e for e, _ in gpu])), float(np.median(cpu32))
-    print(f"configs[1] gradients: {len(gpu)} tensors, GPU median {med:.2e} worst {gpu[0]}, "
-          f"CPU fp32 median {med32:.2e} worst {max(cpu32):.2e}", flush=True)
-    assert med < 2e-4 and med <= 0.25 * med32, (med, med32)
-    assert gpu[0][0] <= max(1e-3, 4 * max(cpu32)), (gpu[:5], max(cpu32))
+    grad_parity(model, g64, g32, "configs[1]")

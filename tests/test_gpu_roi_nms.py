@@ -214,3 +214,50 @@ def test_crop_grad_boxes_bit_exact(cuda, C, crop):
     got = ops.crop_and_resize_3d_grad_boxes(T(g, cuda), T(img, cuda), T(boxes, cuda), T(bi, cuda)).cpu().numpy()
     want = R.crop_and_resize_3d_grad_boxes(g, img, boxes, bi)
     np.testing.assert_array_equal(got, want)
+
+
+def _det_case(rng, kind, B=2, H=9, W=7, D=11, N=23, crop=(5, 4, 3)):
+    lo = rng.uniform(-0.2, 0.9, (N, 3))
+    hi = lo + rng.uniform(0.02, 0.6, (N, 3))
+    boxes = np.concatenate([lo, hi], 1).astype(np.float32)
+    if kind == "flipped":
+        boxes[::3] = boxes[::3][:, [3, 4, 5, 0, 1, 2]]
+    if kind == "aligned":        # in = integer: floor == ceil, two corners on one voxel
+        q = rng.integers(0, 4, (N, 6)).astype(np.float32)
+        boxes = (q / np.array([H - 1, W - 1, D - 1] * 2, np.float32)).astype(np.float32)
+        boxes[:, 3:] = np.maximum(boxes[:, 3:], boxes[:, :3] + np.float32(2.0 / (H - 1)))
+    if kind == "tiny":           # 14 samples over ~1-2 voxels per axis (upsampling)
+        c = rng.uniform(0.1, 0.9, (N, 3))
+        boxes = np.concatenate([c, c + 1.5 / np.array([H, W, D])], 1).astype(np.float32)
+    bi = rng.integers(0, B, N).astype(np.int32)
+    return boxes, bi, (B, H, W, D)
+
+
+@pytest.mark.parametrize("kind,C,crop,method", [
+    ("random", 8, (5, 4, 3), "trilinear"), ("random", 3, (5, 4, 3), "trilinear"),
+    ("flipped", 8, (4, 6, 5), "trilinear"), ("aligned", 4, (7, 5, 9), "trilinear"),
+    ("tiny", 8, (14, 14, 14), "trilinear"), ("random", 8, (1, 4, 1), "trilinear"),
+    ("random", 8, (5, 4, 3), "nearest"), ("aligned", 5, (7, 5, 9), "nearest"),
+    ("random", 4, (3, 2, 70), "trilinear")])
+def test_grad_image_deterministic_parallel_bit_exact(cuda, kind, C, crop, method):
+    """CropAndResize3DGradImage deterministic mode 1 (destination-owned sums,
+    parallel, no atomics) is bit-identical to the sequential replay (mode 2)
+    and to the oracle's sequential scatter, on boxes partly outside the image,
+    flipped boxes, grid-aligned boxes (floor == ceil corners), upsampling
+    crops, size-1 axes, nearest mode, C % 4 != 0, several images, a NaN
+    gradient, and a crop > 64 samples (mode 1 falls back to mode 2)."""
+    from m3d import ops
+    rng = np.random.default_rng([ord(ch) for ch in kind] + [C, *crop, len(method)])
+    boxes, bi, (B, H, W, D) = _det_case(rng, kind)
+    N = len(boxes)
+    g = rng.normal(size=(N, *crop, C)).astype(np.float32)
+    if kind == "random" and C == 8:
+        g[2, 0, 0, 0, 1] = np.nan
+    shape = (B, H, W, D, C)
+    args = (torch.from_numpy(g).to(cuda), torch.from_numpy(boxes).to(cuda), torch.from_numpy(bi).to(cuda), shape)
+    par = ops.crop_and_resize_3d_grad_image(*args, method_name=method, deterministic=1).cpu().numpy()
+    ser = ops.crop_and_resize_3d_grad_image(*args, method_name=method, deterministic=2).cpu().numpy()
+    want = R.crop_and_resize_3d_grad_image(g, boxes, bi, shape, method)
+    np.testing.assert_array_equal(ser, want)
+    np.testing.assert_array_equal(par, want)
+    assert np.abs(np.nan_to_num(want)).sum() > 0
