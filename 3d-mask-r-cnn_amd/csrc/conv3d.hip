@@ -2943,6 +2943,127 @@ extern "C" int m3d_deconv3d_k2s2(const float* x, int64_t B, int64_t H, int64_t W
     return check_launch("conv_gemm_kernel(deconv)");
 }
 
+// ---- the one-channel 7^3 stem: conv1 (core/models.py:242, Conv3D(64, (7,7,7),
+// strides (2,2,1)) after ZeroPadding3D(3)) -------------------------------------
+// The implicit GEMM's scalar loader reaches 0.27 of the f32 MFMA peak here
+// (K = 343 taps of ONE channel: no channel vector to load).  This kernel keeps
+// the whole K operand on chip instead: the 343 x 64 weights live in LDS for
+// the life of a persistent workgroup (loaded once per CU), and each output
+// tile's input window (2x4 output columns x 32 z: 9 x 13 x 38 voxels, 17.8 KB)
+// is staged in LDS, prefetched through registers while the previous tile's
+// MFMAs run.  Wave w owns output column (oy0 + w/4, ox0 + w%4) x 32 z x 64
+// channels: per tap pair one A read (32 consecutive z of the window: lanes
+// broadcast-free), one ds_read_b64 of B (pair-interleaved layout: 64 lanes
+// read 512 contiguous bytes) and two v_mfma_f32_32x32x2_f32.  Epilogue =
+// epi_store (bias, z, frozen BN, ReLU), the same as the generic kernel.
+// Summation order: taps in Keras order (ky, kx, kz), pairs (t, t+1) -- exact
+// f32 FMA chain, a different order than the implicit GEMM (parity 1e-4).
+constexpr int STEM_TY = 2, STEM_TX = 4, STEM_TZ = 32;
+constexpr int STEM_WY = 2 * STEM_TY + 5, STEM_WX = 2 * STEM_TX + 5, STEM_WZ = STEM_TZ + 6;
+constexpr int STEM_WIN = STEM_WY * STEM_WX * STEM_WZ;            // 4446 floats
+constexpr int STEM_KP = 172;                                     // 343 taps -> 172 pairs
+constexpr int STEM_PER = (STEM_WIN + 511) / 512;                 // window values per thread
+
+__global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int ty_n, int tx_n, int tz_n,
+                                                       int64_t ntiles) {
+    __shared__ float wsh[STEM_KP * 128];          // [pair][h*32+l32][nb]  (88 KB)
+    __shared__ float win[STEM_WIN + 1];           // + one zero (the padding tap)
+    __shared__ int toff[2 * STEM_KP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, h = lane >> 5;
+    for (int i = tid; i < STEM_KP * 128; i += 512) {
+        const int kp = i >> 7, r = i & 127, nb = r & 1, hl = r >> 1, hh = hl >> 5, ll = hl & 31;
+        const int t = 2 * kp + hh;
+        wsh[i] = t < 343 ? p.w[t * 64 + nb * 32 + ll] : 0.0f;
+    }
+    for (int t = tid; t < 2 * STEM_KP; t += 512) {
+        const int ky = t / 49, kx = (t / 7) % 7, kz = t % 7;
+        toff[t] = t < 343 ? (ky * STEM_WX + kx) * STEM_WZ + kz : STEM_WIN;
+    }
+    if (tid == 0) win[STEM_WIN] = 0.0f;
+    const size_t plane = (size_t)p.D, row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    auto fetch = [&](int64_t tile, float* v) {
+        int64_t t = tile;
+        const int tz = (int)(t % tz_n); t /= tz_n;
+        const int tx = (int)(t % tx_n); t /= tx_n;
+        const int tyy = (int)(t % ty_n);
+        const int b = (int)(t / ty_n);
+        const int gy0 = 2 * tyy * STEM_TY - p.py, gx0 = 2 * tx * STEM_TX - p.px, gz0 = tz * STEM_TZ - p.pz;
+#pragma unroll
+        for (int q = 0; q < STEM_PER; ++q) {
+            const int i = tid + 512 * q;
+            float val = 0.0f;
+            if (i < STEM_WIN) {
+                const int iz = i % STEM_WZ, ixy = i / STEM_WZ, ix = ixy % STEM_WX, iy = ixy / STEM_WX;
+                const int gy = gy0 + iy, gx = gx0 + ix, gz = gz0 + iz;
+                if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && gz >= 0 && gz < p.D)
+                    val = p.a[b * img + gy * row + gx * plane + gz];
+            }
+            v[q] = val;
+        }
+    };
+    float pre[STEM_PER];
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) fetch(tile, pre);
+    for (; tile < ntiles; tile += gridDim.x) {
+        __syncthreads();                           // previous tile's window reads done
+#pragma unroll
+        for (int q = 0; q < STEM_PER; ++q)
+            if (tid + 512 * q < STEM_WIN) win[tid + 512 * q] = pre[q];
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x, pre);   // next window in flight
+        int64_t t = tile;
+        const int tz = (int)(t % tz_n); t /= tz_n;
+        const int tx = (int)(t % tx_n); t /= tx_n;
+        const int tyy = (int)(t % ty_n);
+        const int b = (int)(t / ty_n);
+        const int oy = tyy * STEM_TY + (wave >> 2), ox = tx * STEM_TX + (wave & 3), oz0 = tz * STEM_TZ;
+        const float* wa = win + ((2 * (wave >> 2)) * STEM_WX + 2 * (wave & 3)) * STEM_WZ + l32;
+        floatx16 acc0 = {}, acc1 = {};
+#pragma unroll 4
+        for (int kp = 0; kp < STEM_KP; ++kp) {
+            const int o = toff[2 * kp + h];
+            const float a = o < STEM_WIN ? wa[o] : 0.0f;
+            const float2 bv = *reinterpret_cast<const float2*>(wsh + kp * 128 + lane * 2);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc1, 0, 0, 0);
+        }
+        if (oy >= p.OH || ox >= p.OW) continue;
+        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int oz = oz0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (oz < p.OD) {
+                epi_store(p, e, mbase + oz, l32, acc0[r]);
+                epi_store(p, e, mbase + oz, 32 + l32, acc1[r]);
+            }
+        }
+    }
+}
+
+static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, int sx, int sz, int dly, int dlx,
+                    int dlz, int res_mode, int64_t split_n, int64_t ldy) {
+    static const int env = [] { const char* v = getenv("M3D_STEM_MFMA"); return v ? atoi(v) : 1; }();
+    return env && Cin == 1 && kh == 7 && kw == 7 && kd == 7 && Cout == 64 && sy == 2 && sx == 2 && sz == 1 &&
+           dly == 1 && dlx == 1 && dlz == 1 && res_mode == 0 && split_n <= 0 && (ldy <= 0 || ldy == 64);
+}
+
+static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int ty_n = (p.OH + STEM_TY - 1) / STEM_TY, tx_n = (p.OW + STEM_TX - 1) / STEM_TX;
+    const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
+    const int64_t ntiles = (int64_t)p.B * ty_n * tx_n * tz_n;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, ncu);
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, ty_n, tx_n, tz_n, ntiles);
+    return check_launch("stem_fwd_kernel");
+}
+
 extern "C" int m3d_conv3d_fwd_dil(const float* x, int64_t B, int64_t H, int64_t W, int64_t D,
                                   int64_t Cin, const float* w, int32_t kh, int32_t kw, int32_t kd,
                                   int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
@@ -2980,6 +3101,7 @@ extern "C" int m3d_conv3d_fwd_dil(const float* x, int64_t B, int64_t H, int64_t 
     p.dly = dly; p.dlx = dlx; p.dlz = dlz;
     Epi e{bias, bn_scale, bn_shift, residual, res_mode, act_code, z_out, y, ldy > 0 ? ldy : Cout,
           y2, ldy2, (int)split_n, (int)OH, (int)OW, (int)OD, 1, 1, 1, 0, 1};
+    if (stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, dly, dlx, dlz, res_mode, split_n, ldy)) return launch_stem(p, e, st(s));
     if (Cin % 32 == 0) dispatch_gemm<false, true>(p, e, st(s));
     else dispatch_gemm<false, false>(p, e, st(s));
     return check_launch("conv_gemm_kernel(fwd)");

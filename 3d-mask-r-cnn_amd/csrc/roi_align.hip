@@ -275,6 +275,168 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(LineArgs a, Pyr P) {
     }
 }
 
+// owner voxel index of a sample coordinate along an axis of S voxels (samples
+// outside the map go to the nearest end voxel: every sample has one owner)
+__device__ __forceinline__ int owner_idx(float in, int S) {
+    return in >= 0.0f ? (in <= (float)(S - 1) ? (int)floorf(in) : S - 1) : 0;
+}
+
+struct RegionBase {
+    int64_t base[4];             // first (y, x) column bucket of each level (B-major inside)
+};
+
+// ---- PyramidROIAlign forward, channel-sliced line kernel --------------------------
+// line_fwd_kernel<true> with the channels cut into SL slices and the grid
+// ordered slice-major: while slice s runs, the feature-map bytes in play are
+// 1/SL of the maps (P2 at 256^3: 1.07 GB -> 134 MB for SL = 8), so rows that
+// overlapping ROIs read again come from the memory-side cache instead of HBM.
+// A wave holds SL lines (consecutive x of one y) x one slice: 64/SL lanes per
+// line, float4 each (C = 256: SL = 8 -> 128 B rows, one L2 line).  Per-sample
+// arithmetic as line_fwd_kernel (bit-identical).  Needs C % (4 * 64 / SL) == 0
+// ... and C/4 == 64 (C = 256) for the lane split below.
+template <int SL>
+__global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, const int32_t* __restrict__ perm,
+                                                          int zs) {
+    constexpr int LPL = 64 / SL;                      // lanes (float4) per line slice
+    // blocks: SL slices in dispatch order, each a multiple of 8 blocks remapped
+    // XCD-contiguously within the slice (hardware XCD = block % 8); a line is
+    // cut into zs z-parts (more, shorter dependent load chains in flight)
+    const int64_t items = a.lines * zs;
+    const int64_t waves_per_slice = (items + SL - 1) / SL;
+    const int64_t bs8 = ((waves_per_slice + 3) / 4 + 7) / 8 * 8;
+    const int slice = (int)(blockIdx.x / bs8);
+    const int64_t lr = blockIdx.x - (int64_t)slice * bs8;
+    const int64_t wv = ((lr % 8) * (bs8 / 8) + lr / 8) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (slice >= SL || wv >= waves_per_slice) return;
+    const int64_t item = wv * SL + lane / LPL;
+    if (item >= items) return;
+    int64_t line = item / zs;
+    const int part = (int)(item - line * zs);
+    const int zb = part * a.cd / zs, ze = (part + 1) * a.cd / zs;
+    if (perm) line = perm[line];                      // spatially sorted line order
+    const int c = slice * LPL + (lane % LPL);         // float4 index within the voxel
+    int64_t t = line;
+    const int x = (int)(t % a.cw); t /= a.cw;
+    const int y = (int)(t % a.ch);
+    const int64_t n = t / a.ch;
+    const int l = a.levels[n] - 2;
+    const int H = P.H[l], W = P.W[l], D = P.D[l];
+    const float* img = P.fmaps[l] + (size_t)(n / a.N) * H * W * D * a.C;
+    const float* box = a.boxes + n * 6;
+    const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
+    const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
+    const float in_x = axis_coord(x1, x2, W, a.cw, x, axis_scale(x1, x2, W, a.cw));
+    const float zsc = axis_scale(z1, z2, D, a.cd);
+    const int C4 = a.C >> 2;
+    float4* o = reinterpret_cast<float4*>(a.out + line * (int64_t)a.cd * a.C);
+    const bool yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
+    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
+    if (yx_oob) {
+        for (int z = zb; z < ze; ++z) st_nt(o + (int64_t)z * C4 + c, ex);
+        return;
+    }
+    const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
+    const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+    const float yl = in_y - (float)ty, xl = in_x - (float)lx;
+    const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
+    const float4* base = reinterpret_cast<const float4*>(img);
+    const float4* col[4] = {base + ty * rowW + lx * rowD, base + ty * rowW + rx * rowD,
+                            base + by * rowW + lx * rowD, base + by * rowW + rx * rowD};
+    int pk = -1;
+    float4 kv[4];
+    for (int z = zb; z < ze; ++z) {
+        const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
+        float4 r;
+        if (in_z < 0 || in_z > (float)(D - 1)) {
+            r = ex;
+        } else {
+            const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+            const float zl = in_z - (float)fz;
+            float4 fv[4];
+            if (fz == pk) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fv[q] = kv[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
+            }
+            if (kz != fz) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) kv[q] = fv[q];
+            }
+            pk = kz;
+            r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
+            r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
+        }
+        st_nt(o + (int64_t)z * C4 + c, r);
+    }
+}
+
+// Spatial order of the lines (m3d_pyramid_roi_align3d_fwd_ws): a counting sort
+// by the owner (y, x) column of each line -- bucket = level base + (b, ty, lx)
+// in raster order -- so lines of different, overlapping ROIs that read the
+// same feature-map columns run next to each other, on one XCD (its L2).  The
+// order inside a bucket comes from atomics; every line writes only its own
+// output, so the result does not depend on it.
+__global__ void line_key_kernel(LineArgs a, Pyr P, RegionBase rb, int32_t* __restrict__ keys,
+                                int32_t* __restrict__ counts) {
+    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= a.lines) return;
+    int64_t t = L;
+    const int x = (int)(t % a.cw); t /= a.cw;
+    const int y = (int)(t % a.ch);
+    const int64_t n = t / a.ch;
+    const int l = a.levels[n] - 2;
+    const int H = P.H[l], W = P.W[l];
+    const int64_t b = n / a.N;
+    const float* box = a.boxes + n * 6;
+    const int ty = owner_idx(axis_coord(box[0], box[3], H, a.ch, y, axis_scale(box[0], box[3], H, a.ch)), H);
+    const int lx = owner_idx(axis_coord(box[1], box[4], W, a.cw, x, axis_scale(box[1], box[4], W, a.cw)), W);
+    const int32_t k = (int32_t)(rb.base[l] + (b * H + ty) * W + lx);
+    keys[L] = k;
+    atomicAdd(counts + k, 1);
+}
+
+// exclusive prefix sum of counts[0..n) into offs, one workgroup of 1024
+__global__ __launch_bounds__(1024) void excl_scan_kernel(const int32_t* __restrict__ counts, int64_t n,
+                                                         int32_t* __restrict__ offs) {
+    __shared__ int32_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024;
+    const int64_t i0 = tid * per, i1 = min<int64_t>(n, i0 + per);
+    int32_t sum = 0;
+    for (int64_t i = i0; i < i1; ++i) sum += counts[i];
+    part[tid] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int32_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int32_t run = part[tid] - sum;
+    for (int64_t i = i0; i < i1; ++i) {
+        offs[i] = run;
+        run += counts[i];
+    }
+}
+
+__global__ void line_scatter_kernel(const int32_t* __restrict__ keys, int64_t lines, int32_t* __restrict__ offs,
+                                    int32_t* __restrict__ perm) {
+    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= lines) return;
+    perm[atomicAdd(offs + keys[L], 1)] = (int32_t)L;
+}
+
+static int roi_slices() {
+    static const int env = [] { const char* e = getenv("M3D_ROI_SLICES"); return e ? atoi(e) : 8; }();
+    return env;
+}
+
 // ---- PyramidROIAlign forward, region-major --------------------------------------
 // The ROI-major line kernel reads each ROI's own corner rows once, but rows
 // shared by overlapping ROIs are fetched again for every ROI (PMC traffic 2x
@@ -293,11 +455,6 @@ struct RegionGrid {
     int64_t off[5];              // first block of each level
     int gy[4], gx[4], gz[4];     // blocks per axis and level
 };
-
-// owner voxel index of a sample coordinate along an axis of S voxels
-__device__ __forceinline__ int owner_idx(float in, int S) {
-    return in >= 0.0f ? (in <= (float)(S - 1) ? (int)floorf(in) : S - 1) : 0;
-}
 
 template <int TY, int TX, int TZ>
 __global__ __launch_bounds__(256) void region_fwd_kernel(LineArgs a, Pyr P, RegionGrid G) {
@@ -405,10 +562,11 @@ __global__ __launch_bounds__(256) void region_fwd_kernel(LineArgs a, Pyr P, Regi
     }
 }
 
-// block shape of the region-major forward: M3D_ROI_REGION = 0 (off: line kernel),
-// 1 (2x2x8, default), 2 (4x4x4), 3 (2x2x16), 4 (4x4x8)
+// block shape of the region-major forward: M3D_ROI_REGION = 0 (off: line kernel,
+// default -- measured 3x slower at 256^3), 1 (2x2x8), 2 (4x4x4),
+// 3 (2x2x16), 4 (4x4x8)
 static int roi_region_mode() {
-    static const int env = [] { const char* e = getenv("M3D_ROI_REGION"); return e ? atoi(e) : 1; }();
+    static const int env = [] { const char* e = getenv("M3D_ROI_REGION"); return e ? atoi(e) : 0; }();
     return env;
 }
 
@@ -1139,19 +1297,33 @@ static int make_pyr(Pyr& P, const float* const fmaps[4], float* const gmaps[4],
     return M3D_OK;
 }
 
-extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
-                                           const int64_t fshape[4][3], int64_t C,
-                                           const float* boxes, const float* image_meta,
-                                           int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
-                                           int32_t pw, int32_t pd, float* out, float* boxes_adj,
-                                           int32_t* levels, m3d_stream_t s) {
+// workspace of the spatially sorted line order (m3d_pyramid_roi_align3d_fwd_ws)
+static size_t pyr_sort_layout(const int64_t fshape[4][3], int64_t B, int64_t N, int32_t ph, int32_t pw,
+                              int64_t* nbuckets, int64_t* lines) {
+    int64_t nb = 0;
+    for (int l = 0; l < 4; ++l) nb += B * fshape[l][0] * fshape[l][1];
+    const int64_t nl = B * N * ph * pw;
+    if (nbuckets) *nbuckets = nb;
+    if (lines) *lines = nl;
+    return sizeof(int32_t) * (size_t)(2 * nb + 2 * nl) + 256;
+}
+
+extern "C" size_t m3d_pyramid_roi_align3d_fwd_workspace_bytes(const int64_t fshape[4][3], int64_t B, int64_t N,
+                                                              int32_t ph, int32_t pw) {
+    return pyr_sort_layout(fshape, B, N, ph, pw, nullptr, nullptr);
+}
+
+static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4][3], int64_t C,
+                            const float* boxes, const float* image_meta, int64_t meta_stride, int64_t B,
+                            int64_t N, int32_t ph, int32_t pw, int32_t pd, float* out, float* boxes_adj,
+                            int32_t* levels, void* workspace, size_t ws_bytes, hipStream_t s) {
     Pyr P;
     int rc = make_pyr(P, fmaps, nullptr, fshape);
     if (rc) return rc;
     if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
     if (meta_stride < 8) return einval("image_meta must have at least 8 columns");
     if (B * N == 0) return M3D_OK;
-    hipLaunchKernelGGL(pyramid_prep_kernel, dim3(grid_for(B * N, 256)), dim3(256), 0, st(s),
+    hipLaunchKernelGGL(pyramid_prep_kernel, dim3(grid_for(B * N, 256)), dim3(256), 0, s,
                        boxes, image_meta, meta_stride, B, N, boxes_adj, levels);
     rc = check_launch("pyramid_prep_kernel");
     if (rc) return rc;
@@ -1159,22 +1331,78 @@ extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
     if ((C & 3) == 0) {
         LineArgs a{nullptr, nullptr, boxes_adj, levels, N, B * N * ph * pw, 0, 0, 0, (int)C, ph, pw, pd,
                    0.0f, out};
+        const int sl = roi_slices();
+        if (C == 256 && (sl == 2 || sl == 4 || sl == 8 || sl == 16)) {
+            const int32_t* perm = nullptr;
+            int64_t nb = 0, nl = 0;
+            const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
+            static const int sort_env = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : 0; }();
+            if (sort_env && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
+                int32_t* counts = (int32_t*)workspace;
+                int32_t* offs = counts + nb;
+                int32_t* keys = offs + nb;
+                int32_t* pm = keys + nl;
+                RegionBase rb;
+                int64_t acc = 0;
+                for (int l = 0; l < 4; ++l) {
+                    rb.base[l] = acc;
+                    acc += B * fshape[l][0] * fshape[l][1];
+                }
+                if (hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)nb, s) != hipSuccess)
+                    return check_launch("memset line buckets");
+                hipLaunchKernelGGL(line_key_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, a, P, rb, keys, counts);
+                hipLaunchKernelGGL(excl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nb, offs);
+                hipLaunchKernelGGL(line_scatter_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, keys, nl, offs, pm);
+                rc = check_launch("line sort");
+                if (rc) return rc;
+                perm = pm;
+            }
+            static const int zs_env = [] { const char* e = getenv("M3D_ROI_ZSPLIT"); return e ? atoi(e) : 1; }();
+            const int zs = std::max(1, std::min(zs_env, (int)pd));
+            const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
+            const unsigned grid = (unsigned)(bs8 * sl);
+            if (sl == 2) hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
+            else if (sl == 4) hipLaunchKernelGGL(line_fwd_sl_kernel<4>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
+            else if (sl == 16) hipLaunchKernelGGL(line_fwd_sl_kernel<16>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
+            else hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
+            return check_launch("line_fwd_sl_kernel");
+        }
         const int mode = roi_region_mode();
         if (mode && ph <= 64 && pw <= 64 && pd <= 64) {
             switch (mode) {
-                case 2: launch_region_fwd<4, 4, 4>(a, P, B, st(s)); break;
-                case 3: launch_region_fwd<2, 2, 16>(a, P, B, st(s)); break;
-                case 4: launch_region_fwd<4, 4, 8>(a, P, B, st(s)); break;
-                default: launch_region_fwd<2, 2, 8>(a, P, B, st(s));
+                case 2: launch_region_fwd<4, 4, 4>(a, P, B, s); break;
+                case 3: launch_region_fwd<2, 2, 16>(a, P, B, s); break;
+                case 4: launch_region_fwd<4, 4, 8>(a, P, B, s); break;
+                default: launch_region_fwd<2, 2, 8>(a, P, B, s);
             }
             return check_launch("region_fwd_kernel");
         }
-        hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, st(s), a, P);
+        hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, s, a, P);
         return check_launch("line_fwd_kernel");
     }
-    hipLaunchKernelGGL(pyramid_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, st(s), P,
+    hipLaunchKernelGGL(pyramid_fwd_kernel, dim3(grid_for(total, 4)), dim3(256), 0, s, P,
                        (int)C, boxes_adj, levels, N, total, ph, pw, pd, out);
     return check_launch("pyramid_fwd_kernel");
+}
+
+extern "C" int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4],
+                                           const int64_t fshape[4][3], int64_t C,
+                                           const float* boxes, const float* image_meta,
+                                           int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
+                                           int32_t pw, int32_t pd, float* out, float* boxes_adj,
+                                           int32_t* levels, m3d_stream_t s) {
+    return pyramid_fwd_impl(fmaps, fshape, C, boxes, image_meta, meta_stride, B, N, ph, pw, pd, out,
+                            boxes_adj, levels, nullptr, 0, st(s));
+}
+
+extern "C" int m3d_pyramid_roi_align3d_fwd_ws(const float* const fmaps[4], const int64_t fshape[4][3],
+                                              int64_t C, const float* boxes, const float* image_meta,
+                                              int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
+                                              int32_t pw, int32_t pd, float* out, float* boxes_adj,
+                                              int32_t* levels, void* workspace, size_t ws_bytes,
+                                              m3d_stream_t s) {
+    return pyramid_fwd_impl(fmaps, fshape, C, boxes, image_meta, meta_stride, B, N, ph, pw, pd, out,
+                            boxes_adj, levels, workspace, ws_bytes, st(s));
 }
 
 extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,

@@ -36,6 +36,9 @@ _SIGS = {
                                         c_i64, c_i32, c_i32, c_i32, c_p, c_p],
     "m3d_pyramid_roi_align3d_fwd": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_i32,
                                     c_i32, c_p, c_p, c_p, c_p],
+    "m3d_pyramid_roi_align3d_fwd_ws": [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_i32,
+                                       c_i32, c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_pyramid_roi_align3d_fwd_workspace_bytes": [c_p, c_i64, c_i64, c_i32, c_i32],
     "m3d_pyramid_roi_align3d_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p,
                                     c_i64, c_p],
     "m3d_mask_targets3d": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_i32,
@@ -130,6 +133,7 @@ _SIGS = {
     "m3d_get_deterministic": [],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
+             "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32,

@@ -23,6 +23,9 @@ from ._lib import check, ptr, stream
 # the MFMA work of the algorithm actually run (the 64 batched GEMMs for a
 # Winograd layer); compulsory bytes = input + weights + residual + output.
 LAYER_LOG = None
+# with LAYER_LOG: also bracket every logged launch group with HIP events
+# (bench.py step_roofline: measured time per layer beside its roofline time)
+LAYER_TIMING = False
 
 
 # ReLU branch record for parity tests: when set to a dict, every conv unit
@@ -87,9 +90,32 @@ def _grad_done(grads, side=None):
             h[0].done(h[1])
 
 
-def _log(kind, direct_flops, exec_flops, nbytes):
+def _span():
+    """Start event of a logged launch group (LAYER_TIMING): recorded on the
+    current stream before the group's first launch; None when not timing."""
+    if LAYER_LOG is None or not LAYER_TIMING:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _log(kind, direct_flops, exec_flops, nbytes, phase="fwd", name="", t0=None):
+    """Append (kind, direct_flops, executed_flops, compulsory_bytes, phase, name,
+    start_event, end_event) to LAYER_LOG; the end event is recorded on the
+    current stream right after the group's launches (both None when not timing)."""
     if LAYER_LOG is not None:
-        LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes)))
+        t1 = None
+        if t0 is not None:
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record()
+        LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes), phase, name, t0, t1))
+
+
+def _wino_exec(B, OH, OW, OD, cin, cout, nz):
+    """MFMA FLOPs of the Winograd point GEMMs, F(2x2xnz): 16*(nz+2) points."""
+    tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // nz)
+    return 2.0 * 16 * (nz + 2) * tiles * cin * cout
 
 
 def _L():
@@ -318,7 +344,9 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, halo=None,
-                wshare=None):
+                wshare=None, name=""):
+        t0 = _span()
+        ctx.name = name
         B, H, W, D, Cin = x.shape
         # depth slab (m3d.slab): halo = (planes [B,H,W,2,C], has_lo, has_hi) read by the
         # Winograd kernels beside x instead of a halo-extended copy of x
@@ -392,11 +420,9 @@ class _ConvBNAct(torch.autograd.Function):
             direct = 2.0 * (y.numel() // Cout) * kh * kw * kd * Cin * Cout
             exe = direct
             if ctx.wino:
-                nz = int(_L().m3d_conv3d_wino_tile_z())
-                tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // nz)
-                exe = 2.0 * 16 * (nz + 2) * tiles * Cin * Cout
+                exe = _wino_exec(B, OH, OW, OD, Cin, Cout, int(_L().m3d_conv3d_wino_tile_z()))
             nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
-            _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb)
+            _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb, "fwd", name, t0)
         ctx.save_for_backward(x, w, y, z)
         ctx.wshare = wshare
         if wshare is not None and ctx.wino and halo is None and need_dx:
@@ -420,6 +446,9 @@ class _ConvBNAct(torch.autograd.Function):
         L = _L()
         need_res = ctx.res_mode != 0
         trivial = ctx.bn is None and not ctx.relu
+        logging = LAYER_LOG is not None
+        direct = 2.0 * M * kh * kw * kd * Cin * Cout
+        t0 = _span()
         if trivial:
             dz = dy
             dres = dy if need_res else None
@@ -434,6 +463,10 @@ class _ConvBNAct(torch.autograd.Function):
                 mean, rstd, scale = ctx.bn
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
+        if logging:
+            nel = dy.numel() * (1 + (0 if trivial else 1 + (ctx.relu or ctx.bn is not None) +
+                                     (z is not None) + (dres is not None and not trivial)))
+            _log("bn_act_bwd", 0, 0, 4.0 * nel, "bwd_bn", ctx.name, t0)
         side = _wgrad_stream(x.device) if grads.get("kernel") is not None else None
         if side is not None:
             dz.record_stream(side)
@@ -445,6 +478,7 @@ class _ConvBNAct(torch.autograd.Function):
         if ctx.wino:
             if grads.get("kernel") is not None:
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    tw = _span()
                     if min(Cin, Cout) < WINO_WGRAD_MIN_C:
                         xw, gw = x, geo
                         if halo is not None:        # the direct kernel reads the halo-extended slab
@@ -474,7 +508,13 @@ class _ConvBNAct(torch.autograd.Function):
                                                                geo.pad[2], ptr(grads["kernel"]), ptr(wsw),
                                                                wswb, stream()),
                                   "conv3d_bwd_weight_wino")
+                    if logging:
+                        exe = direct if min(Cin, Cout) < WINO_WGRAD_MIN_C else \
+                            _wino_exec(B, OH, OW, OD, Cin, Cout, 2)
+                        _log("wino_wgrad", direct, exe, 4.0 * (x.numel() + dz.numel() + w.numel()),
+                             "bwd_weight", ctx.name, tw)
                 ctx.u = None
+            td = _span()
             ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             dx = None
             if ctx.need_dx:
@@ -493,18 +533,27 @@ class _ConvBNAct(torch.autograd.Function):
                                                        geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, stream()),
                           "conv3d_bwd_data_wino")
                     _shared_wino_release(ctx.wshare)
+                if logging:
+                    _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_tile_z())),
+                         4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)), "bwd_data", ctx.name, td)
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             ctx.halo = None
-            return dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None, None
+            return (dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None,
+                    None, None)
         if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                tw = _span()
                 check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                               OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
                                               stream()), "conv3d_bwd_weight")
+                if logging:
+                    _log(f"conv{kh}_wgrad", direct, direct, 4.0 * (x.numel() + dz.numel() + w.numel()),
+                         "bwd_weight", ctx.name, tw)
         dx = None
         link = ctx.link
         acc = 0
+        td = _span()
         if ctx.need_dx:
             strided = any(s != 1 for s in geo.stride)
             dx, acc = _link_take(link, x)                     # dx = parked gradient + conv^T dz
@@ -531,6 +580,9 @@ class _ConvBNAct(torch.autograd.Function):
                 check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
                                             OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
                       "conv3d_bwd_data")
+            if logging:
+                _log(f"conv{kh}_dgrad", direct, direct, 4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)),
+                     "bwd_data", ctx.name, td)
             dx = _link_park(link, dx, acc)
         _grad_done(grads, side)
         dr = None
@@ -541,10 +593,12 @@ class _ConvBNAct(torch.autograd.Function):
                 dr = dres
             else:
                 rb, rh, rw, rd, rc = ctx.res_shape
+                tu = _span()
                 dr = torch.empty(ctx.res_shape, device=dy.device, dtype=torch.float32)
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
-        return dx, dr, None, None, None, None, None, None, None, None, None, None, None
+                _log("upsample_bwd", 0, 0, 4.0 * (dres.numel() + dr.numel()), "bwd_data", ctx.name, tu)
+        return dx, dr, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _slab_extend(x, geo):
@@ -586,7 +640,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     y = _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                         need_dx and x.requires_grad, link, halo, wshare)
+                         need_dx and x.requires_grad, link, halo, wshare, layer.name)
     if RELU_CAPTURE is not None and relu:
         RELU_CAPTURE.setdefault(layer.name, []).append((y.detach() > 0).cpu())
     return y
@@ -595,12 +649,13 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
 class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, stride, pad, out):
+        t0 = _span()
         B, H, W, D, C = x.shape
         y = torch.empty((B, *out, C), device=x.device, dtype=torch.float32)
         am = torch.empty((B, *out, C), device=x.device, dtype=torch.uint8)
         check(_L().m3d_maxpool3d_fwd(ptr(x), B, H, W, D, C, *k, *stride, *pad, *out, ptr(y), ptr(am),
                                      stream()), "maxpool3d_fwd")
-        _log("maxpool", 0, 0, 4.0 * (x.numel() + y.numel()))
+        _log("maxpool", 0, 0, 4.0 * (x.numel() + y.numel()), "fwd", "pool1", t0)
         ctx.save_for_backward(am)
         ctx.cfg = (tuple(x.shape), k, stride, pad, out)
         return y
@@ -609,9 +664,11 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         (am,) = ctx.saved_tensors
         shape, k, stride, pad, out = ctx.cfg
+        t0 = _span()
         dx = torch.empty(shape, device=dy.device, dtype=torch.float32)
         check(_L().m3d_maxpool3d_bwd(ptr(dy.contiguous()), ptr(am), *shape, *k, *stride, *pad, *out,
                                      ptr(dx), stream()), "maxpool3d_bwd")
+        _log("maxpool_bwd", 0, 0, 4.0 * (dy.numel() + dx.numel()) + am.numel(), "bwd_data", "pool1", t0)
         return dx, None, None, None, None
 
 
@@ -632,18 +689,21 @@ class _Subsample221(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x):
+        t0 = _span()
         B, H, W, D, C = x.shape
         y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, D, C), device=x.device, dtype=torch.float32)
         check(_L().m3d_subsample221_fwd(ptr(x), B, H, W, D, C, ptr(y), stream()), "subsample221")
-        _log("subsample", 0, 0, 4.0 * (x.numel() + y.numel()))
+        _log("subsample", 0, 0, 4.0 * (x.numel() + y.numel()), "fwd", "fpn_p6", t0)
         ctx.shape = tuple(x.shape)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        t0 = _span()
         dx = torch.zeros(ctx.shape, device=dy.device, dtype=torch.float32)
         check(_L().m3d_subsample221_bwd(ptr(dy.contiguous()), *ctx.shape, ptr(dx), stream()),
               "subsample221_bwd")
+        _log("subsample_bwd", 0, 0, 4.0 * (dy.numel() + dx.numel()), "bwd_data", "fpn_p6", t0)
         return dx
 
 
@@ -659,6 +719,7 @@ class _RPNOut(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, w24, b24, grads, apl, *shared):
+        t0 = _span()
         dev = shared[0].device
         B = shared[0].shape[0]
         rows = [s.shape[1] * s.shape[2] * s.shape[3] for s in shared]
@@ -680,7 +741,8 @@ class _RPNOut(torch.autograd.Function):
                 off += r
         if LAYER_LOG is not None:
             f = 2.0 * B * sum(rows) * Cin * 8 * apl
-            _log("conv1", f, f, 4.0 * (sum(s.numel() for s in shared) + w24.numel() + logits.numel() + bbox.numel()))
+            _log("conv1", f, f, 4.0 * (sum(s.numel() for s in shared) + w24.numel() + logits.numel() + bbox.numel()),
+                 "fwd", "rpn_class_raw+rpn_bbox_pred", t0)
         ctx.save_for_backward(w24, *shared)
         ctx.grads, ctx.rows, ctx.apl = grads, rows, apl
         return logits, bbox
@@ -698,6 +760,7 @@ class _RPNOut(torch.autograd.Function):
             dlogits = torch.zeros((B, sum(rows) * apl, 2), device=dev)
         if dbbox is None:
             dbbox = torch.zeros((B, sum(rows) * apl, 6), device=dev)
+        t0 = _span()
         w_pad = torch.nn.functional.pad(w24.reshape(Cin, n_out), (0, npad - n_out))
         dshared = [torch.empty_like(s) for s in shared]
         L = _L()
@@ -725,4 +788,9 @@ class _RPNOut(torch.autograd.Function):
                                             W, D, 1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(),
                                             0, stream()), "rpn_out_dgrad")
                 off += r
+        if LAYER_LOG is not None:
+            f = 2.0 * B * R * Cin * n_out
+            nx = sum(s.numel() for s in shared)
+            _log("conv1_bwd", 2 * f, 2 * f, 4.0 * (2 * nx + 2 * B * R * npad + 2 * w24.numel()), "bwd_data",
+                 "rpn_class_raw+rpn_bbox_pred (wgrad+dgrad)", t0)
         return (None, None, None, None) + tuple(dshared)

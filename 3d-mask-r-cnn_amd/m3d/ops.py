@@ -220,9 +220,12 @@ class _PyramidROIAlign(torch.autograd.Function):
         levels = torch.empty((B, N), device=p2.device, dtype=torch.int32)
         fptrs = (_lib.c_p * 4)(*[f.data_ptr() for f in fmaps])
         fshape = ((_lib.c_i64 * 3) * 4)(*[(_lib.c_i64 * 3)(*f.shape[1:4]) for f in fmaps])
-        check(_L().m3d_pyramid_roi_align3d_fwd(fptrs, fshape, C, ptr(boxes), ptr(image_meta),
-                                               image_meta.shape[1], B, N, ph, pw, pd, ptr(out),
-                                               ptr(boxes_adj), ptr(levels), stream()),
+        # workspace of the spatially sorted line order (overlapping ROIs share rows in L2)
+        wsb = int(_L().m3d_pyramid_roi_align3d_fwd_workspace_bytes(fshape, B, N, ph, pw))
+        ws = torch.empty(wsb, device=boxes.device, dtype=torch.uint8)
+        check(_L().m3d_pyramid_roi_align3d_fwd_ws(fptrs, fshape, C, ptr(boxes), ptr(image_meta),
+                                                  image_meta.shape[1], B, N, ph, pw, pd, ptr(out),
+                                                  ptr(boxes_adj), ptr(levels), ptr(ws), wsb, stream()),
               "pyramid_roi_align")
         ctx.save_for_backward(boxes_adj, levels)
         ctx.shapes = [tuple(f.shape) for f in fmaps]

@@ -95,8 +95,10 @@ class KerasOptimizer:
         return self._state
 
     def step(self, store):
+        from . import nn as mnn
         L = _lib.load()
         s = self.state(store)
+        t0 = mnn._span()
         common = (store.n_chunks, store.seg_of_chunk.data_ptr(), store.l2_coef.data_ptr(), len(store.params))
         if self.kind == "SGD":
             rc = L.m3d_sgd_keras(store.flat.data_ptr(), store.grad_flat.data_ptr(), s[0].data_ptr(), *common,
@@ -115,4 +117,8 @@ class KerasOptimizer:
                                       float(self.params["epsilon"]), self.clipnorm, store.norms.data_ptr(),
                                       _lib.stream())
         _lib.check(rc, self.kind.lower())
+        # compulsory bytes: read w, g and the slots, write w and the slots (+ the clip-norm read of g)
+        nslot = len(s)
+        mnn._log("optimizer", 0, 0, 4.0 * store.total * (2 + 2 * nslot + 1 + (self.clipnorm > 0)),
+                 "optimizer", self.kind, t0)
         self.iterations += 1

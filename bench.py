@@ -524,6 +524,12 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
            "volumes_per_s": round(steps / el, 4), "scaling": "strong",
            "loss": round(float(r["loss"]), 6),
            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    if world == 1:
+        try:
+            out["step_roofline"] = step_roofline(model, lambda: srpn.train_step(image, proposals=proposals),
+                                                 el / steps * 1e3, os.environ.get("M3D_STEP_ROOFLINE_TABLE_256"))
+        except Exception as e:  # report, never hide
+            out["step_roofline"] = {"error": repr(e)}
     del model, srpn, image
     torch.cuda.empty_cache()
     return out
@@ -550,9 +556,9 @@ def fwd_roofline(model, image, reps=3):
         rec, mnn.LAYER_LOG = mnn.LAYER_LOG, None
         with torch.no_grad():
             t = _event_time(fn, reps)
-        t_exec = sum(max(fe / (F32_MFMA_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9)) for _, _, fe, b in rec)
-        t_dir = sum(max(fd / (F32_MFMA_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9)) for _, fd, _, b in rec)
-        nb = sum(b for *_, b in rec)
+        t_exec = sum(max(r_[2] / (F32_MFMA_PEAK_TFLOPS * 1e12), r_[3] / (HBM_PEAK_GBS * 1e9)) for r_ in rec)
+        t_dir = sum(max(r_[1] / (F32_MFMA_PEAK_TFLOPS * 1e12), r_[3] / (HBM_PEAK_GBS * 1e9)) for r_ in rec)
+        nb = sum(r_[3] for r_ in rec)
         stages[name] = {"ms": round(t * 1e3, 3), "layers": len(rec),
                         "direct_tflop": round(sum(r_[1] for r_ in rec) / 1e12, 4),
                         "executed_tflop": round(sum(r_[2] for r_ in rec) / 1e12, 4),
@@ -571,6 +577,59 @@ def fwd_roofline(model, image, reps=3):
                        "frac_roofline": round(roof / tot_ms, 4),
                        "compulsory_gb": round(sum(v["compulsory_gb"] for v in stages.values()), 3)}
     return stages
+
+
+def step_roofline(model, run_step, ms_per_step, table_path=None):
+    """Roofline of the whole headline step (forward + backward + optimizer;
+    SURVEY.md 8d per-layer form): one extra instrumented step logs every
+    launch group (m3d.nn.LAYER_LOG with LAYER_TIMING: conv forward, BN/ReLU
+    backward, data gradient, weight gradient, pooling / resampling, the fused
+    RPN output heads, the optimizer) with its executed MFMA FLOPs and
+    compulsory HBM bytes, bracketed by HIP events on the stream it runs on.
+    t_roof = sum_l max(F_l / P_f32mfma, B_l / P_hbm); frac = t_roof /
+    ms_per_step (the timed headline step).  Per layer the measured time sits
+    beside its roofline time; 'top_gaps' lists the five largest differences
+    (weight gradients run on a side stream concurrently with the data-gradient
+    chain, so measured times overlap and their sum exceeds the step).  The
+    loss, the ProposalLayer (side stream, latency-bound) and the gradient
+    zero-fill are not logged: the roofline is a lower bound."""
+    from m3d import nn as mnn
+    mnn.LAYER_LOG, mnn.LAYER_TIMING = [], True
+    try:
+        run_step()
+        torch.cuda.synchronize()
+        rec = mnn.LAYER_LOG
+    finally:
+        mnn.LAYER_LOG, mnn.LAYER_TIMING = None, False
+    pf, pb = F32_MFMA_PEAK_TFLOPS * 1e12, HBM_PEAK_GBS * 1e9
+    rows, phases = [], {}
+    for kind, fd, fe, nb, phase, name, e0, e1 in rec:
+        tr = max(fe / pf, nb / pb)
+        tm = e0.elapsed_time(e1) / 1e3 if e0 is not None else None
+        rows.append({"layer": name, "kind": kind, "phase": phase, "flop": fe, "bytes": nb,
+                     "bound": "mfma" if fe / pf >= nb / pb else "hbm",
+                     "roof_us": round(tr * 1e6, 2), "meas_us": None if tm is None else round(tm * 1e6, 2)})
+        ph = phases.setdefault(phase, {"launch_groups": 0, "roof_ms": 0.0, "meas_ms": 0.0, "tflop": 0.0, "gb": 0.0})
+        ph["launch_groups"] += 1
+        ph["roof_ms"] += tr * 1e3
+        ph["meas_ms"] += (tm or 0.0) * 1e3
+        ph["tflop"] += fe / 1e12
+        ph["gb"] += nb / 1e9
+    for ph in phases.values():
+        for k in ("roof_ms", "meas_ms", "tflop", "gb"):
+            ph[k] = round(ph[k], 3)
+    roof = sum(r["roof_us"] for r in rows) / 1e3
+    gaps = sorted((r for r in rows if r["meas_us"] is not None), key=lambda r: r["meas_us"] - r["roof_us"],
+                  reverse=True)[:5]
+    if table_path:
+        with open(table_path, "w") as f:
+            json.dump({"ms_per_step": ms_per_step, "step_roofline_ms": roof, "rows": rows}, f, indent=0)
+    return {"step_roofline_ms": round(roof, 3), "ms_per_step": round(ms_per_step, 3),
+            "frac": round(roof / ms_per_step, 4), "launch_groups": len(rows), "phases": phases,
+            "top_gaps": [{k: r[k] for k in ("layer", "kind", "phase", "bound", "roof_us", "meas_us")} for r in gaps],
+            "peaks": {"f32_mfma_tflops": F32_MFMA_PEAK_TFLOPS, "hbm_gbs": HBM_PEAK_GBS},
+            "note": "sum over launch groups of max(executed MFMA FLOPs / f32 MFMA peak, compulsory bytes / HBM "
+                    "peak) / ms_per_step; Winograd layers priced at their executed GEMM FLOPs"}
 
 
 def roi_leg_large(S, dev, n_rois=512):
@@ -790,6 +849,11 @@ def main():
                       "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
                       "anchors": int(model.anchors.shape[1]),
                       "hip_graph": bool(world == 1 and args.graph)}}
+    if world == 1 and not args.no_extras:
+        try:
+            out["step_roofline"] = step_roofline(model, step, ms, os.environ.get("M3D_STEP_ROOFLINE_TABLE"))
+        except Exception as e:  # report, never hide
+            out["step_roofline"] = {"error": repr(e)}
     if world > 1 and not args.no_extras:
         try:
             ar = time_allreduce(model.store.grad_flat, world)

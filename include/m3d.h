@@ -101,6 +101,18 @@ int m3d_pyramid_roi_align3d_fwd(const float* const fmaps[4], const int64_t fshap
                                 int32_t pw, int32_t pd, float* out /*[B,N,ph,pw,pd,C]*/,
                                 float* boxes_adj, int32_t* levels, m3d_stream_t s);
 
+/* The same forward with a workspace (>= the _workspace_bytes size, device
+ * memory, caller-owned): the ROI lines are first counting-sorted by the
+ * feature-map column they read, so overlapping ROIs share their rows through
+ * L2 (bit-identical output; the order only changes which cache serves them). */
+size_t m3d_pyramid_roi_align3d_fwd_workspace_bytes(const int64_t fshape[4][3], int64_t B, int64_t N,
+                                                   int32_t ph, int32_t pw);
+int m3d_pyramid_roi_align3d_fwd_ws(const float* const fmaps[4], const int64_t fshape[4][3],
+                                   int64_t C, const float* boxes, const float* image_meta,
+                                   int64_t meta_stride, int64_t B, int64_t N, int32_t ph,
+                                   int32_t pw, int32_t pd, float* out, float* boxes_adj,
+                                   int32_t* levels, void* workspace, size_t ws_bytes, m3d_stream_t s);
+
 /* gmaps[l] are zero-filled by the callee, then receive the image gradient. */
 int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
                                 const int32_t* levels, int64_t B, int64_t N, int32_t ph,
