@@ -2947,96 +2947,145 @@ extern "C" int m3d_deconv3d_k2s2(const float* x, int64_t B, int64_t H, int64_t W
 // strides (2,2,1)) after ZeroPadding3D(3)) -------------------------------------
 // The implicit GEMM's scalar loader reaches 0.27 of the f32 MFMA peak here
 // (K = 343 taps of ONE channel: no channel vector to load).  This kernel keeps
-// the whole K operand on chip instead: the 343 x 64 weights live in LDS for
-// the life of a persistent workgroup (loaded once per CU), and each output
-// tile's input window (2x4 output columns x 32 z: 9 x 13 x 38 voxels, 17.8 KB)
-// is staged in LDS, prefetched through registers while the previous tile's
-// MFMAs run.  Wave w owns output column (oy0 + w/4, ox0 + w%4) x 32 z x 64
-// channels: per tap pair one A read (32 consecutive z of the window: lanes
-// broadcast-free), one ds_read_b64 of B (pair-interleaved layout: 64 lanes
-// read 512 contiguous bytes) and two v_mfma_f32_32x32x2_f32.  Epilogue =
-// epi_store (bias, z, frozen BN, ReLU), the same as the generic kernel.
-// Summation order: taps in Keras order (ky, kx, kz), pairs (t, t+1) -- exact
-// f32 FMA chain, a different order than the implicit GEMM (parity 1e-4).
-constexpr int STEM_TY = 2, STEM_TX = 4, STEM_TZ = 32;
-constexpr int STEM_WY = 2 * STEM_TY + 5, STEM_WX = 2 * STEM_TX + 5, STEM_WZ = STEM_TZ + 6;
-constexpr int STEM_WIN = STEM_WY * STEM_WX * STEM_WZ;            // 4446 floats
-constexpr int STEM_KP = 172;                                     // 343 taps -> 172 pairs
-constexpr int STEM_PER = (STEM_WIN + 511) / 512;                 // window values per thread
+// the whole K operand on chip: the 343 x 64 weights live in LDS for the life
+// of a persistent workgroup (loaded once per CU), and every wave owns one
+// output column (oy, ox) x 32 z x 64 channels with its own input window (the
+// 49 (ky, kx) rows x 38 z voxels, + one zero row) in its own LDS region,
+// refilled from registers prefetched during the previous tile's MFMAs.  No
+// barrier after the weight load: the waves of a CU run out of phase.
+// K order: the two MFMA k-slots (lane halves h) walk (ky, kx) rows R = rp and
+// R = rp + 25 in step, 7 taps kz each -- so a lane's window offset is
+// R * 38 + kz: one add per row, the 7 taps as ds_read immediates (a
+// per-tap index walk cost more issue than the MFMAs).  Row R = 49 is the
+// padding (zero weights, zero window row).  Epilogue: each 32-channel
+// accumulator is staged in the wave's LDS region (row stride 40 floats:
+// the lane halves, 4 rows apart, land 32 banks apart) and leaves as
+// row-contiguous float4s through epi_store4 (bias, z, frozen BN, ReLU).
+// Summation order: K in the (R pair, kz) order above -- an exact f32 FMA
+// chain, a different order than the implicit GEMM (parity 1e-4).
+constexpr int STEM_TZ = 32;
+constexpr int STEM_WZ = STEM_TZ + 6;                             // 38
+constexpr int STEM_WIN = 50 * STEM_WZ;                           // 49 rows + the zero row: 1900 floats
+constexpr int STEM_RP = 25;                                      // row pairs (R, R + 25)
+constexpr int STEM_NP = STEM_RP * 7;                             // 175 k pairs
+constexpr int STEM_PER = (49 * STEM_WZ + 63) / 64;               // window values per lane (30)
+constexpr int STEM_SLD = 40;                                     // epilogue staging row stride
 
-__global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int ty_n, int tx_n, int tz_n,
-                                                       int64_t ntiles) {
-    __shared__ float wsh[STEM_KP * 128];          // [pair][h*32+l32][nb]  (88 KB)
-    __shared__ float win[STEM_WIN + 1];           // + one zero (the padding tap)
-    __shared__ int toff[2 * STEM_KP];
+__global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
+    __shared__ float wsh[STEM_NP * 128];          // [pair][h*32+l32][nb]  (89.6 KB)
+    __shared__ float win[8][STEM_WIN];            // one window / staging region per wave (60.8 KB)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, h = lane >> 5;
-    for (int i = tid; i < STEM_KP * 128; i += 512) {
+    for (int i = tid; i < STEM_NP * 128; i += 512) {
         const int kp = i >> 7, r = i & 127, nb = r & 1, hl = r >> 1, hh = hl >> 5, ll = hl & 31;
-        const int t = 2 * kp + hh;
-        wsh[i] = t < 343 ? p.w[t * 64 + nb * 32 + ll] : 0.0f;
+        const int R = kp / 7 + STEM_RP * hh, kz = kp % 7;
+        wsh[i] = R < 49 ? p.w[(R * 7 + kz) * 64 + nb * 32 + ll] : 0.0f;
     }
-    for (int t = tid; t < 2 * STEM_KP; t += 512) {
-        const int ky = t / 49, kx = (t / 7) % 7, kz = t % 7;
-        toff[t] = t < 343 ? (ky * STEM_WX + kx) * STEM_WZ + kz : STEM_WIN;
-    }
-    if (tid == 0) win[STEM_WIN] = 0.0f;
+    float* ww = win[wave];
+    if (lane < STEM_WZ) ww[49 * STEM_WZ + lane] = 0.0f;   // the padding row
+    __syncthreads();                              // the only barrier: waves run free below
     const size_t plane = (size_t)p.D, row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
+        tz = (int)(t % tz_n); t /= tz_n;
+        ox = (int)(t % p.OW); t /= p.OW;
+        oy = (int)(t % p.OH);
+        b = (int)(t / p.OH);
+    };
     auto fetch = [&](int64_t tile, float* v) {
-        int64_t t = tile;
-        const int tz = (int)(t % tz_n); t /= tz_n;
-        const int tx = (int)(t % tx_n); t /= tx_n;
-        const int tyy = (int)(t % ty_n);
-        const int b = (int)(t / ty_n);
-        const int gy0 = 2 * tyy * STEM_TY - p.py, gx0 = 2 * tx * STEM_TX - p.px, gz0 = tz * STEM_TZ - p.pz;
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
+        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
+        const float* xb = p.a + b * img;
 #pragma unroll
         for (int q = 0; q < STEM_PER; ++q) {
-            const int i = tid + 512 * q;
+            const int i = lane + 64 * q;
             float val = 0.0f;
-            if (i < STEM_WIN) {
-                const int iz = i % STEM_WZ, ixy = i / STEM_WZ, ix = ixy % STEM_WX, iy = ixy / STEM_WX;
-                const int gy = gy0 + iy, gx = gx0 + ix, gz = gz0 + iz;
+            if (i < 49 * STEM_WZ) {
+                const int R = i / STEM_WZ, iz = i - R * STEM_WZ;
+                const int gy = gy0 + R / 7, gx = gx0 + R % 7, gz = gz0 + iz;
                 if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && gz >= 0 && gz < p.D)
-                    val = p.a[b * img + gy * row + gx * plane + gz];
+                    val = xb[gy * row + gx * plane + gz];
             }
             v[q] = val;
         }
     };
+    const int64_t w0 = (int64_t)blockIdx.x * 8 + wave, wstride = (int64_t)gridDim.x * 8;
+    float4 ebias[2], escale[2], eshift[2];
+    for (int nb = 0; nb < 2; ++nb) {
+        const int n = nb * 32 + 4 * (lane & 7);
+        ebias[nb] = e.bias ? ld4(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        escale[nb] = e.scale ? ld4(e.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+        eshift[nb] = e.scale ? ld4(e.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float pre[STEM_PER];
-    int64_t tile = blockIdx.x;
-    if (tile < ntiles) fetch(tile, pre);
-    for (; tile < ntiles; tile += gridDim.x) {
-        __syncthreads();                           // previous tile's window reads done
+    if (w0 < ntiles) fetch(w0, pre);
+    for (int64_t tile = w0; tile < ntiles; tile += wstride) {
 #pragma unroll
         for (int q = 0; q < STEM_PER; ++q)
-            if (tid + 512 * q < STEM_WIN) win[tid + 512 * q] = pre[q];
-        __syncthreads();
-        if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x, pre);   // next window in flight
-        int64_t t = tile;
-        const int tz = (int)(t % tz_n); t /= tz_n;
-        const int tx = (int)(t % tx_n); t /= tx_n;
-        const int tyy = (int)(t % ty_n);
-        const int b = (int)(t / ty_n);
-        const int oy = tyy * STEM_TY + (wave >> 2), ox = tx * STEM_TX + (wave & 3), oz0 = tz * STEM_TZ;
-        const float* wa = win + ((2 * (wave >> 2)) * STEM_WX + 2 * (wave & 3)) * STEM_WZ + l32;
+            if (lane + 64 * q < 49 * STEM_WZ) ww[lane + 64 * q] = pre[q];
+        __builtin_amdgcn_wave_barrier();
+        if (tile + wstride < ntiles) fetch(tile + wstride, pre);      // next window in flight
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
         floatx16 acc0 = {}, acc1 = {};
-#pragma unroll 4
-        for (int kp = 0; kp < STEM_KP; ++kp) {
-            const int o = toff[2 * kp + h];
-            const float a = o < STEM_WIN ? wa[o] : 0.0f;
-            const float2 bv = *reinterpret_cast<const float2*>(wsh + kp * 128 + lane * 2);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc1, 0, 0, 0);
-        }
-        if (oy >= p.OH || ox >= p.OW) continue;
-        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
+        const float* wa = ww + STEM_RP * STEM_WZ * h + l32;           // row R = rp + 25 h
+        const float* wb = wsh + lane * 2;
+        for (int rp = 0; rp < STEM_RP; ++rp) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int oz = oz0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (oz < p.OD) {
-                epi_store(p, e, mbase + oz, l32, acc0[r]);
-                epi_store(p, e, mbase + oz, 32 + l32, acc1[r]);
+            for (int kz = 0; kz < 7; ++kz) {
+                const float a = wa[kz];
+                const float2 bv = *reinterpret_cast<const float2*>(wb + kz * 128);
+#if defined(M3D_STEM_DBG) && M3D_STEM_DBG == 2
+                acc0[kz] += a * bv.x;             // timing probe: no MFMA
+                acc1[kz] += a * bv.y;
+#else
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc1, 0, 0, 0);
+#endif
             }
+            wa += STEM_WZ;
+            wb += 7 * 128;
+        }
+        __builtin_amdgcn_wave_barrier();          // window reads done before the staging writes
+#if defined(M3D_STEM_DBG) && M3D_STEM_DBG == 1
+        {   // timing probe: no epilogue (one store per lane keeps the MFMAs live)
+            float t = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t += acc0[r] + acc1[r];
+            if (t == 1.2345f) e.y[lane] = t;
+            continue;
+        }
+#endif
+        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
+        const int oz0 = tz * STEM_TZ;
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const floatx16& acc = nb ? acc1 : acc0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ww[((r & 3) + 8 * (r >> 2) + 4 * h) * STEM_SLD + l32] = acc[r];
+            __builtin_amdgcn_wave_barrier();
+            // a lane's 4 channels are the same in every row it stores (c4 = lane & 7):
+            // the epilogue parameters are held in registers (epi_store4's order of ops)
+            const int n = nb * 32 + 4 * (lane & 7);
+            const float4 bb = ebias[nb], sc = escale[nb], sh = eshift[nb];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {                 // 32 rows x 8 float4 = 4 per lane
+                const int rr = (lane >> 3) + 8 * q;
+                float4 v = *reinterpret_cast<const float4*>(ww + rr * STEM_SLD + 4 * (lane & 7));
+                if (oz0 + rr >= p.OD) continue;
+                const int64_t m = mbase + oz0 + rr;
+                if (e.bias) { v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w; }
+                if (e.z) st4(e.z + m * 64 + n, v);
+                if (e.scale) {
+                    v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
+                    v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
+                }
+                if (e.relu) {
+                    v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
+                }
+                st4(e.y + m * 64 + n, v);
+            }
+            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -3044,6 +3093,8 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int ty_n,
 static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, int sx, int sz, int dly, int dlx,
                     int dlz, int res_mode, int64_t split_n, int64_t ldy) {
     static const int env = [] { const char* v = getenv("M3D_STEM_MFMA"); return v ? atoi(v) : 1; }();
+    // the kernel's own epilogue covers bias / z / frozen BN / activation, plain
+    // [M, 64] stores (no residual, split or accumulate)
     return env && Cin == 1 && kh == 7 && kw == 7 && kd == 7 && Cout == 64 && sy == 2 && sx == 2 && sz == 1 &&
            dly == 1 && dlx == 1 && dlz == 1 && res_mode == 0 && split_n <= 0 && (ldy <= 0 || ldy == 64);
 }
@@ -3056,11 +3107,10 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
             n = 256;
         return n;
     }();
-    const int ty_n = (p.OH + STEM_TY - 1) / STEM_TY, tx_n = (p.OW + STEM_TX - 1) / STEM_TX;
     const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
-    const int64_t ntiles = (int64_t)p.B * ty_n * tx_n * tz_n;
-    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, ncu);
-    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, ty_n, tx_n, tz_n, ntiles);
+    const int64_t ntiles = (int64_t)p.B * p.OH * p.OW * tz_n;
+    const unsigned grid = (unsigned)std::min<int64_t>((ntiles + 7) / 8, ncu);
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, tz_n, ntiles);
     return check_launch("stem_fwd_kernel");
 }
 

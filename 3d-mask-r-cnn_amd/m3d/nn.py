@@ -640,9 +640,9 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     y = _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                         need_dx and x.requires_grad, link, halo, wshare, layer.name)
+                         need_dx and x.requires_grad, link, halo, wshare, getattr(layer, "name", ""))
     if RELU_CAPTURE is not None and relu:
-        RELU_CAPTURE.setdefault(layer.name, []).append((y.detach() > 0).cpu())
+        RELU_CAPTURE.setdefault(getattr(layer, "name", ""), []).append((y.detach() > 0).cpu())
     return y
 
 
