@@ -238,18 +238,20 @@ class SlabRPN:
             return rois
         return join
 
-    def train_step(self, image_slab, proposals=True, apply=True, overlap=True):
+    def train_step(self, image_slab, proposals=True, apply=True, overlap=True, force_hook=False):
         """One sharded step.  The weight gradients (partial sums of one
         gradient) are SUM-all-reduced in buckets DURING the backward
         (OverlappedAllReduce, as the data-parallel path) -- the halo exchanges
         and the bucket all-reduces then share the backward.  apply=False stops
-        before the optimizer (tests compare the reduced gradient)."""
+        before the optimizer (tests compare the reduced gradient); force_hook:
+        the overlapped all-reduce also for a one-rank group (exercises the
+        collective path on one GPU)."""
         from . import nn as mnn
         from . import slab
         m = self.model
         m.store.zero_grad()
         hook = None
-        if self.sg.world > 1 and overlap:
+        if (self.sg.world > 1 or force_hook) and overlap:
             hook = getattr(self, "_hook", None)
             if hook is None:
                 hook = self._hook = OverlappedAllReduce(m.store, self.sg.world, average=False)

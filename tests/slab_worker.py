@@ -11,6 +11,8 @@ Modes:
                                     the flat gradient saved as .npy under OUT.
   slab_worker.py cmp OUT S D REF    (torchrun) the sharded step compared with
                                     the saved unsharded one (memory-mapped).
+  slab_worker.py nccl OUT D         (torchrun, 1 rank, RCCL) the slab step with
+                                    the overlapped all-reduce forced on.
 """
 import json
 import os
@@ -124,9 +126,37 @@ def mode_cmp(out_dir, S, D, ref_dir):
     dist.destroy_process_group()
 
 
+def mode_nccl(out_dir, D):
+    """One rank on RCCL ("nccl"; RCCL refuses two ranks on one GPU): the slab
+    step with the overlapped SUM all-reduce forced on (force_hook) and the
+    slab ProposalLayer on its side stream, against the plain step."""
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    dev, model, image, match, bbox = setup(64, D, 3000, 400, 512)
+    full, loss_full, g_full = full_step(model, image, match, bbox, dev)
+    from m3d import slab
+    from m3d.parallel import SlabRPN
+    sg = slab.SlabGroup(D)
+    srpn = SlabRPN(model, sg, match, bbox)
+    r = srpn.train_step(srpn.slice(image), proposals=True, apply=False, force_hook=True)
+    torch.cuda.synchronize()
+    g = model.store.grad_flat.detach()
+    res = {"backend": dist.get_backend(), "world": dist.get_world_size(),
+           "hook_used": getattr(srpn, "_hook", None) is not None,
+           "rois_bitexact": bool(torch.equal(r["rpn_rois"], full["rpn_rois"])),
+           "loss_full": loss_full, "loss_slab": float(r["loss"]),
+           "grad_rel_err": float((g - g_full).abs().max() / g_full.abs().max())}
+    with open(os.path.join(out_dir, "rank0.json"), "w") as f:
+        json.dump(res, f)
+    print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     a = sys.argv[1:]
-    if a[0] == "ref":
+    if a[0] == "nccl":
+        mode_nccl(a[1], int(a[2]))
+    elif a[0] == "ref":
         mode_ref(a[1], int(a[2]), int(a[3]))
     elif a[0] == "cmp":
         mode_cmp(a[1], int(a[2]), int(a[3]), a[4])

@@ -7,31 +7,20 @@ parameters after SGD agree, gradients are identical on every rank, and all
 but the last bucket launch before the backward ends."""
 import json
 import os
-import socket
-import subprocess
-import sys
 
 import pytest
+
+from launch import torchrun
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def test_overlapped_dp_step_matches(cuda, tmp_path):
     world = 2
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}",
-           os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path)]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    r = torchrun(world, [os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path)], ROOT, 300,
+                 tmp_path / "torchrun.log")
+    assert r.returncode == 0, r.log[-3000:]
     res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
     for x in res:
         assert x["grads_close"] and x["grads_same_on_ranks"] and x["param_max_diff"] < 1e-6, x
@@ -44,12 +33,9 @@ def test_overlapped_dp_step_rccl_device_path(cuda, tmp_path):
     the autograd thread under the weight-gradient side stream, waited on by the
     compute stream before SGD -- the same gradients and parameters as the step
     without collectives."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}",
-           os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path), "nccl"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
-    assert r.returncode == 0, r.stderr[-3000:]
+    r = torchrun(1, [os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path), "nccl"], ROOT, 300,
+                 tmp_path / "torchrun.log", env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.log[-3000:]
     x = json.load(open(tmp_path / "rank0.json"))
     assert x["grads_close"] and x["grads_same_on_ranks"] and x["param_max_diff"] < 1e-6, x
     assert x["n_buckets"] > 8 and x["n_early"] >= x["n_buckets"] - 2, x

@@ -5,31 +5,22 @@ forward, the loss equal and the SUM-all-reduced gradient equal up to fp32
 summation order (1e-4 of the gradient scale, north-star tolerance)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
 import pytest
 
+from launch import torchrun
+
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @pytest.mark.parametrize("world,D", [(2, 16), (3, 16)])
 def test_slab_rpn_matches_single_volume(cuda, tmp_path, world, D):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}",
-           os.path.join(ROOT, "tests", "slab_worker.py"), str(tmp_path), str(D)]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    r = torchrun(world, [os.path.join(ROOT, "tests", "slab_worker.py"), str(tmp_path), str(D)], ROOT, 300,
+                 tmp_path / "torchrun.log")
+    assert r.returncode == 0, r.log[-3000:]
     res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
     for x in res:
         assert x["p2_bitexact"] and x["logits_bitexact"] and x["bbox_bitexact"], x
@@ -50,11 +41,9 @@ def test_slab_rpn_256_eight_ranks(cuda, tmp_path):
                        cwd=ROOT, timeout=600)          # output streams into the (-s) log
     assert r.returncode == 0, r.returncode
     world = 8
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}",
-           os.path.join(ROOT, "tests", "slab_worker.py"), "cmp", str(tmp_path), "256", "256", str(ref)]
-    r = subprocess.run(cmd, cwd=ROOT, timeout=900)
-    assert r.returncode == 0, r.returncode
+    r = torchrun(world, [os.path.join(ROOT, "tests", "slab_worker.py"), "cmp", str(tmp_path), "256", "256",
+                         str(ref)], ROOT, 900, tmp_path / "torchrun.log")
+    assert r.returncode == 0, r.log[-3000:]
     res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
     for x in res:
         print(x)
@@ -63,3 +52,18 @@ def test_slab_rpn_256_eight_ranks(cuda, tmp_path):
             assert x[f"{k}_bitexact"], (k, x)
         assert abs(x["loss_slab"] - x["loss_full"]) <= 1e-5 * abs(x["loss_full"]), x
         assert x["grad_rel_err"] < 1e-4, x
+
+
+def test_slab_rpn_rccl_one_rank(cuda, tmp_path):
+    """SlabRPN on the RCCL device path (backend "nccl", one rank: RCCL refuses
+    two ranks on one GPU): the overlapped SUM all-reduce forced on
+    (force_hook), the slab ProposalLayer on its side stream -- proposals
+    bit-exact and the gradient equal to the plain step's up to the fp32
+    atomics' order (1e-5 of its scale)."""
+    r = torchrun(1, [os.path.join(ROOT, "tests", "slab_worker.py"), "nccl", str(tmp_path), "16"], ROOT, 300,
+                 tmp_path / "torchrun.log", env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.log[-3000:]
+    x = json.load(open(tmp_path / "rank0.json"))
+    assert x["backend"] == "nccl" and x["hook_used"] and x["rois_bitexact"], x
+    assert abs(x["loss_slab"] - x["loss_full"]) <= 1e-5 * abs(x["loss_full"]), x
+    assert x["grad_rel_err"] < 1e-5, x
