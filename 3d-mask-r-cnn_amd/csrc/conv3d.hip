@@ -2948,7 +2948,7 @@ extern "C" int m3d_deconv3d_k2s2(const float* x, int64_t B, int64_t H, int64_t W
 // The implicit GEMM's scalar loader reaches 0.27 of the f32 MFMA peak here
 // (K = 343 taps of ONE channel: no channel vector to load).  This kernel keeps
 // the whole K operand on chip: the 343 x 64 weights live in LDS for the life
-// of a persistent workgroup (loaded once per CU), and every wave owns one
+// of a workgroup that loops over many tiles (about 4 per CU), and every wave owns one
 // output column (oy, ox) x 32 z x 64 channels with its own input window (the
 // 49 (ky, kx) rows x 38 z voxels, + one zero row) in its own LDS region,
 // refilled from registers prefetched during the previous tile's MFMAs.  No
@@ -3109,7 +3109,12 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     }();
     const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
     const int64_t ntiles = (int64_t)p.B * p.OH * p.OW * tz_n;
-    const unsigned grid = (unsigned)std::min<int64_t>((ntiles + 7) / 8, ncu);
+    // about four workgroups per CU, not one persistent workgroup per CU: the
+    // stem opens the step while the previous step's side-stream work (the
+    // one-CU NMS reduce) may still hold a CU, and a persistent block waiting
+    // for that CU would stall the whole launch (measured 1.5 ms in the step
+    // vs 0.28 ms alone at 128^3); with 4 per CU the others absorb its share
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 7) / 8, 4 * (int64_t)ncu));
     hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, tz_n, ntiles);
     return check_launch("stem_fwd_kernel");
 }

@@ -432,6 +432,42 @@ __global__ void line_scatter_kernel(const int32_t* __restrict__ keys, int64_t li
     perm[atomicAdd(offs + keys[L], 1)] = (int32_t)L;
 }
 
+// ROI order (M3D_ROI_SORT=2): the boxes ranked by (level, Morton code of the
+// centre's owner voxel), ties by index; perm[line] keeps each ROI's lines
+// contiguous (consecutive x lines share corner columns in L1) while
+// overlapping ROIs run next to each other.  One workgroup; O(n^2) ranking
+// over at most a few thousand boxes.
+__device__ __forceinline__ uint32_t morton2(uint32_t y, uint32_t x) {
+    uint32_t r = 0;
+    for (int i = 0; i < 12; ++i) r |= (((y >> i) & 1u) << (2 * i + 1)) | (((x >> i) & 1u) << (2 * i));
+    return r;
+}
+__global__ __launch_bounds__(1024) void roi_rank_kernel(LineArgs a, Pyr P, int64_t nbox,
+                                                        uint64_t* __restrict__ keys, int32_t* __restrict__ inv) {
+    for (int64_t n = threadIdx.x; n < nbox; n += 1024) {
+        const int l = a.levels[n] - 2;
+        const float* bx = a.boxes + n * 6;
+        const int cy = owner_idx(0.5f * (bx[0] + bx[3]) * (float)(P.H[l] - 1), P.H[l]);
+        const int cx = owner_idx(0.5f * (bx[1] + bx[4]) * (float)(P.W[l] - 1), P.W[l]);
+        const int64_t b = n / a.N;
+        keys[n] = ((uint64_t)b << 58) | ((uint64_t)l << 56) | ((uint64_t)morton2(cy, cx) << 32) | (uint64_t)n;
+    }
+    __syncthreads();
+    for (int64_t n = threadIdx.x; n < nbox; n += 1024) {
+        const uint64_t k = keys[n];
+        int64_t rank = 0;
+        for (int64_t j = 0; j < nbox; ++j) rank += keys[j] < k;
+        inv[rank] = (int32_t)n;
+    }
+}
+__global__ void roi_perm_kernel(const int32_t* __restrict__ inv, int64_t lines, int per_box,
+                                int32_t* __restrict__ perm) {
+    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= lines) return;
+    const int64_t r = L / per_box;
+    perm[L] = (int32_t)(inv[r] * (int64_t)per_box + (L - r * per_box));
+}
+
 static int roi_slices() {
     static const int env = [] { const char* e = getenv("M3D_ROI_SLICES"); return e ? atoi(e) : 8; }();
     return env;
@@ -1337,7 +1373,17 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             int64_t nb = 0, nl = 0;
             const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
             static const int sort_env = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : 0; }();
-            if (sort_env && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
+            if (sort_env == 2 && workspace && ws_bytes >= need && nl < INT32_MAX && B * N <= nb) {
+                // ROI order: keys [B*N] (uint64, 8-B aligned at the start), inv [B*N], perm [lines]
+                uint64_t* rkeys = (uint64_t*)workspace;
+                int32_t* inv = (int32_t*)(rkeys + B * N);
+                int32_t* pm = inv + B * N;
+                hipLaunchKernelGGL(roi_rank_kernel, dim3(1), dim3(1024), 0, s, a, P, B * N, rkeys, inv);
+                hipLaunchKernelGGL(roi_perm_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, inv, nl, ph * pw, pm);
+                rc = check_launch("roi order");
+                if (rc) return rc;
+                perm = pm;
+            } else if (sort_env == 1 && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
                 int32_t* counts = (int32_t*)workspace;
                 int32_t* offs = counts + nb;
                 int32_t* keys = offs + nb;
