@@ -2013,6 +2013,73 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
         }
 }
 
+// The same transform with 4 consecutive channels per thread (N % 4 == 0):
+// 16-B loads and non-temporal 16-B stores (1 KiB per wave-instruction instead
+// of 256 B) for this write-dominated kernel (P*16 outputs per 2x2xNZ inputs).
+// Per element the same arithmetic as wino_grad_kernel (bit-identical).
+typedef float f4vec __attribute__((ext_vector_type(4)));
+template <int NZ>
+__global__ __launch_bounds__(256) void wino_grad4_kernel(const float* __restrict__ dz, WinoGeom g,
+                                                         int N, float* __restrict__ DY) {
+    constexpr int P = ZT<NZ>::P;
+    const int N4 = N >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.T * N4) return;
+    const int n4 = (int)(i % N4);
+    const int64_t t = i / N4;
+    int b, ty, tx, tz;
+    tile_coords(t, g, b, ty, tx, tz);
+    f4vec ev[2][2][NZ];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) {
+                const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
+                ev[a][bb][k] = (y < g.H && xx < g.W && z < g.D)
+                                   ? *reinterpret_cast<const f4vec*>(
+                                         dz + ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * N + 4 * n4)
+                                   : f4vec{0.f, 0.f, 0.f, 0.f};
+            }
+    // z transform (ZT::a on each of the 4 channels), then x (a4), then y (a4)
+    f4vec t1[2][2][P];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            float e[4][NZ], o[4][P];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int k = 0; k < NZ; ++k) e[q][k] = ev[a][bb][k][q];
+                ZT<NZ>::a(e[q], o[q]);
+            }
+#pragma unroll
+            for (int k = 0; k < P; ++k) t1[a][bb][k] = f4vec{o[0][k], o[1][k], o[2][k], o[3][k]};
+        }
+    const int64_t stride = g.T * N;
+    float* out = DY + t * N + 4 * n4;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        f4vec t2[2][4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            // a4(e0, e1) = [e0, e0 + e1, e0 - e1, -e1] per channel
+            const f4vec e0 = t1[a][0][k], e1 = t1[a][1][k];
+            t2[a][0] = e0; t2[a][1] = e0 + e1; t2[a][2] = e0 - e1; t2[a][3] = -e1;
+        }
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const f4vec e0 = t2[0][bb], e1 = t2[1][bb];
+            const f4vec o[4] = {e0, e0 + e1, e0 - e1, -e1};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                __builtin_nontemporal_store(o[a], reinterpret_cast<f4vec*>(out + (int64_t)((a * 4 + bb) * P + k) * stride));
+        }
+    }
+}
+
 // dW[t][c][n] += (G^T (x) G^T (x) Gz^T) dWh[.][c][n]
 template <int NZ>
 __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ dWh, int C,
@@ -3920,7 +3987,13 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
         ws.U = const_cast<float*>(u_in);       // the forward's transformed input, kept
     else
         WINO_INPUT(nz, false, dim3(grid_for(g.T * Cin, 256)), st(s), x, g, (int)Cin, ws.U);
-    WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
+    // M3D_WINO_GRAD4=1: the float4 form (measured slower: 278 vs 253 us avg, write-bound)
+    static const int grad4 = [] { const char* v = getenv("M3D_WINO_GRAD4"); return v ? atoi(v) : 0; }();
+    if (grad4 && Cout % 4 == 0)
+        WINO_LAUNCH_NZ(nz, wino_grad4_kernel, dim3(grid_for(g.T * (Cout / 4), 256)), dim3(256), 0, st(s), dz, g,
+                       (int)Cout, ws.M);
+    else
+        WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     if (wgrad_x3_env() && Cout > 64) {
         launch_wgrad_x3(ws.U, ws.M, ws.V, g.T, (int)Cin, (int)Cout, wino_points(nz), g.T * Cin, g.T * Cout,
