@@ -48,6 +48,13 @@ struct ConvP {
     int64_t bsa, bsw, bsy;
     int dly = 1, dlx = 1, dlz = 1;   // dilation (fwd only; mrcnn_mask_conv3b)
     int nbatch = 1;                  // batches (PERSIST: looped inside the grid)
+    // depth-slab halo planes beside the slab (the stem and the direct weight
+    // gradient, m3d_conv3d_*_halo): the conv runs on the virtual z grid
+    // [lower halo (hnlo planes) | slab (hdl) | upper halo], D = its depth; x (a)
+    // holds the slab [B,H,W,hdl,C], halo [B,H,W,2*hr,C] the neighbours' planes
+    // ([0,hr) from below, [hr,2hr) from above)
+    const float* halo = nullptr;
+    int hnlo = 0, hdl = 0, hr = 0;
 };
 
 struct Epi {
@@ -824,7 +831,7 @@ static void wg_finish(const WgOut& o, int64_t splits, int64_t nbatch, int64_t K,
 // grid (K/BI, N/BJ, splits); each block reduces its m-range, fp32 atomics out
 // (or the deterministic-mode target, WgOut).
 // -------------------------------------------------------------------------
-template <int BI, int BJ, int WI, int WJ, bool AVEC>
+template <int BI, int BJ, int WI, int WJ, bool AVEC, bool HALO = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float* __restrict__ dz,
                                                             float* __restrict__ dw,
                                                             int64_t m_per_split, WgOut wo) {
@@ -905,10 +912,17 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
             }
         }
     };
+    const int dx_ = HALO ? p.hdl : p.D;               // depth of the tensor behind p.a
     const __amdgpu_buffer_rsrc_t rsX =
-        make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * p.D * p.C * 4);
+        make_rsrc(p.a, (uint64_t)p.B * p.H * p.W * dx_ * p.C * 4);
     const __amdgpu_buffer_rsrc_t rsG = make_rsrc(dz, (uint64_t)p.M * p.N * 4);
-    const int rowWx = p.D * p.C, rowHx = p.W * rowWx;
+    const int rowWx = dx_ * p.C, rowHx = p.W * rowWx;
+    // halo planes: a second descriptor; each element is loaded from both with
+    // one offset out of range (0) and the lane picks its source (no per-lane
+    // descriptor select)
+    const __amdgpu_buffer_rsrc_t rsH =
+        make_rsrc(HALO ? p.halo : p.a, HALO ? (uint64_t)p.B * p.H * p.W * 2 * p.hr * p.C * 4 : 0);
+    const int rowWh = 2 * p.hr * p.C, rowHh = p.W * rowWh;
     auto load_tile = [&](int64_t mb) {
         int rb = cb_, ry = cy_, rx = cx_, rz = cz_;
 #pragma unroll
@@ -919,10 +933,29 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
                       iz = rz * p.sz - p.pz + kz;
             const bool ok = kok && m < me && (unsigned)iy < (unsigned)p.H &&
                             (unsigned)ix < (unsigned)p.W && (unsigned)iz < (unsigned)p.D;
-            const uint32_t off = ok ? (uint32_t)((rb * p.H + iy) * rowHx + ix * rowWx + iz * p.C + cc) * 4u
-                                    : M3D_OOB;
-            if (AVEC) rx4[q] = bload4(rsX, off);
-            else rx1[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, (int)off, 0, 0));
+            if constexpr (HALO) {
+                const int zl = iz - p.hnlo;
+                const bool inx = ok && (unsigned)zl < (unsigned)p.hdl;
+                const bool inh = ok && !inx;
+                const int pl = zl < 0 ? zl + p.hr : p.hr + zl - p.hdl;
+                const uint32_t ox = inx ? (uint32_t)((rb * p.H + iy) * rowHx + ix * rowWx + zl * p.C + cc) * 4u
+                                        : M3D_OOB;
+                const uint32_t oh = inh ? (uint32_t)((rb * p.H + iy) * rowHh + ix * rowWh + pl * p.C + cc) * 4u
+                                        : M3D_OOB;
+                if (AVEC) {
+                    const float4 vx = bload4(rsX, ox), vh = bload4(rsH, oh);
+                    rx4[q] = inh ? vh : vx;
+                } else {
+                    const float vx = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, (int)ox, 0, 0));
+                    const float vh = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsH, (int)oh, 0, 0));
+                    rx1[q] = inh ? vh : vx;
+                }
+            } else {
+                const uint32_t off = ok ? (uint32_t)((rb * p.H + iy) * rowHx + ix * rowWx + iz * p.C + cc) * 4u
+                                        : M3D_OOB;
+                if (AVEC) rx4[q] = bload4(rsX, off);
+                else rx1[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, (int)off, 0, 0));
+            }
         }
         advance(cb_, cy_, cx_, cz_, BKM);
 #pragma unroll
@@ -1127,7 +1160,7 @@ static int wgrad_k64_env() {
     return v;
 }
 
-template <int BI, int BJ, int WI, int WJ, bool AVEC>
+template <int BI, int BJ, int WI, int WJ, bool AVEC, bool HALO = false>
 static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s, int nbatch = 1) {
     const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;                   // aim >= 1024 blocks
@@ -1141,7 +1174,7 @@ static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t
     splits = (p.M + mper - 1) / mper;
     dim3 grid((unsigned)((p.K + BI - 1) / BI), (unsigned)((p.N + BJ - 1) / BJ),
               (unsigned)(splits * nbatch));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BI, BJ, WI, WJ, AVEC>), grid, dim3(256), 0, s, p, dz, dw,
+    hipLaunchKernelGGL((conv_wgrad_kernel<BI, BJ, WI, WJ, AVEC, HALO>), grid, dim3(256), 0, s, p, dz, dw,
                        mper, wo);
     wg_finish(wo, splits, nbatch, p.K, p.N, p.bsy, dw, s);
 }
@@ -3051,7 +3084,7 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
     float* ww = win[wave];
     if (lane < STEM_WZ) ww[49 * STEM_WZ + lane] = 0.0f;   // the padding row
     __syncthreads();                              // the only barrier: waves run free below
-    const size_t plane = (size_t)p.D, row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
     auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
         tz = (int)(t % tz_n); t /= tz_n;
         ox = (int)(t % p.OW); t /= p.OW;
@@ -3070,8 +3103,18 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
             if (i < 49 * STEM_WZ) {
                 const int R = i / STEM_WZ, iz = i - R * STEM_WZ;
                 const int gy = gy0 + R / 7, gx = gx0 + R % 7, gz = gz0 + iz;
-                if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && gz >= 0 && gz < p.D)
-                    val = xb[gy * row + gx * plane + gz];
+                if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && gz >= 0 && gz < p.D) {
+                    if (p.halo) {     // virtual z grid: slab planes from x, the others from the halo
+                        const int zl = gz - p.hnlo;
+                        if ((unsigned)zl < (unsigned)p.hdl)
+                            val = xb[gy * row + gx * plane + zl];
+                        else
+                            val = p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
+                                         (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
+                    } else {
+                        val = xb[gy * row + gx * plane + gz];
+                    }
+                }
             }
             v[q] = val;
         }
@@ -3468,6 +3511,76 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
         else launch_wgrad<128, 128, 2, 2, false>(p, dz, dw, st(s));
     }
     return check_launch("conv_wgrad_kernel");
+}
+
+// ---- depth-slab forms of the direct convs: halo planes beside the slab ---------
+// x [B,H,W,Dl,Cin] is the local slab, halo [B,H,W,2r,Cin] the neighbours' r
+// boundary planes (has_lo / has_hi: that neighbour exists); the conv is the
+// 'same' z window kd = 2r+1 at z-stride 1 with pad pz = r where the volume ends,
+// OD = Dl -- the same taps and sums as on the halo-extended copy of the slab.
+static int conv_halo_geom(ConvP& p, const float* halo, int32_t has_lo, int32_t has_hi, int32_t r, int64_t Dl,
+                          int32_t kd, int32_t sz, int32_t pz, int64_t OD) {
+    if (!halo) return einval("conv3d halo: null halo planes");
+    if (r <= 0 || kd != 2 * r + 1 || sz != 1 || pz != r || OD != Dl || Dl < r)
+        return einval("conv3d halo: z window must be 'same' 2r+1 at stride 1 on a slab of >= r planes");
+    const int nlo = has_lo ? r : 0, nhi = has_hi ? r : 0;
+    p.D = (int)(Dl + nlo + nhi);
+    p.pz = pz - nlo;
+    p.halo = halo;
+    p.hnlo = nlo;
+    p.hdl = (int)Dl;
+    p.hr = r;
+    return M3D_OK;
+}
+
+// The one-channel 7^3 stem (stem_fwd_kernel) on a depth slab.
+extern "C" int m3d_conv3d_fwd_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi, int32_t r,
+                                   int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin, const float* w,
+                                   int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW,
+                                   int64_t OD, int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                                   const float* bias, const float* bn_scale, const float* bn_shift, int32_t relu,
+                                   float* z_out, float* y, m3d_stream_t s) {
+    int rc = conv_check(B, H, W, Dl, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
+    if (rc) return rc;
+    if (!stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
+        return einval("conv3d_fwd_halo: only the one-channel 7^3 stem (1 -> 64, strides (2,2,1)) has a halo form");
+    if ((bn_scale == nullptr) != (bn_shift == nullptr))
+        return einval("conv3d: bn_scale and bn_shift must be given together");
+    if (relu < 0 || relu > 2) return einval("conv3d: activation must be 0 (none), 1 (relu), 2 (sigmoid)");
+    if (B * H * W * (Dl + 2 * r) * Cin >= op_lim() || B * OH * OW * OD * Cout >= op_lim())
+        return einval("conv3d_fwd_halo: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p{x, (int)B, (int)H, (int)W, (int)Dl, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
+            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), w, (int)Cout, 0, 0, 0, 0};
+    if ((rc = conv_halo_geom(p, halo, has_lo, has_hi, r, Dl, kd, sz, pz, OD))) return rc;
+    Epi e{bias, bn_scale, bn_shift, nullptr, 0, relu, z_out, y, Cout, nullptr, 0, 0, (int)OH, (int)OW, (int)OD,
+          1, 1, 1, 0, 1};
+    return launch_stem(p, e, st(s));
+}
+
+// The direct weight gradient (conv_wgrad_kernel) on a depth slab: the stem's
+// and the 64-channel 3^3 convs' (whose weight gradient is not Winograd).
+extern "C" int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi,
+                                          int32_t r, const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl,
+                                          int64_t Cin, int32_t kh, int32_t kw, int32_t kd, int64_t Cout,
+                                          int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
+                                          int32_t py, int32_t px, int32_t pz, float* dw, m3d_stream_t s) {
+    int rc = conv_check(B, H, W, Dl, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
+    if (rc) return rc;
+    if (B * H * W * (Dl + 2 * r) * Cin >= op_lim() || B * OH * OW * OD * Cout >= op_lim())
+        return einval("conv3d_bwd_weight_halo: operand larger than 4 GiB (32-bit buffer offsets)");
+    ConvP p{x, (int)B, (int)H, (int)W, (int)Dl, (int)Cin, (int)OH, (int)OW, (int)OD, kh, kw, kd,
+            sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
+            (int)Cout, 0, 0, 0, 0};
+    if ((rc = conv_halo_geom(p, halo, has_lo, has_hi, r, Dl, kd, sz, pz, OD))) return rc;
+    const bool vec = (Cin % 4) == 0;
+    if (Cout <= 64) {
+        if (vec) launch_wgrad<128, 64, 2, 2, true, true>(p, dz, dw, st(s));
+        else launch_wgrad<128, 64, 2, 2, false, true>(p, dz, dw, st(s));
+    } else {
+        if (vec) launch_wgrad<128, 128, 2, 2, true, true>(p, dz, dw, st(s));
+        else launch_wgrad<128, 128, 2, 2, false, true>(p, dz, dw, st(s));
+    }
+    return check_launch("conv_wgrad_kernel<halo>");
 }
 
 // ---- Winograd entry points -------------------------------------------------

@@ -89,11 +89,36 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const uint8_t* 
 // the window order, the first-valid initialisation and the strict '>' (so the
 // argmax byte and NaN behaviour) and the backward summation order are the
 // scalar kernels' own, so results are bit-identical.
+// Depth-slab halo planes beside the slab (m3d.slab.halo_planes): the pool runs on
+// the virtual z grid [lower halo (nlo planes) | slab (Dl) | upper halo], D =
+// nlo + Dl + nhi; plane zl = z - nlo < 0 reads halo plane zl + r, zl >= Dl
+// reads halo plane r + zl - Dl ([B,H,W,2r,C]: [0,r) from below, [r,2r) from
+// above).  Same values and order as the pool over the halo-extended copy.
+struct PoolHalo {
+    const float4* h;     // [B,H,W,2r,C/4]
+    float4* dh;          // backward: gradient of the halo planes, same layout
+    int nlo, Dl, r;
+};
+template <bool HALO>
+__device__ __forceinline__ uint32_t pool_zoff(const PoolHalo& hz, uint32_t bhw, int D, int iz, int C4,
+                                              bool& in_halo) {
+    if (!HALO) {
+        in_halo = false;
+        return (bhw * (uint32_t)D + iz) * (uint32_t)C4;
+    }
+    const int zl = iz - hz.nlo;
+    in_halo = zl < 0 || zl >= hz.Dl;
+    if (!in_halo) return (bhw * (uint32_t)hz.Dl + zl) * (uint32_t)C4;
+    const int pl = zl < 0 ? zl + hz.r : hz.r + zl - hz.Dl;
+    return (bhw * (uint32_t)(2 * hz.r) + pl) * (uint32_t)C4;
+}
+
+template <bool HALO>
 __global__ __launch_bounds__(256) void maxpool_fwd4_kernel(const float4* __restrict__ x, int H, int W, int D,
                                                            int C4, int kh, int kw, int kd, int sy, int sx,
                                                            int sz, int py, int px, int pz, int OH, int OW,
                                                            int OD, uint32_t total, float4* __restrict__ y,
-                                                           uchar4* __restrict__ am) {
+                                                           uchar4* __restrict__ am, PoolHalo hz) {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
         const uint32_t c = i % (uint32_t)C4;
         uint32_t t = i / (uint32_t)C4;
@@ -110,11 +135,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd4_kernel(const float4* __restr
             for (int kx = 0; kx < kw; ++kx) {
                 const int ix = ox * sx - px + kx;
                 if (ix < 0 || ix >= W) continue;
-                const uint32_t row = ((b * (uint32_t)H + iy) * (uint32_t)W + ix) * (uint32_t)D;
+                const uint32_t bhw = (b * (uint32_t)H + iy) * (uint32_t)W + ix;
                 for (int kz = 0; kz < kd; ++kz) {
                     const int iz = oz * sz - pz + kz;
                     if (iz < 0 || iz >= D) continue;
-                    const float4 v = x[(row + iz) * (uint32_t)C4 + c];
+                    bool hal;
+                    const uint32_t zo = pool_zoff<HALO>(hz, bhw, D, iz, C4, hal);
+                    const float4 v = (HALO && hal ? hz.h : x)[zo + c];
                     const float vv[4] = {v.x, v.y, v.z, v.w};
                     const int id = (ky * kw + kx) * kd + kz;
 #pragma unroll
@@ -130,12 +157,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd4_kernel(const float4* __restr
     }
 }
 
+template <bool HALO>
 __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float4* __restrict__ dy,
                                                            const uchar4* __restrict__ am, int H, int W,
                                                            int D, int C4, int kh, int kw, int kd, int sy,
                                                            int sx, int sz, int py, int px, int pz, int OH,
                                                            int OW, int OD, uint32_t total,
-                                                           float4* __restrict__ dx) {
+                                                           float4* __restrict__ dx, PoolHalo hz) {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
         const uint32_t c = i % (uint32_t)C4;
         uint32_t t = i / (uint32_t)C4;
@@ -168,7 +196,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float4* __restr
                 }
             }
         }
-        dx[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        const float4 r = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        if (HALO) {     // i runs over the virtual grid: the slab's planes go to dx, the halo's to dh
+            bool hal;
+            const uint32_t zo = pool_zoff<true>(hz, (b * (uint32_t)H + iy) * (uint32_t)W + ix, D, iz, C4, hal);
+            (hal ? hz.dh : dx)[zo + c] = r;
+        } else {
+            dx[i] = r;
+        }
     }
 }
 
@@ -555,10 +590,10 @@ extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && B * H * W * D * C / 4 < 0x7FFFFFFF && total / 4 < 0x7FFFFFFF &&
         ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
-        hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+        hipLaunchKernelGGL(maxpool_fwd4_kernel<false>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
                            (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, sz,
                            py, px, pz, (int)OH, (int)OW, (int)OD, (uint32_t)(total / 4), (float4*)y,
-                           (uchar4*)argmax);
+                           (uchar4*)argmax, PoolHalo{});
         return check_launch("maxpool_fwd4_kernel");
     }
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), x, (int)B,
@@ -578,16 +613,78 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && total / 4 < 0x7FFFFFFF && B * OH * OW * OD * C / 4 < 0x7FFFFFFF &&
         ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
-        hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+        hipLaunchKernelGGL(maxpool_bwd4_kernel<false>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
                            (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
                            kh, kw, kd, sy, sx, sz, py, px, pz, (int)OH, (int)OW, (int)OD,
-                           (uint32_t)(total / 4), (float4*)dx);
+                           (uint32_t)(total / 4), (float4*)dx, PoolHalo{});
         return check_launch("maxpool_bwd4_kernel");
     }
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s), dy, argmax,
                        (int)B, (int)H, (int)W, (int)D, (int)C, kh, kw, kd, sy, sx, sz, py, px, pz,
                        (int)OH, (int)OW, (int)OD, dx);
     return check_launch("maxpool_bwd_kernel");
+}
+
+// Depth-slab form (core/models.py:246 MaxPooling3D on the slab): x is the
+// local slab [B,H,W,Dl,C], halo [B,H,W,2r,C] the neighbours' r boundary planes
+// (has_lo / has_hi: present), z window kd = 2r + 1 at z-stride 1 with the 'same'
+// z pad r only where the volume ends; y / argmax [B,OH,OW,Dl,C].
+static int pool_halo_args(const float* x, const float* h, int64_t B, int64_t H, int64_t W, int64_t Dl,
+                          int64_t C, int32_t kd, int32_t sz, int32_t pz, int32_t r, int64_t OD) {
+    if (!x || !h) return einval("maxpool3d_halo: null slab or halo");
+    if (C % 4 || ((uintptr_t)x & 15) || ((uintptr_t)h & 15))
+        return einval("maxpool3d_halo: C % 4 == 0 and 16-B aligned tensors required");
+    if (r <= 0 || kd != 2 * r + 1 || sz != 1 || pz != r || OD != Dl || Dl < r)
+        return einval("maxpool3d_halo: z window must be 'same' 2r+1 at stride 1 on a slab of >= r planes");
+    if (B * H * W * (Dl + 2 * r) * C / 4 >= 0x7FFFFFFF) return einval("maxpool3d_halo: tensor too large");
+    return M3D_OK;
+}
+
+extern "C" int m3d_maxpool3d_fwd_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi,
+                                      int32_t r, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t C,
+                                      int32_t kh, int32_t kw, int32_t kd, int32_t sy, int32_t sx, int32_t sz,
+                                      int32_t py, int32_t px, int32_t pz, int64_t OH, int64_t OW, int64_t OD,
+                                      float* y, uint8_t* argmax, m3d_stream_t s) {
+    const int nlo = has_lo ? r : 0, nhi = has_hi ? r : 0;
+    const int64_t D = Dl + nlo + nhi;
+    int rc = check_pool_args(B, H, W, D, C, kh, kw, kd, sy, sx, sz, py, px, pz - nlo, OH, OW, OD);
+    if (rc) return rc;
+    if ((rc = pool_halo_args(x, halo, B, H, W, Dl, C, kd, sz, pz, r, OD))) return rc;
+    if (!y || !argmax || ((uintptr_t)y & 15) || ((uintptr_t)argmax & 3))
+        return einval("maxpool3d_halo: y / argmax must be aligned");
+    const int64_t total = B * OH * OW * OD * C;
+    if (total == 0) return M3D_OK;
+    PoolHalo hz{(const float4*)halo, nullptr, nlo, (int)Dl, r};
+    hipLaunchKernelGGL(maxpool_fwd4_kernel<true>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+                       (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, sz,
+                       py, px, pz - nlo, (int)OH, (int)OW, (int)OD, (uint32_t)(total / 4), (float4*)y,
+                       (uchar4*)argmax, hz);
+    return check_launch("maxpool_fwd4_kernel<halo>");
+}
+
+// Backward of m3d_maxpool3d_fwd_halo: dx [B,H,W,Dl,C] (the slab's own planes)
+// and dhalo [B,H,W,2r,C] (the gradient of the neighbours' planes, to be sent
+// back: m3d.slab.return_halo_grads); planes of an absent neighbour are not written.
+extern "C" int m3d_maxpool3d_bwd_halo(const float* dy, const uint8_t* argmax, int32_t has_lo, int32_t has_hi,
+                                      int32_t r, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t C,
+                                      int32_t kh, int32_t kw, int32_t kd, int32_t sy, int32_t sx, int32_t sz,
+                                      int32_t py, int32_t px, int32_t pz, int64_t OH, int64_t OW, int64_t OD,
+                                      float* dx, float* dhalo, m3d_stream_t s) {
+    const int nlo = has_lo ? r : 0, nhi = has_hi ? r : 0;
+    const int64_t D = Dl + nlo + nhi;
+    int rc = check_pool_args(B, H, W, D, C, kh, kw, kd, sy, sx, sz, py, px, pz - nlo, OH, OW, OD);
+    if (rc) return rc;
+    if ((rc = pool_halo_args(dx, dhalo, B, H, W, Dl, C, kd, sz, pz, r, OD))) return rc;
+    if (!dy || !argmax || ((uintptr_t)dy & 15) || ((uintptr_t)argmax & 3))
+        return einval("maxpool3d_halo: dy / argmax must be aligned");
+    const int64_t total = B * H * W * D * C;
+    if (total == 0) return M3D_OK;
+    PoolHalo hz{nullptr, (float4*)dhalo, nlo, (int)Dl, r};
+    hipLaunchKernelGGL(maxpool_bwd4_kernel<true>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
+                       (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
+                       kh, kw, kd, sy, sx, sz, py, px, pz - nlo, (int)OH, (int)OW, (int)OD,
+                       (uint32_t)(total / 4), (float4*)dx, hz);
+    return check_launch("maxpool_bwd4_kernel<halo>");
 }
 
 extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D,

@@ -294,9 +294,13 @@ struct RegionBase {
 // line, float4 each (C = 256: SL = 8 -> 128 B rows, one L2 line).  Per-sample
 // arithmetic as line_fwd_kernel (bit-identical).  Needs C % (4 * 64 / SL) == 0
 // ... and C/4 == 64 (C = 256) for the lane split below.
-template <int SL>
+// PD > 0 (crop depth known at compile time, one z-part): the line's PD outputs
+// are kept in registers and stored after the loop, so no corner load of the
+// line waits behind an earlier output store (one vmcnt counter covers loads
+// and stores) -- the z loop's loads can all be in flight at once.
+template <int SL, int PD = 0>
 __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, const int32_t* __restrict__ perm,
-                                                          int zs) {
+                                                          int zs, const int32_t* __restrict__ wperm) {
     constexpr int LPL = 64 / SL;                      // lanes (float4) per line slice
     // blocks: SL slices in dispatch order, each a multiple of 8 blocks remapped
     // XCD-contiguously within the slice (hardware XCD = block % 8); a line is
@@ -306,9 +310,10 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     const int64_t bs8 = ((waves_per_slice + 3) / 4 + 7) / 8 * 8;
     const int slice = (int)(blockIdx.x / bs8);
     const int64_t lr = blockIdx.x - (int64_t)slice * bs8;
-    const int64_t wv = ((lr % 8) * (bs8 / 8) + lr / 8) * 4 + (threadIdx.x >> 6);
+    int64_t wv = ((lr % 8) * (bs8 / 8) + lr / 8) * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (slice >= SL || wv >= waves_per_slice) return;
+    if (wperm) wv = wperm[wv];                        // spatially sorted wave order (lines stay per ROI)
     const int64_t item = wv * SL + lane / LPL;
     if (item >= items) return;
     int64_t line = item / zs;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
                             base + by * rowW + lx * rowD, base + by * rowW + rx * rowD};
     int pk = -1;
     float4 kv[4];
-    for (int z = zb; z < ze; ++z) {
+    auto sample = [&](int z) -> float4 {
         const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
         float4 r;
         if (in_z < 0 || in_z > (float)(D - 1)) {
@@ -372,7 +377,16 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
             r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
             r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
         }
-        st_nt(o + (int64_t)z * C4 + c, r);
+        return r;
+    };
+    if constexpr (PD > 0) {
+        float4 res[PD];
+#pragma unroll
+        for (int z = 0; z < PD; ++z) res[z] = sample(z);
+#pragma unroll
+        for (int z = 0; z < PD; ++z) st_nt(o + (int64_t)z * C4 + c, res[z]);
+    } else {
+        for (int z = zb; z < ze; ++z) st_nt(o + (int64_t)z * C4 + c, sample(z));
     }
 }
 
@@ -423,6 +437,30 @@ __global__ __launch_bounds__(1024) void excl_scan_kernel(const int32_t* __restri
         offs[i] = run;
         run += counts[i];
     }
+}
+
+// Wave order (M3D_ROI_SORT=3): the SL consecutive lines of one wave (one ROI,
+// consecutive x) stay together -- their z samples coincide, so the loop stays
+// wave-uniform -- and the waves are counting-sorted by the owner (y, x) column
+// of their first line, so waves of different, overlapping ROIs that read the
+// same columns run next to each other on one XCD (band of rows per XCD).
+__global__ void wave_key_kernel(LineArgs a, Pyr P, RegionBase rb, int sl, int64_t nwaves,
+                                int32_t* __restrict__ keys, int32_t* __restrict__ counts) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwaves) return;
+    int64_t t = w * sl;
+    const int x = (int)(t % a.cw); t /= a.cw;
+    const int y = (int)(t % a.ch);
+    const int64_t n = t / a.ch;
+    const int l = a.levels[n] - 2;
+    const int H = P.H[l], W = P.W[l];
+    const int64_t b = n / a.N;
+    const float* box = a.boxes + n * 6;
+    const int ty = owner_idx(axis_coord(box[0], box[3], H, a.ch, y, axis_scale(box[0], box[3], H, a.ch)), H);
+    const int lx = owner_idx(axis_coord(box[1], box[4], W, a.cw, x, axis_scale(box[1], box[4], W, a.cw)), W);
+    const int32_t k = (int32_t)(rb.base[l] + (b * H + ty) * W + lx);
+    keys[w] = k;
+    atomicAdd(counts + k, 1);
 }
 
 __global__ void line_scatter_kernel(const int32_t* __restrict__ keys, int64_t lines, int32_t* __restrict__ offs,
@@ -1370,6 +1408,7 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
         const int sl = roi_slices();
         if (C == 256 && (sl == 2 || sl == 4 || sl == 8 || sl == 16)) {
             const int32_t* perm = nullptr;
+            const int32_t* wperm = nullptr;
             int64_t nb = 0, nl = 0;
             const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
             static const int sort_env = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : 0; }();
@@ -1383,6 +1422,27 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 rc = check_launch("roi order");
                 if (rc) return rc;
                 perm = pm;
+            } else if (sort_env == 3 && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
+                const int64_t nw = (nl + sl - 1) / sl;
+                int32_t* counts = (int32_t*)workspace;
+                int32_t* offs = counts + nb;
+                int32_t* keys = offs + nb;
+                int32_t* pm = keys + nl;
+                RegionBase rb;
+                int64_t acc = 0;
+                for (int l = 0; l < 4; ++l) {
+                    rb.base[l] = acc;
+                    acc += B * fshape[l][0] * fshape[l][1];
+                }
+                if (hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)nb, s) != hipSuccess)
+                    return check_launch("memset wave buckets");
+                hipLaunchKernelGGL(wave_key_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, s, a, P, rb, sl, nw,
+                                   keys, counts);
+                hipLaunchKernelGGL(excl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nb, offs);
+                hipLaunchKernelGGL(line_scatter_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, s, keys, nw, offs, pm);
+                rc = check_launch("wave sort");
+                if (rc) return rc;
+                wperm = pm;
             } else if (sort_env == 1 && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
                 int32_t* counts = (int32_t*)workspace;
                 int32_t* offs = counts + nb;
@@ -1404,13 +1464,19 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 perm = pm;
             }
             static const int zs_env = [] { const char* e = getenv("M3D_ROI_ZSPLIT"); return e ? atoi(e) : 1; }();
-            const int zs = std::max(1, std::min(zs_env, (int)pd));
+            const int zs = wperm ? 1 : std::max(1, std::min(zs_env, (int)pd));
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
-            if (sl == 2) hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
-            else if (sl == 4) hipLaunchKernelGGL(line_fwd_sl_kernel<4>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
-            else if (sl == 16) hipLaunchKernelGGL(line_fwd_sl_kernel<16>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
-            else hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs);
+            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 1; }();
+            if (sl == 8 && zs == 1 && stage_env && (pd == 7 || pd == 14)) {
+                if (pd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+                else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+                return check_launch("line_fwd_sl_kernel<staged>");
+            }
+            if (sl == 2) hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else if (sl == 4) hipLaunchKernelGGL(line_fwd_sl_kernel<4>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else if (sl == 16) hipLaunchKernelGGL(line_fwd_sl_kernel<16>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
             return check_launch("line_fwd_sl_kernel");
         }
         const int mode = roi_region_mode();

@@ -118,6 +118,18 @@ _SIGS = {
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p],
+    "m3d_conv3d_fwd_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32,
+                            c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p,
+                            c_p, c_i32, c_p, c_p, c_p],
+    "m3d_conv3d_bwd_weight_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32,
+                                   c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                   c_i32, c_p, c_p],
+    "m3d_maxpool3d_fwd_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32,
+                               c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p,
+                               c_p],
+    "m3d_maxpool3d_bwd_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32,
+                               c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p,
+                               c_p],
     "m3d_upsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p],
     "m3d_subsample221_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_subsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],

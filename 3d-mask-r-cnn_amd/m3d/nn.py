@@ -369,10 +369,17 @@ class _ConvBNAct(torch.autograd.Function):
         else:
             ctx.bn = None
         ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
-        if halo is not None and not ctx.wino:
-            raise ValueError("halo planes are read by the Winograd kernels only")
+        if halo is not None and not ctx.wino and not _stem_halo(geo, Cin, Cout, res_mode):
+            raise ValueError("halo planes are read by the Winograd kernels and the stem only")
         ctx.u = None
-        if ctx.wino:
+        if halo is not None and not ctx.wino:
+            # the 7^3 stem on a depth slab: the neighbours' 3 planes beside the slab
+            r = halo[0].shape[3] // 2
+            check(_L().m3d_conv3d_fwd_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], r, B, H, W, D, Cin, ptr(w),
+                                           kh, kw, kd, Cout, OH, OW, OD, *geo.stride, *geo.pad, ptr(b),
+                                           ptr(scale), ptr(shift), 1 if relu else 0, ptr(z), ptr(y), stream()),
+                  "conv3d_fwd_halo")
+        elif ctx.wino:
             dext = D + (halo[1] + halo[2] if halo is not None else 0)
             ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             # training: keep the transformed input U for the weight gradient when
@@ -479,15 +486,15 @@ class _ConvBNAct(torch.autograd.Function):
             if grads.get("kernel") is not None:
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                     tw = _span()
-                    if min(Cin, Cout) < WINO_WGRAD_MIN_C:
-                        xw, gw = x, geo
-                        if halo is not None:        # the direct kernel reads the halo-extended slab
-                            parts = ([halo[0][:, :, :, :1]] if halo[1] else []) + [x] + \
-                                ([halo[0][:, :, :, 1:]] if halo[2] else [])
-                            xw = torch.cat(parts, dim=3)
-                            gw = ConvGeom(geo.k, geo.stride, (geo.pad[0], geo.pad[1], 1 - halo[1]), geo.out)
-                        check(L.m3d_conv3d_bwd_weight(ptr(xw), ptr(dz), B, H, W, xw.shape[3], Cin, kh, kw, kd,
-                                                      Cout, OH, OW, OD, *gw.stride, *gw.pad,
+                    if min(Cin, Cout) < WINO_WGRAD_MIN_C and halo is not None:
+                        # the direct kernel reads the neighbours' planes beside the slab
+                        check(L.m3d_conv3d_bwd_weight_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], 1, ptr(dz),
+                                                           B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
+                                                           *geo.stride, *geo.pad, ptr(grads["kernel"]), stream()),
+                              "conv3d_bwd_weight_halo")
+                    elif min(Cin, Cout) < WINO_WGRAD_MIN_C:
+                        check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd,
+                                                      Cout, OH, OW, OD, *geo.stride, *geo.pad,
                                                       ptr(grads["kernel"]), stream()), "conv3d_bwd_weight")
                     elif halo is not None and ctx.u is None:
                         wsw, wswb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
@@ -541,12 +548,20 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.halo = None
             return (dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None,
                     None, None)
+        if halo is not None and ctx.need_dx:
+            raise ValueError("the stem's halo form has no data gradient (its input is the volume)")
         if grads.get("kernel") is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 tw = _span()
-                check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
-                                              OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
-                                              stream()), "conv3d_bwd_weight")
+                if halo is not None:        # the stem on a depth slab: halo planes beside the slab
+                    check(L.m3d_conv3d_bwd_weight_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], halo[0].shape[3] // 2,
+                                                       ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
+                                                       *geo.stride, *geo.pad, ptr(grads["kernel"]), stream()),
+                          "conv3d_bwd_weight_halo")
+                else:
+                    check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
+                                                  OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
+                                                  stream()), "conv3d_bwd_weight")
                 if logging:
                     _log(f"conv{kh}_wgrad", direct, direct, 4.0 * (x.numel() + dz.numel() + w.numel()),
                          "bwd_weight", ctx.name, tw)
@@ -601,6 +616,13 @@ class _ConvBNAct(torch.autograd.Function):
         return dx, dr, None, None, None, None, None, None, None, None, None, None, None, None
 
 
+def _stem_halo(geo, cin, cout, res_mode):
+    """The one-channel 7^3 stem (core/models.py:242) in the shape whose kernel
+    reads halo planes beside a depth slab (m3d_conv3d_fwd_halo)."""
+    return (cin == 1 and cout == 64 and geo.k == (7, 7, 7) and geo.stride == (2, 2, 1) and res_mode == 0
+            and geo.pad[2] == 3 and geo.out[2] > 0)
+
+
 def _slab_extend(x, geo):
     """Under depth-slab sharding (m3d.slab.active), give a z-spanning window
     its neighbours' halo planes; z padding stays only where the volume ends."""
@@ -636,6 +658,10 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
             and use_winograd(geo, x.shape[-1], w.shape[-1], tuple(x.shape[1:4]))):
         # Winograd convs read the neighbours' planes beside the slab (no extended copy)
         halo = slab.halo_planes(x.contiguous(), 1)
+    elif (slab.current() is not None and SLAB_HALO_PLANES and _stem_halo(geo, x.shape[-1], w.shape[-1], res_mode)
+          and not (need_dx and x.requires_grad) and x.shape[3] >= geo.pad[2]):
+        # the 7^3 stem reads its 3 halo planes per side beside the slab
+        halo = slab.halo_planes(x.contiguous(), geo.pad[2])
     else:
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
@@ -672,6 +698,41 @@ class _MaxPool(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+class _MaxPoolHalo(torch.autograd.Function):
+    """Depth-slab max-pool reading the neighbours' halo planes beside the slab
+    (m3d_maxpool3d_fwd_halo): no halo-extended copy of the 64-channel C1 slab;
+    the backward returns the halo planes' gradient to their owners."""
+
+    @staticmethod
+    def forward(ctx, x, halo, k, stride, pad, out):
+        t0 = _span()
+        hp, has_lo, has_hi = halo
+        B, H, W, D, C = x.shape
+        r = hp.shape[3] // 2
+        y = torch.empty((B, *out, C), device=x.device, dtype=torch.float32)
+        am = torch.empty((B, *out, C), device=x.device, dtype=torch.uint8)
+        check(_L().m3d_maxpool3d_fwd_halo(ptr(x), ptr(hp), has_lo, has_hi, r, B, H, W, D, C, *k, *stride, *pad,
+                                          *out, ptr(y), ptr(am), stream()), "maxpool3d_fwd_halo")
+        _log("maxpool", 0, 0, 4.0 * (x.numel() + y.numel()), "fwd", "pool1", t0)
+        ctx.save_for_backward(am)
+        ctx.cfg = (tuple(x.shape), k, stride, pad, out, has_lo, has_hi, r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        shape, k, stride, pad, out, has_lo, has_hi, r = ctx.cfg
+        t0 = _span()
+        B, H, W, D, C = shape
+        dx = torch.empty(shape, device=dy.device, dtype=torch.float32)
+        dh = torch.empty((B, H, W, 2 * r, C), device=dy.device, dtype=torch.float32)
+        check(_L().m3d_maxpool3d_bwd_halo(ptr(dy.contiguous()), ptr(am), has_lo, has_hi, r, *shape, *k, *stride,
+                                          *pad, *out, ptr(dx), ptr(dh), stream()), "maxpool3d_bwd_halo")
+        _log("maxpool_bwd", 0, 0, 4.0 * (dy.numel() + dx.numel()) + am.numel(), "bwd_data", "pool1", t0)
+        slab.return_halo_grads(dx, dh, r)
+        return dx, None, None, None, None, None
+
+
 def max_pool3d(x, k, stride, padding="same"):
     """KL.MaxPooling3D(k, strides, padding) with TF SAME semantics."""
     sp = x.shape[1:4]
@@ -680,6 +741,12 @@ def max_pool3d(x, k, stride, padding="same"):
         out, pad = tuple(o for o, _ in op), tuple(p for _, p in op)
     else:
         out, pad = tuple(valid_out(n, kk, s) for n, kk, s in zip(sp, k, stride)), (0, 0, 0)
+    r = (k[2] - 1) // 2
+    if (slab.current() is not None and SLAB_HALO_PLANES and k[2] > 1 and stride[2] == 1 and pad[2] == r
+            and 2 * r + 1 == k[2] and x.shape[-1] % 4 == 0 and x.shape[3] >= r):
+        # the neighbours' planes beside the slab (no extended copy of C1)
+        xc = x.contiguous()
+        return _MaxPoolHalo.apply(xc, slab.halo_planes(xc, r), tuple(k), tuple(stride), pad, out)
     x, geo = _slab_extend(x.contiguous(), ConvGeom(tuple(k), tuple(stride), pad, out))
     return _MaxPool.apply(x.contiguous(), tuple(k), tuple(stride), geo.pad, out)
 

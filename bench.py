@@ -692,6 +692,27 @@ def mrcnn_inference_leg(S, steps, warmup, dev):
 
 
 # ---------------------------------------------------------------- CPU baseline
+def _host_cpus():
+    """The box's CPUs beside the thread count the baseline used: os.cpu_count()
+    (the whole machine), the CPUs this process may run on (its affinity / the
+    box's CPU share, which OMP_NUM_THREADS mirrors) and the lscpu model name."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
+
+
 def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
     """The oracle restatement timed on the host for the SAME step as the GPU
     leg: oracle/model_ref.py forward (torch-CPU fp32) -> the RPN losses of
@@ -745,6 +766,7 @@ def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
     t_rest = time.perf_counter() - t1
     t = t_net * (S / depth_slab) + t_rest
     return {"value": 1.0 / t, "unit": "volumes/s", "cores": torch.get_num_threads(), "kind": "port",
+            "host": _host_cpus(),
             "sample": f"one RPN training step (the GPU step's work) on the host: oracle/model_ref.py torch-CPU fp32 fwd + RPN "
                       f"losses + bwd on a {S}x{S}x{depth_slab} volume ({t_net:.1f} s"
                       + (f", scaled x{S // depth_slab}" if depth_slab != S else "")

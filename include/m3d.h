@@ -253,6 +253,25 @@ int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,
                           int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
                           int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dw,
                           m3d_stream_t s);
+/* Depth-slab forms of the direct convs (no halo-extended copy of the slab): x
+ * [B,H,W,Dl,Cin] is the local slab, halo [B,H,W,2r,Cin] the neighbours' r
+ * boundary planes (planes [0,r) from below, [r,2r) from above; has_lo / has_hi:
+ * that neighbour exists); the z window is 'same' kd = 2r+1 at stride 1 with
+ * pad pz = r applied only where the volume ends, OD = Dl.  Same taps and sums
+ * as the conv on the halo-extended slab.  fwd: the one-channel 7^3 stem only
+ * (core/models.py:242, 1 -> 64, strides (2,2,1)); bwd_weight: any direct conv
+ * (the stem, the 64-channel 3^3 convs of stage 2). */
+int m3d_conv3d_fwd_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi, int32_t r,
+                        int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin, const float* w,
+                        int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
+                        int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                        const float* bias, const float* bn_scale, const float* bn_shift, int32_t relu,
+                        float* z_out, float* y, m3d_stream_t s);
+int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi, int32_t r,
+                               const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
+                               int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW,
+                               int64_t OD, int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px,
+                               int32_t pz, float* dw, m3d_stream_t s);
 
 /* Winograd F(2x2x2,3x3x3) versions of the three passes for stride-1 3x3x3
  * convs with 'same' padding in y/x (every 3x3x3 conv of the graph:
@@ -476,6 +495,22 @@ int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t B, int64_t
                       int64_t D, int64_t C, int32_t kh, int32_t kw, int32_t kd, int32_t sy,
                       int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, int64_t OH,
                       int64_t OW, int64_t OD, float* dx, m3d_stream_t s);
+/* Depth-slab form of the pool (core/models.py:245 on one z-slab of the volume):
+ * x [B,H,W,Dl,C] is the local slab and halo [B,H,W,2r,C] the neighbours' r
+ * boundary planes (planes [0,r) from below, [r,2r) from above; has_lo / has_hi:
+ * that neighbour exists), read beside the slab instead of a halo-extended copy;
+ * z window kd = 2r+1 at stride 1 with 'same' pad pz = r (applied only where the
+ * volume ends), OD = Dl, C % 4 == 0.  The backward writes dx [B,H,W,Dl,C] and
+ * dhalo [B,H,W,2r,C] (the gradient of the neighbours' planes, to be returned to
+ * them).  Values and summation order are those of the pool on the extended slab. */
+int m3d_maxpool3d_fwd_halo(const float* x, const float* halo, int32_t has_lo, int32_t has_hi, int32_t r,
+                           int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t C, int32_t kh, int32_t kw,
+                           int32_t kd, int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                           int64_t OH, int64_t OW, int64_t OD, float* y, uint8_t* argmax, m3d_stream_t s);
+int m3d_maxpool3d_bwd_halo(const float* dy, const uint8_t* argmax, int32_t has_lo, int32_t has_hi, int32_t r,
+                           int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t C, int32_t kh, int32_t kw,
+                           int32_t kd, int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz,
+                           int64_t OH, int64_t OW, int64_t OD, float* dx, float* dhalo, m3d_stream_t s);
 /* d_src[b,y,x,z,c] (+)= sum_{i,j in {0,1}} d_up[b,2y+i,2x+j,z,c]  (UpSampling3D((2,2,1)) bwd) */
 int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C,
                         float* d_src, int32_t accumulate, m3d_stream_t s);
