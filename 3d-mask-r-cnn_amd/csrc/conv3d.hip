@@ -30,6 +30,7 @@
 namespace m3d {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct ConvP {
     const float* a;   // A source (x or dz), channels-last [B,H,W,D,C]
@@ -3209,6 +3210,143 @@ static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, i
            dly == 1 && dlx == 1 && dlz == 1 && res_mode == 0 && split_n <= 0 && (ldy <= 0 || ldy == 64);
 }
 
+// ---- the stem's weight gradient: dW[343][64] += sum_m window(m)[tap] dz[m][ch] ----
+// The implicit-GEMM weight gradient reads the one-channel window through its
+// scalar loader (0.27 of the f32 MFMA peak).  Here a workgroup (8 waves) loops
+// over a contiguous range of m-tiles (one output column (oy, ox) x 32 z); per
+// tile the 49 x 38 input window (the same fetch as stem_fwd_kernel, halo planes
+// included) and the 32 x 64 dz rows are staged in LDS (double-buffered, one
+// barrier per tile) and every wave accumulates its 11 of the 88 16 x 16 dW
+// tiles (v_mfma_f32_16x16x4_f32: one n-tile of 16 channels x 11 k-tiles of 16
+// taps) over the tile's 32 m in steps of 4.  A lane's window offset per k-tile
+// is precomputed (tap -> R * 38 + kz), so every operand read is a ds_read_b32
+// with an immediate offset.  Taps 343..351 read the zero row.  The partial dW
+// leaves through wg_put (fp32 atomics, or the deterministic-mode partials).
+constexpr int SWG_STR = 80;                                      // dz staging row stride (floats)
+__global__ __launch_bounds__(512) void stem_wgrad_kernel(ConvP p, const float* __restrict__ dz,
+                                                         float* __restrict__ dw, WgOut wo, int tz_n,
+                                                         int64_t ntiles, int64_t per_block) {
+    __shared__ float win[2][STEM_WIN];            // 49 rows x 38 z + the zero row
+    __shared__ float dzs[2][STEM_TZ * SWG_STR];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t t_begin = (int64_t)blockIdx.x * per_block;
+    const int64_t t_end = t_begin + per_block < ntiles ? t_begin + per_block : ntiles;
+    if (t_begin >= t_end) return;
+    float* const wp = wo.part ? wo.part + (int64_t)blockIdx.x * wo.pstride : nullptr;
+    if (tid < STEM_WZ) { win[0][49 * STEM_WZ + tid] = 0.0f; win[1][49 * STEM_WZ + tid] = 0.0f; }
+    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    // per tile: window values i = tid + 512 q (q < 4), dz float4 tid
+    float wv[4];
+    float4 dv;
+    auto fetch = [&](int64_t tile) {
+        int64_t t = tile;
+        const int tz = (int)(t % tz_n); t /= tz_n;
+        const int ox = (int)(t % p.OW); t /= p.OW;
+        const int oy = (int)(t % p.OH);
+        const int b = (int)(t / p.OH);
+        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
+        const float* xb = p.a + b * img;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = tid + 512 * q;
+            float val = 0.0f;
+            if (i < 49 * STEM_WZ) {
+                const int R = i / STEM_WZ, iz = i - R * STEM_WZ;
+                const int gy = gy0 + R / 7, gx = gx0 + R % 7, gz = gz0 + iz;
+                if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && gz >= 0 && gz < p.D) {
+                    if (p.halo) {
+                        const int zl = gz - p.hnlo;
+                        if ((unsigned)zl < (unsigned)p.hdl)
+                            val = xb[gy * row + gx * plane + zl];
+                        else
+                            val = p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
+                                         (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
+                    } else {
+                        val = xb[gy * row + gx * plane + gz];
+                    }
+                }
+            }
+            wv[q] = val;
+        }
+        const int zi = tid >> 4, c4 = tid & 15;          // 32 rows x 16 float4
+        const int oz = tz * STEM_TZ + zi;
+        dv = oz < p.OD ? *reinterpret_cast<const float4*>(
+                             dz + ((((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD + oz) * 64 + c4 * 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (tid + 512 * q < 49 * STEM_WZ) win[buf][tid + 512 * q] = wv[q];
+        *reinterpret_cast<float4*>(&dzs[buf][(tid >> 4) * SWG_STR + (tid & 15) * 4]) = dv;
+    };
+    // this wave: n-tile nt (16 channels), k-tiles kt = kg + 2 j (j < 11) of 16 taps
+    const int nt = wave & 3, kg = wave >> 2;
+    const int l16 = lane & 15, lq = lane >> 4;
+    int abase[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+        const int tap = 16 * (kg + 2 * j) + l16;
+        const int R = tap < 343 ? tap / 7 : 49, kz = tap < 343 ? tap % 7 : 0;
+        abase[j] = R * STEM_WZ + kz + lq;
+    }
+    const int bbase = lq * SWG_STR + nt * 16 + l16;
+    floatx4 acc[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    fetch(t_begin);
+    stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t t = t_begin; t < t_end; ++t) {
+        if (t + 1 < t_end) fetch(t + 1);
+        const float* W = win[buf];
+        const float* Z = dzs[buf];
+#pragma unroll
+        for (int s = 0; s < STEM_TZ / 4; ++s) {
+            const float bv = Z[bbase + 4 * s * SWG_STR];
+#pragma unroll
+            for (int j = 0; j < 11; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(W[abase[j] + 4 * s], bv, acc[j], 0, 0, 0);
+        }
+        if (t + 1 < t_end) stage(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int j = 0; j < 11; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int tap = 16 * (kg + 2 * j) + 4 * lq + r;
+            if (tap < 343) wg_put(wo, dw, wp, (int64_t)tap * 64 + nt * 16 + l16, acc[j][r]);
+        }
+}
+
+static bool stem_wgrad_env() {
+    static const int v = [] { const char* e = getenv("M3D_STEM_WGRAD"); return e ? atoi(e) : 1; }();
+    return v != 0;
+}
+
+static int launch_stem_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
+    const int64_t ntiles = (int64_t)p.B * p.OH * p.OW * tz_n;
+    // two workgroups per CU (LDS 2 x 23.4 KB each, 8 waves), >= 8 m-tiles each
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)ncu, (ntiles + 7) / 8));
+    const WgOut wo = wg_out(blocks, 1, 343, 64);
+    const int64_t per = (ntiles + blocks - 1) / blocks;
+    blocks = (ntiles + per - 1) / per;
+    hipLaunchKernelGGL(stem_wgrad_kernel, dim3((unsigned)blocks), dim3(512), 0, s, p, dz, dw, wo, tz_n, ntiles, per);
+    wg_finish(wo, blocks, 1, 343, 64, 343 * 64, dw, s);
+    return check_launch("stem_wgrad_kernel");
+}
+
 static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     static int ncu = [] {
         int dev = 0, n = 0;
@@ -3493,6 +3631,8 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
     const bool vec = (Cin % 4) == 0;
+    if (stem_wgrad_env() && stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
+        return launch_stem_wgrad(p, dz, dw, st(s));
     // 1x1x1 stride-1 convs: im2col is x itself, the plain weight-gradient GEMM
     // dW += x^T dz -- on the exact bf16 split like the Winograd ones
     if (vec && ((x3_mask() >> 3) & 1) && kh == 1 && kw == 1 && kd == 1 && sy == 1 && sx == 1 && sz == 1 &&
@@ -3572,6 +3712,8 @@ extern "C" int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
     if ((rc = conv_halo_geom(p, halo, has_lo, has_hi, r, Dl, kd, sz, pz, OD))) return rc;
+    if (stem_wgrad_env() && stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
+        return launch_stem_wgrad(p, dz, dw, st(s));
     const bool vec = (Cin % 4) == 0;
     if (Cout <= 64) {
         if (vec) launch_wgrad<128, 64, 2, 2, true, true>(p, dz, dw, st(s));

@@ -350,7 +350,11 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
                             base + by * rowW + lx * rowD, base + by * rowW + rx * rowD};
     int pk = -1;
     float4 kv[4];
-    auto sample = [&](int z) -> float4 {
+    // (no lambda around the body: capturing col / kv by reference put them in scratch)
+    float4 res[PD > 0 ? PD : 1];
+    const int z0_ = PD > 0 ? 0 : zb, z1_ = PD > 0 ? PD : ze;
+#pragma unroll
+    for (int z = z0_; z < z1_; ++z) {
         const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
         float4 r;
         if (in_z < 0 || in_z > (float)(D - 1)) {
@@ -377,16 +381,12 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
             r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
             r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
         }
-        return r;
-    };
+        if constexpr (PD > 0) res[z] = r;
+        else st_nt(o + (int64_t)z * C4 + c, r);
+    }
     if constexpr (PD > 0) {
-        float4 res[PD];
-#pragma unroll
-        for (int z = 0; z < PD; ++z) res[z] = sample(z);
 #pragma unroll
         for (int z = 0; z < PD; ++z) st_nt(o + (int64_t)z * C4 + c, res[z]);
-    } else {
-        for (int z = zb; z < ze; ++z) st_nt(o + (int64_t)z * C4 + c, sample(z));
     }
 }
 
@@ -1411,7 +1411,12 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             const int32_t* wperm = nullptr;
             int64_t nb = 0, nl = 0;
             const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
-            static const int sort_env = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : 0; }();
+            // default order: waves sorted by their feature-map column (mode 3) for the
+            // 14^3 mask pool -- PMC fabric reads at 256^3 / 512 ROIs 3.41 -> 1.89 GB,
+            // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for the 7^3 pool
+            // (its lines are short and the sort does not pay); M3D_ROI_SORT overrides
+            static const int sort_env0 = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : -1; }();
+            const int sort_env = sort_env0 >= 0 ? sort_env0 : (pd >= 14 ? 3 : 0);
             if (sort_env == 2 && workspace && ws_bytes >= need && nl < INT32_MAX && B * N <= nb) {
                 // ROI order: keys [B*N] (uint64, 8-B aligned at the start), inv [B*N], perm [lines]
                 uint64_t* rkeys = (uint64_t*)workspace;
@@ -1467,7 +1472,9 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             const int zs = wperm ? 1 : std::max(1, std::min(zs_env, (int)pd));
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
-            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 1; }();
+            // register-staged outputs (M3D_ROI_STAGE=1): 138 VGPRs halve the occupancy,
+            // 14^3 at 256^3 0.87 -> 1.11 ms; off
+            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 0; }();
             if (sl == 8 && zs == 1 && stage_env && (pd == 7 || pd == 14)) {
                 if (pd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);

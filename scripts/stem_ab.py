@@ -1,7 +1,8 @@
-"""Stem conv (conv1: 7^3, 1 -> 64, strides (2,2,1), ZeroPadding3D(3)) forward:
-time per launch at 128^3 / 256^3 through m3d_conv3d_fwd (M3D_STEM_MFMA picks
-the kernel, read once per process) and the error against torch's fp32 conv3d
-(MIOpen) on the same input.  python scripts/stem_ab.py"""
+"""Stem conv (conv1: 7^3, 1 -> 64, strides (2,2,1), ZeroPadding3D(3)) forward
+and weight gradient: time per launch at 128^3 / 256^3 through m3d_conv3d_fwd /
+m3d_conv3d_bwd_weight (M3D_STEM_MFMA / M3D_STEM_WGRAD pick the kernels, read
+once per process) and the error against torch's fp32 conv3d and its weight
+gradient (MIOpen) on the same input.  python scripts/stem_ab.py"""
 import json
 import os
 import sys
@@ -38,9 +39,23 @@ for S in (128, 256):
     ez = float((z - ref).abs().max() / ref.abs().max())
     yr = torch.relu(ref * sc + sh)
     ey = float((y - yr).abs().max() / yr.abs().max())
+    dz = torch.randn((1, O, O, S, 64), device=dev, generator=g)
+    dw = torch.zeros_like(w)
+
+    def runw():
+        _lib.check(L.m3d_conv3d_bwd_weight(x.data_ptr(), dz.data_ptr(), 1, S, S, S, 1, 7, 7, 7, 64, O, O, S,
+                                           2, 2, 1, 3, 3, 3, dw.data_ptr(), _lib.stream()), "stem wgrad")
+    tw = bench._event_time(runw, 10)
+    dw.zero_()
+    runw()
+    refw = torch.nn.grad.conv3d_weight(x.permute(0, 4, 1, 2, 3), (64, 1, 7, 7, 7), dz.permute(0, 4, 1, 2, 3),
+                                       stride=(2, 2, 1), padding=3).permute(2, 3, 4, 1, 0)
+    ew = float((dw - refw).abs().max() / refw.abs().max())
     res[f"S{S}"] = {"ms": round(t * 1e3, 4), "tflops": round(flops / t / 1e12, 2),
                     "frac_f32_mfma": round(flops / t / 1e12 / bench.F32_MFMA_PEAK_TFLOPS, 4),
-                    "rel_err_z": ez, "rel_err_y": ey}
-    del x, y, z, ref, yr
+                    "rel_err_z": ez, "rel_err_y": ey,
+                    "wgrad_ms": round(tw * 1e3, 4), "wgrad_frac_f32_mfma":
+                        round(flops / tw / 1e12 / bench.F32_MFMA_PEAK_TFLOPS, 4), "rel_err_dw": ew}
+    del x, y, z, ref, yr, dz, refw
     torch.cuda.empty_cache()
 print(json.dumps(res), flush=True)
