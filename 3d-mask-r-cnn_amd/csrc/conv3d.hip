@@ -1606,6 +1606,10 @@ struct WinoGeom {
     // of the slab read from halo [B][H][W][2][C] (plane 0 / 1) when present
     const float* halo;
     int hlo, hhi;
+    // z-tile subset of an input-transform launch (depth-slab overlap of the halo
+    // exchange): 0 all tiles, 1 interior only (tz in [1, TZ-1): no halo plane in
+    // the window), 2 the first / last z tile only
+    int tz_mode;
 };
 
 __device__ __forceinline__ void bt4(float& a0, float& a1, float& a2, float& a3) {
@@ -1733,6 +1737,10 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     const int64_t t = i / C;
     int b, ty, tx, tz;
     tile_coords(t, g, b, ty, tx, tz);
+    if (g.tz_mode) {
+        const bool edge = tz == 0 || tz == g.TZ - 1;
+        if ((g.tz_mode == 1) == edge) return;
+    }
     float d[4][4][P];
     // branch-free window loads: raw buffer loads whose out-of-range offset
     // returns 0 (the zero padding), so all 16*P loads issue back to back
@@ -2855,6 +2863,7 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     g.T = B * g.TY * g.TX * g.TZ;
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
+    g.tz_mode = 0;
     return g;
 }
 
@@ -3201,6 +3210,170 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
     }
 }
 
+// ---- the stem forward on the exact bf16 split (default) ----------------------
+// stem_fwd_kernel above runs the f32 MFMA (1/16 of the bf16 rate), which bounds
+// it near 1.2 ms at 256^3 even at full issue.  Here the product runs as 6
+// v_mfma_f32_32x32x16_bf16 on the 3-way split of both operands (as the
+// Winograd GEMMs; exact to the f32 rounding).  The bf16 MFMA wants 8
+// consecutive k per lane as one 16-B read, so K is ordered k = kz * 56 + R
+// (R = ky * 7 + kx padded 49 -> 56, kz padded 7 -> 8 in the last chunk: 25
+// chunks of 16) and each wave's window is stored TRANSPOSED, [z (40)][R (56)]
+// bf16 per plane: a lane (output z m, k-group g) reads window[m + kz][R0 .. R0+7]
+// with R0 = k0 % 56 a multiple of 8 -- 16-B aligned, rows 112 B apart
+// (conflict-free over 16 lanes).  A workgroup = 4 waves and one 32-channel
+// half of the output (weights [plane][n][k] in LDS, 76.8 KB); every wave owns
+// its tile (one output column x 32 z x 32 channels: ONE accumulator) and its
+// window (13.4 KB), refilled from registers prefetched during the previous
+// tile's MFMAs; lanes load (z, R-pair) values so each plane gets one b32 write
+// per pair.  Same epilogue order as epi_store4 (bias, z, frozen BN, activation).
+constexpr int SX_R = 56, SX_ZR = 40, SX_KC = 25, SX_K = SX_KC * 16;
+constexpr int SX_PL = SX_ZR * SX_R * 2;          // window plane bytes (4480)
+constexpr int SX_WPL = 32 * SX_K * 2;            // weight plane bytes (25600)
+constexpr int SX_PAIRS = 38 * 25;                // (z, R pair) values per window: R 0..49 (49 = pad)
+constexpr int SX_PER = (SX_PAIRS + 63) / 64;     // 15 per lane
+constexpr int SX_SLD = 36;                       // epilogue staging row stride (floats)
+
+__global__ __launch_bounds__(256, 1) void stem_fwd_x3_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char wsh[3 * SX_WPL];
+    __shared__ __attribute__((aligned(16))) char win[4][3 * SX_PL];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hc = blockIdx.x & 1;                                   // output channels hc*32 .. +31
+    for (int i = tid; i < 32 * SX_K; i += 256) {
+        const int n = i / SX_K, k = i - n * SX_K;
+        const int kz = k / SX_R, R = k - kz * SX_R;
+        const float v = (kz < 7 && R < 49) ? p.w[(R * 7 + kz) * 64 + hc * 32 + n] : 0.0f;
+        uint32_t h, m, l;
+        split3(v, h, m, l);
+        unsigned short* W = reinterpret_cast<unsigned short*>(wsh);
+        W[i] = (unsigned short)h;
+        W[32 * SX_K + i] = (unsigned short)m;
+        W[64 * SX_K + i] = (unsigned short)l;
+    }
+    char* ww = win[wave];
+    for (int i = lane; i < SX_ZR * SX_R; i += 64) {                  // pad cells stay zero
+        const int zz = i / SX_R, R = i - zz * SX_R;
+        if (R >= 49 || zz >= 38)
+            for (int pl = 0; pl < 3; ++pl) reinterpret_cast<unsigned short*>(ww + pl * SX_PL)[i] = 0;
+    }
+    __syncthreads();
+    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
+        tz = (int)(t % tz_n); t /= tz_n;
+        ox = (int)(t % p.OW); t /= p.OW;
+        oy = (int)(t % p.OH);
+        b = (int)(t / p.OH);
+    };
+    auto xval = [&](const float* xb, int b, int gy, int gx, int gz) -> float {
+        if (gy < 0 || gy >= p.H || gx < 0 || gx >= p.W || gz < 0 || gz >= p.D) return 0.0f;
+        if (p.halo) {
+            const int zl = gz - p.hnlo;
+            if ((unsigned)zl < (unsigned)p.hdl) return xb[gy * row + gx * plane + zl];
+            return p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
+                          (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
+        }
+        return xb[gy * row + gx * plane + gz];
+    };
+    auto fetch = [&](int64_t tile, float (&v)[SX_PER][2]) {
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
+        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
+        const float* xb = p.a + b * img;
+#pragma unroll
+        for (int q = 0; q < SX_PER; ++q) {
+            const int j = lane + 64 * q;
+            v[q][0] = v[q][1] = 0.0f;
+            if (j < SX_PAIRS) {
+                const int zz = j / 25, rp = j - zz * 25;
+                const int R0 = 2 * rp, R1 = R0 + 1;
+                v[q][0] = xval(xb, b, gy0 + R0 / 7, gx0 + R0 % 7, gz0 + zz);
+                if (R1 < 49) v[q][1] = xval(xb, b, gy0 + R1 / 7, gx0 + R1 % 7, gz0 + zz);
+            }
+        }
+    };
+    auto stage = [&](const float (&v)[SX_PER][2]) {
+#pragma unroll
+        for (int q = 0; q < SX_PER; ++q) {
+            const int j = lane + 64 * q;
+            if (j < SX_PAIRS) {
+                const int zz = j / 25, rp = j - zz * 25;
+                uint32_t h0, m0, l0, h1, m1, l1;
+                split3(v[q][0], h0, m0, l0);
+                split3(v[q][1], h1, m1, l1);
+                const int off = (zz * SX_R + 2 * rp) * 2;
+                *reinterpret_cast<uint32_t*>(ww + off) = h0 | (h1 << 16);
+                *reinterpret_cast<uint32_t*>(ww + SX_PL + off) = m0 | (m1 << 16);
+                *reinterpret_cast<uint32_t*>(ww + 2 * SX_PL + off) = l0 | (l1 << 16);
+            }
+        }
+    };
+    const int g = lane >> 5, l32 = lane & 31;
+    const char* wb = wsh + (l32 * SX_K + 8 * g) * 2;                 // B: column n = l32, k = 16c + 8g
+    const char* wa = ww + l32 * (SX_R * 2);                          // A: row m = l32
+    const int n = hc * 32 + 4 * (lane & 7);
+    const float4 bb = e.bias ? ld4(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 sc = e.scale ? ld4(e.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 sh = e.scale ? ld4(e.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t w0 = (int64_t)(blockIdx.x >> 1) * 4 + wave, wstride = (int64_t)(gridDim.x >> 1) * 4;
+    float pre[SX_PER][2];
+    if (w0 < ntiles) fetch(w0, pre);
+    for (int64_t tile = w0; tile < ntiles; tile += wstride) {
+        stage(pre);
+        __builtin_amdgcn_wave_barrier();
+        if (tile + wstride < ntiles) fetch(tile + wstride, pre);      // next window in flight
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < SX_KC; ++c) {
+            // k0 = 16c + 8g: kz = k0 / 56, R0 = k0 % 56 (both halves of a chunk within one kz
+            // except where 16c + 8 crosses a multiple of 56)
+            const int k0a = 16 * c, k0b = 16 * c + 8;
+            const int offa = (k0a / SX_R) * (SX_R * 2) + (k0a % SX_R) * 2;
+            const int offb = (k0b / SX_R) * (SX_R * 2) + (k0b % SX_R) * 2;
+            const int aoff = g ? offb : offa;
+            bf16x8 af[3], bw[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                af[pl] = *reinterpret_cast<const bf16x8*>(wa + pl * SX_PL + aoff);
+                bw[pl] = *reinterpret_cast<const bf16x8*>(wb + pl * SX_WPL + c * 32);
+            }
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bw[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bw[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bw[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[0], acc, 0, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();          // window reads done before the staging writes
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
+        float* st = reinterpret_cast<float*>(ww);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * g) * SX_SLD + l32] = acc[r];
+        __builtin_amdgcn_wave_barrier();
+        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
+        const int oz0 = tz * STEM_TZ;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {                 // 32 rows x 8 float4 = 4 per lane
+            const int rr = (lane >> 3) + 8 * q;
+            float4 v = *reinterpret_cast<const float4*>(st + rr * SX_SLD + 4 * (lane & 7));
+            if (oz0 + rr >= p.OD) continue;
+            const int64_t m = mbase + oz0 + rr;
+            if (e.bias) { v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w; }
+            if (e.z) st4(e.z + m * 64 + n, v);
+            if (e.scale) {
+                v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
+                v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
+            }
+            if (e.relu) {
+                v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
+            }
+            st4(e.y + m * 64 + n, v);
+        }
+        __builtin_amdgcn_wave_barrier();          // staging reads done before the next window
+    }
+}
+
 static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, int sx, int sz, int dly, int dlx,
                     int dlz, int res_mode, int64_t split_n, int64_t ldy) {
     static const int env = [] { const char* v = getenv("M3D_STEM_MFMA"); return v ? atoi(v) : 1; }();
@@ -3362,6 +3535,14 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     // one-CU NMS reduce) may still hold a CU, and a persistent block waiting
     // for that CU would stall the whole launch (measured 1.5 ms in the step
     // vs 0.28 ms alone at 128^3); with 4 per CU the others absorb its share
+    static const int x3 = [] { const char* v = getenv("M3D_STEM_X3"); return v ? atoi(v) : 1; }();
+    if (x3) {
+        // one workgroup per CU (131 KB of LDS): pairs of workgroups take the two
+        // 32-channel halves of the same tiles, each wave its own tiles
+        const unsigned grid = (unsigned)(2 * std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, ncu / 2)));
+        hipLaunchKernelGGL(stem_fwd_x3_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
+        return check_launch("stem_fwd_x3_kernel");
+    }
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 7) / 8, 4 * (int64_t)ncu));
     hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, tz_n, ntiles);
     return check_launch("stem_fwd_kernel");
@@ -4036,11 +4217,13 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
                     const float* bn_scale, const float* bn_shift, const float* residual,
                     int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
                     size_t ws_bytes, hipStream_t s, const float* halo = nullptr, int hlo = 0, int hhi = 0,
-                    bool v_ready = false) {
+                    bool v_ready = false, int phase = 0) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd: workspace too small");
+    if (phase && wino_per_item(B, H, W, D, OD, Cin, Cout))
+        return einval("conv3d winograd: a phased launch needs a batch within the 32-bit operand bound");
     if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {
         if (u_keep) return einval("conv3d winograd: u_keep with a batch past the 32-bit operand bound");
         const int64_t os = H * W * OD * Cout;
@@ -4056,16 +4239,29 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     WinoGeom g = wino_geom(B, H, W, OD, D, pz);
     g.halo = halo; g.hlo = hlo; g.hhi = hhi;
     WinoWs ws = wino_ws(workspace, g, Cin, Cout);
+    // phase 1 (depth slab, halo exchange in flight): weight transform + the
+    // interior z tiles' input transform (no halo plane in their windows);
+    // phase 2: the first / last z tiles (halo planes now present), GEMM, output
+    WinoGeom gi = g, ge = g;
+    if (phase) {
+        gi.tz_mode = 1; gi.halo = nullptr; gi.hlo = gi.hhi = 0;
+        ge.tz_mode = 2;
+    }
     if (gemm_x3_env() && !u_keep) {
         float* wt = ws.WT;
-        if (!v_ready) {     // v_ready: V already holds this w's transform (an earlier call, same workspace)
+        if (!v_ready && phase != 2) {     // v_ready: V already holds this w's transform (an earlier call, same workspace)
             hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
                                dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
             WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
                               (int)Cin, (int)Cout, 0, ws.V);
         }
         const bool af32 = x3_af32_env();
-        WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
+        if (phase == 1) {
+            WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, gi, (int)Cin, ws.U);
+            return check_launch("conv3d winograd fwd (x3, phase 1)");
+        }
+        if (phase == 2) WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, ge, (int)Cin, ws.U);
+        else WINO_INPUT(wino_nz(), !af32, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
         wino_gemm_x3(ws, g.T, (int)Cin, (int)Cout, wino_points(), s, af32);
         Epi o{};
         o.bias = bias; o.scale = bn_scale; o.shift = bn_shift; o.res = residual;
@@ -4075,9 +4271,14 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
         return check_launch("conv3d winograd fwd (x3)");
     }
     if (u_keep) ws.U = u_keep;
-    WINO_LAUNCH(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
-                       (int)Cin, (int)Cout, 0, ws.V);
-    WINO_INPUT(wino_nz(), false, dim3(grid_for(g.T * Cin, 256)), s, x, g, (int)Cin, ws.U);
+    if (phase != 2)
+        WINO_LAUNCH(wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, w,
+                           (int)Cin, (int)Cout, 0, ws.V);
+    if (phase == 1) {
+        WINO_INPUT(wino_nz(), false, dim3(grid_for(g.T * Cin, 256)), s, x, gi, (int)Cin, ws.U);
+        return check_launch("conv3d winograd fwd (phase 1)");
+    }
+    WINO_INPUT(wino_nz(), false, dim3(grid_for(g.T * Cin, 256)), s, x, phase == 2 ? ge : g, (int)Cin, ws.U);
     ConvP p = wino_gemm_p(ws.U, g.T, (int)Cin, ws.V, (int)Cout);
     Epi e{};
     e.y = ws.M; e.ldy = Cout; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
@@ -4297,6 +4498,28 @@ extern "C" int m3d_conv3d_fwd_wino_halo(const float* x, const float* x_halo, int
         return einval("conv3d winograd: forward and weight-gradient tiles differ (m3d_conv3d_wino_u_bytes == 0)");
     return fwd_wino(x, B, H, W, Dl, Cin, w, Cout, Dl, 1, bias, bn_scale, bn_shift, residual, relu, z_out, y,
                     u_keep, workspace, ws_bytes, st(s), x_halo, has_lo, has_hi);
+}
+
+// The same conv in two launches around the halo exchange: phase 1 (before the
+// halo planes arrive; x_halo is not read) transforms the weights and the
+// interior z tiles, phase 2 (after) the first / last z tiles, then the GEMM
+// and the output transform -- the caller overlaps the exchange with phase 1.
+// Both phases take the same arguments and workspace; bit-identical to
+// m3d_conv3d_fwd_wino_halo.
+extern "C" int m3d_conv3d_fwd_wino_halo_phase(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi,
+                                              int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
+                                              const float* w, int64_t Cout, const float* bias, const float* bn_scale,
+                                              const float* bn_shift, const float* residual, int32_t relu,
+                                              float* z_out, float* y, float* u_keep, void* workspace,
+                                              size_t ws_bytes, int32_t phase, m3d_stream_t s) {
+    if (phase != 1 && phase != 2) return einval("conv3d winograd halo: phase must be 1 or 2");
+    int rc = phase == 2 ? halo_check(x_halo, has_lo, has_hi) : M3D_OK;
+    if (rc) return rc;
+    if (u_keep && wino_nz() != wino_wgrad_nz())
+        return einval("conv3d winograd: forward and weight-gradient tiles differ (m3d_conv3d_wino_u_bytes == 0)");
+    return fwd_wino(x, B, H, W, Dl, Cin, w, Cout, Dl, 1, bias, bn_scale, bn_shift, residual, relu, z_out, y,
+                    u_keep, workspace, ws_bytes, st(s), phase == 2 ? x_halo : nullptr, has_lo, has_hi, false,
+                    phase);
 }
 
 // dx [B,H,W,Dl,Cin] (interior, accumulate as m3d_conv3d_bwd_data_wino) and

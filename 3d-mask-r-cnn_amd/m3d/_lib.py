@@ -73,6 +73,8 @@ _SIGS = {
                               c_p, c_p],
     "m3d_conv3d_fwd_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p,
                                  c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_fwd_wino_halo_phase": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                                       c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_i32, c_p],
     "m3d_conv3d_bwd_data_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
                                       c_p, c_i32, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_weight_wino_halo": [c_p, c_p, c_i32, c_i32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,

@@ -127,6 +127,11 @@ def _L():
 # halo-extended copy of every z-window input instead (torch.cat, the old path)
 SLAB_HALO_PLANES = os.environ.get("M3D_SLAB_HALO_PLANES", "1") != "0"
 
+# ... and post the exchange before the Winograd conv's first launch phase
+# (m3d_conv3d_fwd_wino_halo_phase 1: weights + interior z tiles), waiting only
+# before phase 2 (M3D_SLAB_OVERLAP=0: exchange, then the one-launch conv)
+SLAB_OVERLAP = os.environ.get("M3D_SLAB_OVERLAP", "1") != "0"
+
 # big-K 1x1x1 stride-1 convs on the bf16-split GEMM (M3D_CONV1_X3=0: the f32 direct kernel)
 CONV1_X3 = os.environ.get("M3D_CONV1_X3", "1") != "0"
 # split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
@@ -349,7 +354,12 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.name = name
         B, H, W, D, Cin = x.shape
         # depth slab (m3d.slab): halo = (planes [B,H,W,2,C], has_lo, has_hi) read by the
-        # Winograd kernels beside x instead of a halo-extended copy of x
+        # Winograd kernels beside x instead of a halo-extended copy of x; a
+        # slab.PendingHalo (exchange still in flight) is resolved between the two
+        # launch phases of the Winograd conv below
+        pending = halo if isinstance(halo, slab.PendingHalo) else None
+        if pending is not None:
+            halo = (None, pending.has_lo, pending.has_hi)
         ctx.halo = halo
         kh, kw, kd = geo.k
         Cout = w.shape[-1]
@@ -387,7 +397,17 @@ class _ConvBNAct(torch.autograd.Function):
             nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4 \
                 if grads is not None and grads.get("kernel") is not None \
                 and min(Cin, Cout) >= WINO_WGRAD_MIN_C else 0
-            if halo is not None:
+            if pending is not None:
+                # phase 1 (weights + interior z tiles) overlaps the halo transfer
+                ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
+                args = (B, H, W, D, Cin, ptr(w), Cout, ptr(b), ptr(scale), ptr(shift), ptr(residual),
+                        1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u), ptr(ws), wsb)
+                check(_L().m3d_conv3d_fwd_wino_halo_phase(ptr(x), None, halo[1], halo[2], *args, 1, stream()),
+                      "conv3d_fwd_wino_halo_phase1")
+                halo = ctx.halo = pending.result()
+                check(_L().m3d_conv3d_fwd_wino_halo_phase(ptr(x), ptr(halo[0]), halo[1], halo[2], *args, 2,
+                                                          stream()), "conv3d_fwd_wino_halo_phase2")
+            elif halo is not None:
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
                 check(_L().m3d_conv3d_fwd_wino_halo(ptr(x), ptr(halo[0]), halo[1], halo[2], B, H, W, D, Cin,
                                                     ptr(w), Cout, ptr(b), ptr(scale), ptr(shift), ptr(residual),
@@ -656,8 +676,9 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
     halo = None
     if (slab.current() is not None and SLAB_HALO_PLANES and res_mode != 2
             and use_winograd(geo, x.shape[-1], w.shape[-1], tuple(x.shape[1:4]))):
-        # Winograd convs read the neighbours' planes beside the slab (no extended copy)
-        halo = slab.halo_planes(x.contiguous(), 1)
+        # Winograd convs read the neighbours' planes beside the slab (no extended copy);
+        # the exchange overlaps the conv's weight transform and interior z tiles
+        halo = (slab.halo_planes_start if SLAB_OVERLAP else slab.halo_planes)(x.contiguous(), 1)
     elif (slab.current() is not None and SLAB_HALO_PLANES and _stem_halo(geo, x.shape[-1], w.shape[-1], res_mode)
           and not (need_dx and x.requires_grad) and x.shape[3] >= geo.pad[2]):
         # the 7^3 stem reads its 3 halo planes per side beside the slab

@@ -96,9 +96,11 @@ class SlabGroup:
         dev = "cpu" if self.host_staging else like.device
         return torch.empty(shape, dtype=like.dtype, device=dev)
 
-    def exchange(self, to_lo, to_hi, shape):
-        """Send to_lo to the lower / to_hi to the upper neighbour; receive a
-        `shape` tensor from each neighbour present.  Returns (from_lo, from_hi)."""
+    def exchange_start(self, to_lo, to_hi, shape):
+        """Post the exchange of exchange() and return at once; the returned
+        finish() waits for it (on RCCL: makes the current stream wait for the
+        communicator's stream -- no host sync) and returns (from_lo, from_hi).
+        Work enqueued in between overlaps the transfer."""
         like = to_lo if to_lo is not None else to_hi
         ops, recv = [], [None, None]
         if self.lo is not None:
@@ -109,12 +111,22 @@ class SlabGroup:
             recv[1] = self._buf(shape, like)
             ops += [dist.P2POp(dist.isend, self._out(to_hi), self.hi, self.halo_group),
                     dist.P2POp(dist.irecv, recv[1], self.hi, self.halo_group)]
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
+        works = dist.batch_isend_irecv(ops) if ops else []
+
+        def finish():
+            for req in works:
                 req.wait()
-        if self.host_staging and like.is_cuda:
-            recv = [None if r is None else r.to(like.device, non_blocking=False) for r in recv]
-        return recv[0], recv[1]
+            r = recv
+            if self.host_staging and like.is_cuda:
+                r = [None if t is None else t.to(like.device, non_blocking=False) for t in recv]
+            ops.clear()                    # the send buffers lived until here
+            return r[0], r[1]
+        return finish
+
+    def exchange(self, to_lo, to_hi, shape):
+        """Send to_lo to the lower / to_hi to the upper neighbour; receive a
+        `shape` tensor from each neighbour present.  Returns (from_lo, from_hi)."""
+        return self.exchange_start(to_lo, to_hi, shape)()
 
     def all_gather(self, t):
         """[world, *t.shape] stack of every rank's t."""
@@ -218,6 +230,44 @@ def halo_planes(x, r=1):
     if from_hi is not None:
         halo[:, :, :, r:] = from_hi
     return halo, int(from_lo is not None), int(from_hi is not None)
+
+
+class PendingHalo:
+    """halo_planes() whose exchange is in flight (halo_planes_start): has_lo /
+    has_hi are known at once; result() waits and returns halo_planes()'s tuple."""
+
+    def __init__(self, finish, has_lo, has_hi):
+        self._finish, self._res = finish, None
+        self.has_lo, self.has_hi = has_lo, has_hi
+
+    def result(self):
+        if self._res is None:
+            self._res = self._finish()
+            self._finish = None
+        return self._res
+
+
+def halo_planes_start(x, r=1):
+    """halo_planes() split around the transfer: posts the exchange and returns
+    a PendingHalo, so the caller can enqueue the work that does not read the
+    halo planes (the Winograd conv's weight transform and interior z tiles,
+    m3d_conv3d_fwd_wino_halo_phase) before waiting for it."""
+    sg = _ACTIVE
+    B, H, W, D, C = x.shape
+    if r > D:
+        raise ValueError(f"z-halo of {r} planes exceeds the slab")
+    fin = sg.exchange_start(x[:, :, :, :r] if sg.lo is not None else None,
+                            x[:, :, :, D - r:] if sg.hi is not None else None, (B, H, W, r, C))
+
+    def finish():
+        from_lo, from_hi = fin()
+        halo = torch.empty((B, H, W, 2 * r, C), device=x.device, dtype=x.dtype)
+        if from_lo is not None:
+            halo[:, :, :, :r] = from_lo
+        if from_hi is not None:
+            halo[:, :, :, r:] = from_hi
+        return halo, int(from_lo is not None), int(from_hi is not None)
+    return PendingHalo(finish, int(sg.lo is not None), int(sg.hi is not None))
 
 
 def return_halo_grads(dx, dhalo, r=1):

@@ -327,6 +327,16 @@ int m3d_conv3d_fwd_wino_halo(const float* x, const float* x_halo, int32_t has_lo
                              const float* bias, const float* bn_scale, const float* bn_shift,
                              const float* residual, int32_t relu, float* z_out, float* y, float* u_keep,
                              void* workspace, size_t ws_bytes, m3d_stream_t s);
+/* The same conv in two launches around the halo exchange (the caller posts the
+ * exchange, then): phase 1 -- weight transform and the interior z tiles, x_halo
+ * not read (may be NULL); phase 2 -- after the halo planes arrived: the first /
+ * last z tiles, the point GEMMs and the output transform.  Same arguments and
+ * workspace in both calls; bit-identical to m3d_conv3d_fwd_wino_halo. */
+int m3d_conv3d_fwd_wino_halo_phase(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi,
+                                   int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin, const float* w,
+                                   int64_t Cout, const float* bias, const float* bn_scale, const float* bn_shift,
+                                   const float* residual, int32_t relu, float* z_out, float* y, float* u_keep,
+                                   void* workspace, size_t ws_bytes, int32_t phase, m3d_stream_t s);
 int m3d_conv3d_bwd_data_wino_halo(const float* dz, const float* w, int32_t has_lo, int32_t has_hi, int64_t B,
                                   int64_t H, int64_t W, int64_t Dl, int64_t Cin, int64_t Cout, float* dx,
                                   float* dx_halo, int32_t accumulate, void* workspace, size_t ws_bytes,

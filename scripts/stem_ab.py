@@ -16,7 +16,7 @@ from m3d import _lib  # noqa: E402
 
 L = _lib.load()
 dev = torch.device("cuda:0")
-res = {"M3D_STEM_MFMA": os.environ.get("M3D_STEM_MFMA", "1")}
+res = {k: os.environ[k] for k in os.environ if k.startswith("M3D_STEM")}
 for S in (128, 256):
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.tanh(0.5 * torch.randn((1, S, S, S, 1), device=dev, generator=g))

@@ -144,3 +144,42 @@ def test_direct_wgrad_halo_equals_extended(cuda, has_lo, has_hi):
     ref = torch.nn.grad.conv3d_weight(xd, (C, C, 3, 3, 3), dzd)          # [Cout, Cin, kh, kw, kd]
     ref = ref.permute(2, 3, 4, 1, 0)
     assert float((dw.double().cpu() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("has_lo,has_hi,Dl", [(1, 1, 16), (0, 1, 8), (1, 0, 4), (1, 1, 12)])
+def test_wino_halo_phases_equal_one_launch(cuda, has_lo, has_hi, Dl):
+    """m3d_conv3d_fwd_wino_halo_phase 1 (weights + interior z tiles, before the
+    halo planes exist -- the buffer is filled only afterwards) then 2 (edge
+    tiles, GEMM, output) == the one-launch m3d_conv3d_fwd_wino_halo, bit for
+    bit; Dl = 4 has no interior tile."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator(device=cuda).manual_seed(11)
+    B, H, W, Cin, Cout = 1, 6, 10, 64, 128
+    x = torch.randn((B, H, W, Dl, Cin), device=cuda, generator=g)
+    halo_src = torch.randn((B, H, W, 2, Cin), device=cuda, generator=g)
+    w = torch.randn((3, 3, 3, Cin, Cout), device=cuda, generator=g) / (27 * Cin) ** 0.5
+    bias = torch.randn(Cout, device=cuda, generator=g) * 0.1
+    res = torch.randn((B, H, W, Dl, Cout), device=cuda, generator=g)
+    dext = Dl + has_lo + has_hi
+    nb = int(L.m3d_conv3d_wino_workspace_bytes(B, H, W, dext, Dl, Cin, Cout))
+    outs = []
+    for phased in (False, True):
+        ws = torch.full((nb // 4 + 1,), float("nan"), device=cuda)
+        y = torch.empty((B, H, W, Dl, Cout), device=cuda)
+        z = torch.empty_like(y)
+        args = (B, H, W, Dl, Cin, w.data_ptr(), Cout, bias.data_ptr(), None, None, res.data_ptr(), 1,
+                z.data_ptr(), y.data_ptr(), None, ws.data_ptr(), nb)
+        if phased:
+            halo = torch.full_like(halo_src, float("nan"))      # not yet arrived
+            _lib.check(L.m3d_conv3d_fwd_wino_halo_phase(x.data_ptr(), None, has_lo, has_hi, *args, 1,
+                                                        _lib.stream()))
+            halo.copy_(halo_src)
+            _lib.check(L.m3d_conv3d_fwd_wino_halo_phase(x.data_ptr(), halo.data_ptr(), has_lo, has_hi, *args, 2,
+                                                        _lib.stream()))
+        else:
+            _lib.check(L.m3d_conv3d_fwd_wino_halo(x.data_ptr(), halo_src.data_ptr(), has_lo, has_hi, *args,
+                                                  _lib.stream()))
+        outs.append((y, z))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.isfinite(outs[1][0]).all()
