@@ -3236,6 +3236,8 @@ constexpr int SX_SLD = 36;                       // epilogue staging row stride 
 __global__ __launch_bounds__(256, 1) void stem_fwd_x3_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
     __shared__ __attribute__((aligned(16))) char wsh[3 * SX_WPL];
     __shared__ __attribute__((aligned(16))) char win[4][3 * SX_PL];
+    __shared__ __attribute__((aligned(16))) float stg[4][32 * SX_SLD];   // epilogue staging (the window's
+                                                                        // pad cells must stay zero)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hc = blockIdx.x & 1;                                   // output channels hc*32 .. +31
     for (int i = tid; i < 32 * SX_K; i += 256) {
@@ -3347,7 +3349,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_x3_kernel(ConvP p, Epi e, int
         __builtin_amdgcn_wave_barrier();          // window reads done before the staging writes
         int b, oy, ox, tz;
         decode(tile, b, oy, ox, tz);
-        float* st = reinterpret_cast<float*>(ww);
+        float* st = stg[wave];
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * g) * SX_SLD + l32] = acc[r];
         __builtin_amdgcn_wave_barrier();
@@ -3371,6 +3373,209 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_x3_kernel(ConvP p, Epi e, int
             st4(e.y + m * 64 + n, v);
         }
         __builtin_amdgcn_wave_barrier();          // staging reads done before the next window
+    }
+}
+
+// ---- stem forward, bf16 split, weights in registers (M3D_STEM_X3=2) ---------
+// The 32x32 form above keeps 77 KB of weights in LDS, so one workgroup (one
+// wave per SIMD) fits a CU and every LDS latency is exposed.  Here each wave
+// owns 16 output channels (a quarter) and keeps its B operand -- the split
+// weights of those channels for all of K -- in registers (13 chunks of 32 k x
+// 3 planes x 4 VGPRs), loaded once; the four waves of a workgroup share one
+// window per tile (double-buffered, built by all 256 threads) and run
+// v_mfma_f32_16x16x32_bf16 on the tile's two 16-row halves.  K = kz * 56 + R
+// as above, padded to 416 (kz = 7 rows read with zero weights).  Outputs are
+// staged per workgroup as [32 z][64 ch] and leave as 256-B rows.
+constexpr int SY_KC = 13;                         // 32-k chunks (416 = 7.43 x 56)
+constexpr int SY_PER = (SX_PAIRS + 255) / 256;    // window pairs per thread (4)
+constexpr int SY_SLD = 68;                        // staging row stride (floats)
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256, 2) void stem_fwd_x3b_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char win[2][3 * SX_PL];
+    __shared__ __attribute__((aligned(16))) float stg[32 * SY_SLD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, l16 = lane & 15;
+    // B: this wave's 16 channels (n = 16 wave + l16), k = 32 c + 8 g + j
+    bf16x8 bw[SY_KC][3];
+#pragma unroll
+    for (int c = 0; c < SY_KC; ++c) {
+        const int k0 = 32 * c + 8 * g, kz = k0 / SX_R, R0 = k0 - kz * SX_R;
+        uint32_t hp[4] = {0, 0, 0, 0}, mp[4] = {0, 0, 0, 0}, lp[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int R = R0 + j;
+            const float v = (kz < 7 && R < 49) ? p.w[(R * 7 + kz) * 64 + 16 * wave + l16] : 0.0f;
+            uint32_t h, m, l;
+            split3(v, h, m, l);
+            hp[j >> 1] |= h << (16 * (j & 1));
+            mp[j >> 1] |= m << (16 * (j & 1));
+            lp[j >> 1] |= l << (16 * (j & 1));
+        }
+        bw[c][0] = __builtin_bit_cast(bf16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
+        bw[c][1] = __builtin_bit_cast(bf16x8, make_uint4(mp[0], mp[1], mp[2], mp[3]));
+        bw[c][2] = __builtin_bit_cast(bf16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
+    }
+    for (int i = tid; i < 2 * SX_ZR * SX_R; i += 256) {          // pad cells stay zero
+        const int bf = i / (SX_ZR * SX_R), c = i - bf * SX_ZR * SX_R;
+        const int zz = c / SX_R, R = c - zz * SX_R;
+        if (R >= 49 || zz >= 38)
+            for (int pl = 0; pl < 3; ++pl) reinterpret_cast<unsigned short*>(win[bf] + pl * SX_PL)[c] = 0;
+    }
+    // A offset of this lane in chunk c: row l16 (+16 for the second half), k0 = 32 c + 8 g;
+    // computed in the loop from compile-time constants (no per-chunk registers)
+    const int arow = l16 * (SX_R * 2);
+    auto aoff = [&](int c) -> int {
+        auto o = [](int k0) { return (k0 / SX_R) * (SX_R * 2) + (k0 % SX_R) * 2; };
+        const int o0 = o(32 * c), o1 = o(32 * c + 8), o2 = o(32 * c + 16), o3 = o(32 * c + 24);
+        return arow + (g == 0 ? o0 : g == 1 ? o1 : g == 2 ? o2 : o3);
+    };
+    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
+    auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
+        tz = (int)(t % tz_n); t /= tz_n;
+        ox = (int)(t % p.OW); t /= p.OW;
+        oy = (int)(t % p.OH);
+        b = (int)(t / p.OH);
+    };
+    auto xval = [&](const float* xb, int b, int gy, int gx, int gz) -> float {
+        if (gy < 0 || gy >= p.H || gx < 0 || gx >= p.W || gz < 0 || gz >= p.D) return 0.0f;
+        if (p.halo) {
+            const int zl = gz - p.hnlo;
+            if ((unsigned)zl < (unsigned)p.hdl) return xb[gy * row + gx * plane + zl];
+            return p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
+                          (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
+        }
+        return xb[gy * row + gx * plane + gz];
+    };
+    // fast path of tiles whose window lies inside the slab: offsets from the
+    // window origin, no per-value bounds / halo checks
+    auto fetch = [&](int64_t tile, float (&v)[SY_PER][2]) {
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
+        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
+        const float* xb = p.a + b * img;
+        const int zl0 = p.halo ? gz0 - p.hnlo : gz0, zlim = p.halo ? p.hdl : p.D;
+        if (gy0 >= 0 && gy0 + 6 < p.H && gx0 >= 0 && gx0 + 6 < p.W && zl0 >= 0 && zl0 + 37 < zlim) {
+            const float* base = xb + gy0 * row + gx0 * plane + zl0;
+#pragma unroll
+            for (int q = 0; q < SY_PER; ++q) {
+                const int j = tid + 256 * q;
+                const int zz = j / 25, rp = j - zz * 25, R0 = 2 * rp, dy = R0 / 7, dx = R0 - 7 * dy;
+                const float* a0 = base + (dy * (int)row + dx * (int)plane + zz);
+                // R0 + 1: the next kx, or the next ky row when dx == 6 (R 49 is padding)
+                const float* a1 = dx < 6 ? a0 + plane : a0 + (row - 6 * plane);
+                v[q][0] = j < SX_PAIRS ? a0[0] : 0.0f;
+                v[q][1] = (j < SX_PAIRS && R0 + 1 < 49) ? a1[0] : 0.0f;
+            }
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < SY_PER; ++q) {
+            const int j = tid + 256 * q;
+            v[q][0] = v[q][1] = 0.0f;
+            if (j < SX_PAIRS) {
+                const int zz = j / 25, rp = j - zz * 25;
+                const int R0 = 2 * rp, R1 = R0 + 1;
+                v[q][0] = xval(xb, b, gy0 + R0 / 7, gx0 + R0 % 7, gz0 + zz);
+                if (R1 < 49) v[q][1] = xval(xb, b, gy0 + R1 / 7, gx0 + R1 % 7, gz0 + zz);
+            }
+        }
+    };
+    auto stage = [&](char* ww, const float (&v)[SY_PER][2]) {
+#pragma unroll
+        for (int q = 0; q < SY_PER; ++q) {
+            const int j = tid + 256 * q;
+            if (j < SX_PAIRS) {
+                const int zz = j / 25, rp = j - zz * 25;
+                uint32_t h0, m0, l0, h1, m1, l1;
+                split3(v[q][0], h0, m0, l0);
+                split3(v[q][1], h1, m1, l1);
+                const int off = (zz * SX_R + 2 * rp) * 2;
+                *reinterpret_cast<uint32_t*>(ww + off) = h0 | (h1 << 16);
+                *reinterpret_cast<uint32_t*>(ww + SX_PL + off) = m0 | (m1 << 16);
+                *reinterpret_cast<uint32_t*>(ww + 2 * SX_PL + off) = l0 | (l1 << 16);
+            }
+        }
+    };
+    const int n4 = 4 * (tid & 15);                                   // epilogue: 16 float4 per row
+    float pre[SY_PER][2];
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) fetch(tile, pre);
+    int buf = 0;
+    if (tile < ntiles) stage(win[0], pre);
+    __syncthreads();
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t next = tile + gridDim.x;
+#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 3
+        (void)next;                                                  // timing probe: no window fetch
+#else
+        if (next < ntiles) fetch(next, pre);                         // next window in flight
+#endif
+        const char* W = win[buf];
+        floatx4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 1
+        acc0[0] = (float)W[aoff(0)];                                 // timing probe: no MFMA
+#else
+#pragma unroll
+        for (int c = 0; c < SY_KC; ++c) {
+            bf16x8 a0[3], a1[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                a0[pl] = *reinterpret_cast<const bf16x8*>(W + pl * SX_PL + aoff(c));
+                a1[pl] = *reinterpret_cast<const bf16x8*>(W + pl * SX_PL + aoff(c) + 16 * SX_R * 2);
+            }
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[2], bw[c][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[2], bw[c][0], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[1], bw[c][1], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[1], bw[c][1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][2], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[1], bw[c][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[1], bw[c][0], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][1], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][0], acc1, 0, 0, 0);
+        }
+#endif
+        // D of 16x16x32: row 4 g + r, column l16
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            stg[(4 * g + r) * SY_SLD + 16 * wave + l16] = acc0[r];
+            stg[(16 + 4 * g + r) * SY_SLD + 16 * wave + l16] = acc1[r];
+        }
+        if (next < ntiles) stage(win[buf ^ 1], pre);
+        __syncthreads();                                             // staging + next window written
+        int b, oy, ox, tz;
+        decode(tile, b, oy, ox, tz);
+        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
+        const int oz0 = tz * STEM_TZ;
+        const float4 bb = e.bias ? ld4(e.bias + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 sc = e.scale ? ld4(e.scale + n4) : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 sh = e.scale ? ld4(e.shift + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {                                // 32 rows x 16 float4
+            const int rr = (tid >> 4) + 16 * q;
+            float4 v = *reinterpret_cast<const float4*>(stg + rr * SY_SLD + n4);
+            if (oz0 + rr >= p.OD) continue;
+            const int64_t m = mbase + oz0 + rr;
+            if (e.bias) { v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w; }
+#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 2
+            if (v.x == 1.2345f) st4(e.y + m * 64 + n4, v);           // timing probe: no stores
+            continue;
+#endif
+            if (e.z) st4(e.z + m * 64 + n4, v);
+            if (e.scale) {
+                v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
+                v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
+            }
+            if (e.relu) {
+                v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
+            }
+            st4(e.y + m * 64 + n4, v);
+        }
+        __syncthreads();                                             // staging read before the next tile's writes
+        buf ^= 1;
     }
 }
 
@@ -3535,7 +3740,14 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     // one-CU NMS reduce) may still hold a CU, and a persistent block waiting
     // for that CU would stall the whole launch (measured 1.5 ms in the step
     // vs 0.28 ms alone at 128^3); with 4 per CU the others absorb its share
-    static const int x3 = [] { const char* v = getenv("M3D_STEM_X3"); return v ? atoi(v) : 1; }();
+    // M3D_STEM_X3=1 / 2: the bf16-split forms (measured slower than the f32 kernel: 2.65 / 2.24-2.5 vs
+    // 2.2 ms at 256^3, DESIGN.md round-3 list); default the f32 MFMA kernel
+    static const int x3 = [] { const char* v = getenv("M3D_STEM_X3"); return v ? atoi(v) : 0; }();
+    if (x3 == 2) {
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, 2 * (int64_t)ncu));
+        hipLaunchKernelGGL(stem_fwd_x3b_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
+        return check_launch("stem_fwd_x3b_kernel");
+    }
     if (x3) {
         // one workgroup per CU (131 KB of LDS): pairs of workgroups take the two
         // 32-channel halves of the same tiles, each wave its own tiles

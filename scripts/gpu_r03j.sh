@@ -1,5 +1,5 @@
 #!/bin/bash
-# bf16-split stem forward: conv / slab-halo / model tests, then the stem A/B
+# bf16-split stem forward + phased slab Winograd: conv / slab-halo / model / slab tests, then the stem A/B
 set -o pipefail
 OUT=gpurun_out/r03j
 mkdir -p $OUT
@@ -10,3 +10,5 @@ for e in "M3D_STEM_X3=1" "M3D_STEM_X3=0" "M3D_STEM_X3=1"; do
   env $e timeout -k 10 200 python -u scripts/stem_ab.py > $OUT/stem.json 2> $OUT/stem.err || { tail -20 $OUT/stem.err; exit 1; }
   echo "$e $(tail -n 1 $OUT/stem.json)"
 done
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 800 --timeout-method thread tests/test_gpu_slab.py -m gpu > $OUT/slab.log 2>&1 || { tail -40 $OUT/slab.log; exit 1; }
+grep -E "passed|failed" $OUT/slab.log | tail -3

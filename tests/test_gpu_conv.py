@@ -68,6 +68,8 @@ CASES = [
     ((6, 6, 4), 64, 256, (1, 1, 1), (1, 1, 1), "valid", True, True, True),
     ((16, 16, 6), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),
     ((14, 12, 40), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),   # stem: two z tiles, a partial one
+    ((64, 60, 8), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),    # stem: several tiles per wave
+    ((20, 18, 80), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),   # stem: windows inside the volume
     ((3, 5, 9), 32, 160, (3, 3, 3), (1, 1, 1), "same", True, False, True),
 ]
 
