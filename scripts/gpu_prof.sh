@@ -14,7 +14,7 @@ timeout -k 10 400 $P --kernel-trace --stats -d $OUT/prof -o run -- python3 bench
 python3 scripts/prof_summary.py $OUT/prof/run_kernel_stats.csv $((STEPS + WARM)) 40 > $OUT/bench_kernels.txt
 rm -f $OUT/prof/run_kernel_trace.csv
 NR=$([ "$S" = 128 ] && echo 128 || echo 512)
-LEGS=${LEGS:-"gemm:x3_gemm256_af_kernel:wino_gemm_x3af_rpn_shared1_S$S wgrad:x3_wgrad:wino_wgrad_gemm_rpn_shared1_S$S direct:conv_gemm_kernel:direct_conv_rpn_shared1_S$S roi7:line_fwd_kernel:pyramid_fwd_pool7_S${S}_N$NR roi14:line_fwd_kernel:pyramid_fwd_pool14_S${S}_N$NR"}
+LEGS=${LEGS:-"gemm:x3_gemm256_af_kernel:wino_gemm_x3af_rpn_shared1_S$S wgrad:x3_wgrad:wino_wgrad_gemm_rpn_shared1_S$S direct:conv_gemm_kernel:direct_conv_rpn_shared1_S$S roi7:line_fwd_sl_kernel:pyramid_fwd_pool7_S${S}_N$NR roi14:line_fwd_sl_kernel:pyramid_fwd_pool14_S${S}_N$NR"}
 for spec in $LEGS; do
   IFS=: read leg kern key <<< "$spec"
   timeout -k 10 300 $P --kernel-trace --stats -d $OUT/k_$leg -o run -- python3 scripts/kernels_for_pmc.py $leg $S > $OUT/k_$leg.log 2>&1 || { echo "rocprof $leg failed"; tail -30 $OUT/k_$leg.log; exit 1; }
