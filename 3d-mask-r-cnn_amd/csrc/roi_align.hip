@@ -1551,6 +1551,58 @@ extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* b
     return check_launch("pyramid_bwd_kernel");
 }
 
+// Deterministic PyramidROIAlign backward (the gradient of core/models.py:597-687
+// through custom_op.py:28-65): per level, CropAndResize3DGradImage over that
+// level's ROIs in ascending order -- the reference's tf.where gather order --
+// as crop_bwd_det_kernel (destination-owned sums in the sequential replay
+// order, bit-identical to it; every voxel written, no zero fill).  box_ind_ws:
+// [4][B*N] int32 device scratch; ROIs of other levels get -1 (never match).
+__global__ void pyr_level_bi_kernel(const int32_t* __restrict__ levels, int64_t BN, int64_t N,
+                                    int32_t* __restrict__ bi) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= BN) return;
+    const int l = levels[i] - 2;
+    for (int k = 0; k < 4; ++k) bi[k * BN + i] = l == k ? (int32_t)(i / N) : -1;
+}
+
+extern "C" int m3d_pyramid_roi_align3d_bwd_det(const float* grad_out, const float* boxes_adj,
+                                               const int32_t* levels, int64_t B, int64_t N,
+                                               int32_t ph, int32_t pw, int32_t pd,
+                                               float* const gmaps[4], const int64_t fshape[4][3],
+                                               int64_t C, int32_t* box_ind_ws, m3d_stream_t s) {
+    Pyr P;
+    int rc = make_pyr(P, nullptr, gmaps, fshape);
+    if (rc) return rc;
+    if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
+    if (ph > 64 || pw > 64 || pd > 64) return einval("pyramid_roi_align3d_bwd_det: crop sizes up to 64");
+    if (B < 0 || N < 0 || C <= 0) return einval("pyramid_roi_align3d_bwd: invalid B, N or C");
+    if (B * N > 0 && !box_ind_ws) return einval("pyramid_roi_align3d_bwd_det: box_ind workspace missing");
+    const int64_t BN = B * N;
+    if (BN > 0) hipLaunchKernelGGL(pyr_level_bi_kernel, dim3(grid_for(BN, 256)), dim3(256), 0, st(s), levels, BN,
+                                   N, box_ind_ws);
+    for (int l = 0; l < 4; ++l) {
+        const int64_t H = P.H[l], W = P.W[l], D = P.D[l];
+        if (BN == 0) {
+            if (hipMemsetAsync(gmaps[l], 0, sizeof(float) * (size_t)(B * H * W * D * C), st(s)) != hipSuccess)
+                return check_launch("memset gmaps");
+            continue;
+        }
+        const bool v4 = (C & 3) == 0;
+        const int64_t cvn = v4 ? C / 4 : C;
+        const int64_t bpc = (D * cvn + 255) / 256;
+        const unsigned grid = (unsigned)std::min<int64_t>(B * H * W * bpc, 1 << 20);
+        if (v4)
+            hipLaunchKernelGGL(crop_bwd_det_kernel<4>, dim3(grid), dim3(256), 0, st(s), grad_out, boxes_adj,
+                               box_ind_ws + l * BN, BN, ph, pw, pd, (int)B, (int)H, (int)W, (int)D, (int)C, 0, bpc,
+                               gmaps[l]);
+        else
+            hipLaunchKernelGGL(crop_bwd_det_kernel<1>, dim3(grid), dim3(256), 0, st(s), grad_out, boxes_adj,
+                               box_ind_ws + l * BN, BN, ph, pw, pd, (int)B, (int)H, (int)W, (int)D, (int)C, 0, bpc,
+                               gmaps[l]);
+    }
+    return check_launch("crop_bwd_det_kernel<pyr>");
+}
+
 extern "C" int m3d_mask_targets3d(const uint8_t* gt_masks, int64_t H, int64_t W, int64_t D,
                                   int64_t G, const float* rois, const int32_t* assign, int64_t P,
                                   int32_t mh, int32_t mw, int32_t md, float* out, m3d_stream_t s) {

@@ -41,6 +41,8 @@ _SIGS = {
     "m3d_pyramid_roi_align3d_fwd_workspace_bytes": [c_p, c_i64, c_i64, c_i32, c_i32],
     "m3d_pyramid_roi_align3d_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p,
                                     c_i64, c_p],
+    "m3d_pyramid_roi_align3d_bwd_det": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p,
+                                        c_i64, c_p, c_p],
     "m3d_mask_targets3d": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_i32,
                            c_p, c_p],
     "m3d_nms3d_workspace_bytes": [c_i64],

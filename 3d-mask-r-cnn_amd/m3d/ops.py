@@ -242,9 +242,16 @@ class _PyramidROIAlign(torch.autograd.Function):
         ph, pw, pd = ctx.pool
         gptrs = (_lib.c_p * 4)(*[g.data_ptr() for g in gmaps])
         fshape = ((_lib.c_i64 * 3) * 4)(*[(_lib.c_i64 * 3)(*s[1:4]) for s in ctx.shapes])
-        check(_L().m3d_pyramid_roi_align3d_bwd(ptr(grad), ptr(boxes_adj), ptr(levels), B, N, ph, pw,
-                                               pd, gptrs, fshape, ctx.shapes[0][-1], stream()),
-              "pyramid_roi_align bwd")
+        if _L().m3d_get_deterministic() and max(ph, pw, pd) <= 64:
+            # bitwise reproducible: per level, the destination-owned sums in the reference's order
+            bi = torch.empty(4 * B * N, device=grad.device, dtype=torch.int32)
+            check(_L().m3d_pyramid_roi_align3d_bwd_det(ptr(grad), ptr(boxes_adj), ptr(levels), B, N, ph, pw,
+                                                       pd, gptrs, fshape, ctx.shapes[0][-1], ptr(bi), stream()),
+                  "pyramid_roi_align bwd (deterministic)")
+        else:
+            check(_L().m3d_pyramid_roi_align3d_bwd(ptr(grad), ptr(boxes_adj), ptr(levels), B, N, ph, pw,
+                                                   pd, gptrs, fshape, ctx.shapes[0][-1], stream()),
+                  "pyramid_roi_align bwd")
         return (None, None, None) + tuple(gmaps)
 
 

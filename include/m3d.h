@@ -119,6 +119,18 @@ int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* boxes_adj,
                                 int32_t pw, int32_t pd, float* const gmaps[4],
                                 const int64_t fshape[4][3], int64_t C, m3d_stream_t s);
 
+/* The same backward, bitwise reproducible: per level, CropAndResize3DGradImage
+ * over that level's ROIs in ascending order (the reference's tf.where gather
+ * order) with destination-owned sums in its sequential replay order (the
+ * deterministic mode 1 kernel of m3d_crop_and_resize3d_bwd_image; crop sizes
+ * up to 64; every voxel written).  box_ind_ws: [4][B*N] int32 device scratch.
+ * Used when m3d_set_deterministic is on. */
+int m3d_pyramid_roi_align3d_bwd_det(const float* grad_out, const float* boxes_adj,
+                                    const int32_t* levels, int64_t B, int64_t N, int32_t ph,
+                                    int32_t pw, int32_t pd, float* const gmaps[4],
+                                    const int64_t fshape[4][3], int64_t C, int32_t* box_ind_ws,
+                                    m3d_stream_t s);
+
 /* DetectionTargetLayer mask targets (core/models.py:972-996): out[p] =
  * round_half_even(CropAndResize3D(float(gt_masks[..., assign[p]]), rois[p],
  * (mh,mw,md), trilinear, extrapolation 0)), reading the boolean masks

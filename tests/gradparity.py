@@ -2,6 +2,7 @@
 test_gpu_config0.py): the GPU step's weight gradients against the float64
 CPU restatement (oracle/model_ref.py) taking the GPU forward's ReLU branches,
 with the CPU fp32 restatement on the same branches as the yardstick."""
+import contextlib
 import numpy as np
 import torch
 
@@ -46,3 +47,19 @@ def grad_parity(model, g64, g32, label):
     assert med < 1e-5, med
     bad = [r for r in rows if r[0] > max(1e-4, 2.0 * r[1])]
     assert not bad, bad[:5]
+
+
+@contextlib.contextmanager
+def deterministic():
+    """Run the enclosed GPU step in m3d's deterministic mode (weight-gradient
+    splits summed in a fixed order, fixed-tree clip norms, the PyramidROIAlign
+    backward in the reference's scatter order), so a parity failure replays
+    bit for bit."""
+    import torch
+    from m3d import _lib
+    _lib.set_deterministic(True)
+    try:
+        yield
+    finally:
+        torch.cuda.synchronize()
+        _lib.set_deterministic(False)

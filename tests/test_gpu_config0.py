@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from gradparity import grad_parity, ref_grads
+from gradparity import deterministic, grad_parity, ref_grads
 from oracle import heads_ref as HR
 
 pytestmark = pytest.mark.gpu
@@ -73,14 +73,15 @@ def test_config0_step_losses_and_gradients(toy, cuda):
     cfg, model, image, gt, builder, t, rm, rb = toy
     model.store.zero_grad()
     mnn.RELU_CAPTURE = {}
-    try:
-        out = model.forward(image.to(cuda), proposals=False)
-        masks = mnn.RELU_CAPTURE
-    finally:
-        mnn.RELU_CAPTURE = None
-    lc, lb = model.losses(out, t)                      # device-resident targets, mask form
-    (lc * 1.0 + lb * 1.5).backward()
-    model.rpn.finish_backward()
+    with deterministic():                              # the GPU step replays bit for bit
+        try:
+            out = model.forward(image.to(cuda), proposals=False)
+            masks = mnn.RELU_CAPTURE
+        finally:
+            mnn.RELU_CAPTURE = None
+        lc, lb = model.losses(out, t)                  # device-resident targets, mask form
+        (lc * 1.0 + lb * 1.5).backward()
+        model.rpn.finish_backward()
     torch.cuda.synchronize()
     match, bbox = rm.reshape(1, -1, 1), rb[None]
     rlc, rlb, g64 = ref_grads(model, image, match, bbox, torch.float64, masks)

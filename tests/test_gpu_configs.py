@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from gradparity import grad_parity, ref_grads
+from gradparity import deterministic, grad_parity, ref_grads
 from oracle import heads_ref as HR
 from oracle import model_ref as MR
 from oracle import ops_ref as R
@@ -201,6 +201,21 @@ def test_config2_pyramid_roi_align_and_grad_image(e2e128, cuda, pool):
                                                     torch.zeros(sel.size, dtype=torch.int32, device=cuda),
                                                     maps_np[li].shape, deterministic=True)
             np.testing.assert_array_equal(det.cpu().numpy(), want_g)
+    # the whole PyramidROIAlign backward in deterministic mode (m3d_set_deterministic):
+    # every level's gradient bit-exact vs the oracle's sequential scatter
+    from m3d import _lib
+    maps2 = [m.detach().clone().requires_grad_(True) for m in maps]
+    _lib.set_deterministic(True)
+    try:
+        layer([rois_t, meta_t] + maps2).backward(g)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_deterministic(False)
+    for li, level in enumerate(range(2, 6)):
+        sel = np.nonzero(lvl == level)[0]
+        want_g = R.crop_and_resize_3d_grad_image(gn[sel], bx[sel], np.zeros(sel.size, np.int32),
+                                                 maps_np[li].shape) if sel.size else np.zeros_like(maps_np[li])
+        np.testing.assert_array_equal(maps2[li].grad.cpu().numpy(), want_g)
     print(f"configs[2] pool {pool}: levels {np.bincount(lvl, minlength=6)[2:].tolist()}")
 
 
@@ -221,14 +236,15 @@ def test_config1_gradients_full_size(fwd128, cuda):
     match, bbox = synthetic_rpn_targets(model.anchors.shape[1], cfg.RPN_TRAIN_ANCHORS_PER_IMAGE, seed=2)
     model.store.zero_grad()
     mnn.RELU_CAPTURE = {}
-    try:
-        out = model.forward(image.to(cuda), proposals=False)
-        masks = mnn.RELU_CAPTURE
-    finally:
-        mnn.RELU_CAPTURE = None
-    lc, lb = model.losses(out, RPNTargets(match, bbox, cuda))
-    (lc * 1.0 + lb * 1.5).backward()
-    model.rpn.finish_backward()
+    with deterministic():                      # the GPU step replays bit for bit
+        try:
+            out = model.forward(image.to(cuda), proposals=False)
+            masks = mnn.RELU_CAPTURE
+        finally:
+            mnn.RELU_CAPTURE = None
+        lc, lb = model.losses(out, RPNTargets(match, bbox, cuda))
+        (lc * 1.0 + lb * 1.5).backward()
+        model.rpn.finish_backward()
     torch.cuda.synchronize()
     del out
     torch.set_num_threads(min(16, torch.get_num_threads()))
