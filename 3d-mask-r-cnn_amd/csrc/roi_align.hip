@@ -351,10 +351,16 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     int pk = -1;
     float4 kv[4];
     // (no lambda around the body: capturing col / kv by reference put them in scratch)
+    // PD > 0: this wave's z part (at most PD samples, zs = ceil(cd / PD) parts per
+    // line) with its outputs held in registers and stored after the loop, so no
+    // corner load waits behind an output store: loads and stores share vmcnt, and
+    // with both kinds in flight the compiler can only wait with vmcnt(0)
     float4 res[PD > 0 ? PD : 1];
-    const int z0_ = PD > 0 ? 0 : zb, z1_ = PD > 0 ? PD : ze;
+    const int n_it = PD > 0 ? PD : ze - zb;
 #pragma unroll
-    for (int z = z0_; z < z1_; ++z) {
+    for (int zz = 0; zz < n_it; ++zz) {
+        const int z = zb + zz;
+        if (PD > 0 && z >= ze) break;
         const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
         float4 r;
         if (in_z < 0 || in_z > (float)(D - 1)) {
@@ -363,6 +369,15 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
             const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
             const float zl = in_z - (float)fz;
             float4 fv[4];
+#if defined(M3D_ROI_DBG) && M3D_ROI_DBG == 2
+            // timing probe: no corner loads (values from the coordinates)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fv[q] = make_float4(in_z, yl, xl, (float)(fz + q));
+            if (kz != fz) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) kv[q] = make_float4(yl, in_z, (float)(kz + q), xl);
+            } else {
+#else
             if (fz == pk) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) fv[q] = kv[q];
@@ -374,6 +389,7 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
 #pragma unroll
                 for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
             } else {
+#endif
 #pragma unroll
                 for (int q = 0; q < 4; ++q) kv[q] = fv[q];
             }
@@ -381,12 +397,17 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
             r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
             r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
         }
-        if constexpr (PD > 0) res[z] = r;
+#if defined(M3D_ROI_DBG) && M3D_ROI_DBG == 1
+        if (r.x == 1.2345f) st_nt(o + (int64_t)z * C4 + c, r);          // timing probe: no stores
+        continue;
+#endif
+        if constexpr (PD > 0) res[zz] = r;
         else st_nt(o + (int64_t)z * C4 + c, r);
     }
     if constexpr (PD > 0) {
 #pragma unroll
-        for (int z = 0; z < PD; ++z) st_nt(o + (int64_t)z * C4 + c, res[z]);
+        for (int zz = 0; zz < PD; ++zz)
+            if (zb + zz < ze) st_nt(o + (int64_t)(zb + zz) * C4 + c, res[zz]);
     }
 }
 
@@ -1416,7 +1437,11 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for the 7^3 pool
             // (its lines are short and the sort does not pay); M3D_ROI_SORT overrides
             static const int sort_env0 = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : -1; }();
-            const int sort_env = sort_env0 >= 0 ? sort_env0 : (pd >= 14 ? 3 : 0);
+            // register-staged z parts (M3D_ROI_STAGE = PD, 0: off): zs = ceil(pd / PD) parts per line
+            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 0; }();
+            const int spd = (stage_env == 4 || stage_env == 7 || stage_env == 14) && sl == 8 ? stage_env : 0;
+            int sort_env = sort_env0 >= 0 ? sort_env0 : (pd >= 14 ? 3 : 0);
+            if (sort_env == 3 && spd && spd < pd) sort_env = 0;   // the wave order sorts whole lines
             if (sort_env == 2 && workspace && ws_bytes >= need && nl < INT32_MAX && B * N <= nb) {
                 // ROI order: keys [B*N] (uint64, 8-B aligned at the start), inv [B*N], perm [lines]
                 uint64_t* rkeys = (uint64_t*)workspace;
@@ -1469,15 +1494,14 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 perm = pm;
             }
             static const int zs_env = [] { const char* e = getenv("M3D_ROI_ZSPLIT"); return e ? atoi(e) : 1; }();
-            const int zs = wperm ? 1 : std::max(1, std::min(zs_env, (int)pd));
+            const int zs = spd ? (int)((pd + spd - 1) / spd)
+                               : (wperm ? 1 : std::max(1, std::min(zs_env, (int)pd)));
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
-            // register-staged outputs (M3D_ROI_STAGE=1): 138 VGPRs halve the occupancy,
-            // 14^3 at 256^3 0.87 -> 1.11 ms; off
-            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 0; }();
-            if (sl == 8 && zs == 1 && stage_env && (pd == 7 || pd == 14)) {
-                if (pd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-                else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            if (spd) {
+                if (spd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+                else if (spd == 7) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+                else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 return check_launch("line_fwd_sl_kernel<staged>");
             }
             if (sl == 2) hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
