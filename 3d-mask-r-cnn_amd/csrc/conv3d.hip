@@ -2838,12 +2838,17 @@ static int wino_nz() {
     static int v = [] { const char* e = getenv("M3D_WINO_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
     return v;
 }
-// The weight gradient keeps F(2x2x2) (M3D_WINO_WGRAD_NZ=4 for A/B): its
-// tile-summed Winograd-domain products go through G^T, whose F(4,3) rows
-// (4, 8/3, ...) amplify the fp32 summation error over the tiles ~10x -- the
-// forward / data-gradient F(2x2x4) stays at the direct conv's error level.
+// The weight gradient runs on the forward's F(2x2x4) tiles (round 3; was
+// F(2x2x2)): the forward keeps its fp32 transformed input U and the weight
+// gradient reads it (no second input transform), with 96 instead of 64 point
+// GEMMs over half the tiles -- 25 % fewer MFMA FLOPs.  Its tile-summed products
+// pass through G^T, whose F(4,3) rows amplify the fp32 summation error:
+// measured 3.3e-6 / 2.8e-6 vs F(2x2x2)'s 1.0e-6 / 1.2e-6 of the gradient's
+// scale (128 -> 128 / 256 -> 512 convs, test_wino_weight_gradient_accuracy),
+// whole-step gradients at 128^3 median 1.2e-6 vs float64; step 30.9 -> 29.7 ms.
+// M3D_WINO_WGRAD_NZ=2 restores F(2x2x2).
 static int wino_wgrad_nz() {
-    static int v = [] { const char* e = getenv("M3D_WINO_WGRAD_NZ"); return e && atoi(e) == 4 ? 4 : 2; }();
+    static int v = [] { const char* e = getenv("M3D_WINO_WGRAD_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
     return v;
 }
 // M3D_WINO_DGRAD_NZ overrides the data-gradient tile (default: the forward's)
@@ -4151,6 +4156,7 @@ static bool wino_per_item(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD
 #define WINO_LAUNCH(kern, ...) WINO_LAUNCH_NZ(wino_nz(), kern, __VA_ARGS__)
 
 extern "C" int32_t m3d_conv3d_wino_tile_z(void) { return wino_nz(); }
+extern "C" int32_t m3d_conv3d_wino_wgrad_tile_z(void) { return wino_wgrad_nz(); }
 
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {
@@ -4420,7 +4426,7 @@ extern "C" int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, i
 
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {
     if (wino_nz() != wino_wgrad_nz()) return 0;       // forward tiles differ from the wgrad's: nothing to keep
-    if (gemm_x3_env()) return 0;                        // the forward's U is in bf16 planes
+    if (gemm_x3_env() && !x3_af32_env()) return 0;     // the forward's U is in bf16 planes
     return sizeof(float) * wino_points() * (size_t)wino_geom(B, H, W, OD, OD, 1).T * (size_t)Cin;
 }
 
@@ -4459,7 +4465,9 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
         gi.tz_mode = 1; gi.halo = nullptr; gi.hlo = gi.hhi = 0;
         ge.tz_mode = 2;
     }
-    if (gemm_x3_env() && !u_keep) {
+    if (gemm_x3_env() && (!u_keep || x3_af32_env())) {
+        // (the fp32-A GEMM reads U in fp32: a kept U is written in place for the weight gradient)
+        if (u_keep) ws.U = u_keep;
         float* wt = ws.WT;
         if (!v_ready && phase != 2) {     // v_ready: V already holds this w's transform (an earlier call, same workspace)
             hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),

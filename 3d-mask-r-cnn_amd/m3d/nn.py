@@ -537,7 +537,7 @@ class _ConvBNAct(torch.autograd.Function):
                                   "conv3d_bwd_weight_wino")
                     if logging:
                         exe = direct if min(Cin, Cout) < WINO_WGRAD_MIN_C else \
-                            _wino_exec(B, OH, OW, OD, Cin, Cout, 2)
+                            _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_wgrad_tile_z()))
                         _log("wino_wgrad", direct, exe, 4.0 * (x.numel() + dz.numel() + w.numel()),
                              "bwd_weight", ctx.name, tw)
                 ctx.u = None

@@ -98,12 +98,13 @@ def _pmc_traffic(kernel_key):
 
 
 def wgrad_gemm_shape(S):
-    """The largest launch of the step's second kernel, x3_wgrad_tr_kernel (15.7 %
-    of the step's kernel time, profiles/r02i_bench_kernels_128.txt): the 64
-    batched Winograd weight-gradient GEMMs of rpn_conv_shared1 (3x3x3, 256->512)
-    on P2 [S/4, S/4, S] -- F(2x2x2) tiles (the weight gradient keeps NZ = 2,
-    conv3d.hip wino_wgrad_nz), reduction over M = T tiles, K = 256, N = 512."""
-    nz = 4 if os.environ.get("M3D_WINO_WGRAD_NZ") == "4" else 2
+    """The largest launch of the step's second kernel, x3_wgrad_tr_kernel: the
+    16*(NZ+2) batched Winograd weight-gradient GEMMs of rpn_conv_shared1
+    (3x3x3, 256->512) on P2 [S/4, S/4, S] -- F(2x2x4) tiles by default (96
+    GEMMs on the forward's kept U; M3D_WINO_WGRAD_NZ=2: F(2x2x2), 64 GEMMs),
+    reduction over M = T tiles, K = 256, N = 512."""
+    from m3d import _lib
+    nz = int(_lib.load().m3d_conv3d_wino_wgrad_tile_z())
     q = S // 4
     T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
     return 16 * (nz + 2), T, 256, 512

@@ -541,3 +541,29 @@ def test_wino_shared_weight_transform_bit_identical(cuda):
                                                     _lib.stream()), "bwd_v")
             outs.append(dx)
         assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout", [(128, 128), (256, 512)])
+def test_wino_weight_gradient_accuracy(cuda, cin, cout):
+    """The Winograd weight gradient (the step's 3^3 convs with >= 128 channels,
+    F(2x2x4) tiles by default, M3D_WINO_WGRAD_NZ=2 for F(2x2x2)) against
+    float64: the fp32 summation over the tiles passes through G^T, whose F(4,3)
+    rows amplify it -- held to 2e-5 of the gradient's scale (the direct fp32
+    weight gradient's own error is ~1e-6 here), with the measured value printed."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator(device=cuda).manual_seed(cin + cout)
+    B, H, W, D = 1, 16, 16, 32
+    x = torch.randn((B, H, W, D, cin), device=cuda, generator=g)
+    dz = torch.randn((B, H, W, D, cout), device=cuda, generator=g)
+    dw = torch.zeros((3, 3, 3, cin, cout), device=cuda)
+    nb = int(L.m3d_conv3d_wino_workspace_bytes(B, H, W, D, D, cin, cout))
+    ws = torch.empty(nb // 4 + 1, device=cuda)
+    _lib.check(L.m3d_conv3d_bwd_weight_wino(x.data_ptr(), dz.data_ptr(), B, H, W, D, cin, cout, D, 1,
+                                            dw.data_ptr(), ws.data_ptr(), nb, _lib.stream()))
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv3d_weight(x.double().cpu().permute(0, 4, 1, 2, 3), (cout, cin, 3, 3, 3),
+                                      dz.double().cpu().permute(0, 4, 1, 2, 3), padding=1).permute(2, 3, 4, 1, 0)
+    err = float((dw.double().cpu() - ref).abs().max() / ref.abs().max())
+    print(f"winograd weight gradient {cin}->{cout}: rel err {err:.2e}")
+    assert err <= 2e-5
