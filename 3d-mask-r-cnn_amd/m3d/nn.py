@@ -142,10 +142,12 @@ SHARE_WINO_MAX_BYTES = int(float(os.environ.get("M3D_SHARE_WINO_MAX_GB", "6")) *
 # Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
 WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
 WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
-# below this channel count the weight gradient runs as a direct implicit GEMM
-# (its F(2x2x2) transforms cost more than they save at 64 channels; measured
-# on res2*_branch2b: Winograd fwd/dgrad 0.23 ms vs direct 0.27, wgrad 0.35 vs 0.33)
-WINO_WGRAD_MIN_C = int(os.environ.get("M3D_WINO_WGRAD_MIN_C", "128"))
+# below this channel count the weight gradient runs as a direct implicit GEMM.
+# Round 2 kept the 64-channel res2*_branch2b on the direct kernel (its own
+# F(2x2x2) input transform cost more than it saved: 0.35 vs 0.33 ms); with the
+# weight gradient on the forward's kept F(2x2x4) U there is no input transform
+# left to pay, and 64 is faster: step 29.8 -> 29.5 ms (same-box A/B, r03n)
+WINO_WGRAD_MIN_C = int(os.environ.get("M3D_WINO_WGRAD_MIN_C", "64"))
 
 
 def use_winograd(geo, cin, cout, in_sp):

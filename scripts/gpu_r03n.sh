@@ -15,3 +15,4 @@ print(json.dumps({k: r[k] for k in ("ms_per_step", "volumes_per_s", "loss", "pea
 PY
   echo "NZ=$nz $(tail -n 1 $OUT/s$nz.json)"
 done
+bash scripts/gpu_step_ab.sh r03n/ab "M3D_WINO_WGRAD_MIN_C=128" "M3D_WINO_WGRAD_MIN_C=64" || true
