@@ -136,6 +136,12 @@ SLAB_OVERLAP = os.environ.get("M3D_SLAB_OVERLAP", "1") != "0"
 CONV1_X3 = os.environ.get("M3D_CONV1_X3", "1") != "0"
 # split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
 SPLITK = os.environ.get("M3D_SPLITK", "1") != "0"
+# largest transformed input U a Winograd conv keeps from its forward for its
+# weight gradient (per layer): at 256^3 the P2 layers' U is 6.4 GB each, and
+# holding them through the backward pushed the caching allocator to the
+# device's capacity (263-306 GB reserved for 115-141 GB allocated, segments
+# freed and re-allocated inside the step)
+WINO_KEEP_MAX_BYTES = int(float(os.environ.get("M3D_WINO_KEEP_MAX_GB", "2")) * 2**30)
 # largest Winograd workspace a shared kernel keeps across its calls
 SHARE_WINO_MAX_BYTES = int(float(os.environ.get("M3D_SHARE_WINO_MAX_GB", "6")) * 2**30)
 
@@ -241,9 +247,36 @@ def _shared_wino_release(wshare):
         wshare.pop("pending_bwd", None)
 
 
-def _wino_ws(B, H, W, D, OD, cin, cout, dev):
+# One Winograd workspace arena per (device, stream), grown to the largest conv
+# and reused by every later one: the convs of a stream run in its order, so a
+# workspace is never live twice.  Per-call allocations of 4-20 GB workspaces
+# (at 256^3) of changing sizes fragmented the caching allocator -- 263 GB
+# reserved for 115 GB allocated, segments freed and re-allocated inside the
+# step, the 256^3 step at 290-890 ms instead of ~190 (r03p).  M3D_WINO_ARENA=0:
+# per-call workspaces.
+WINO_ARENA = os.environ.get("M3D_WINO_ARENA", "0") != "0"
+_ARENA = {}
+
+
+def _wino_ws(B, H, W, D, OD, cin, cout, dev, dedicated=False):
+    """(workspace, bytes) of one Winograd conv call; from the stream's arena
+    unless ``dedicated`` (a workspace the caller keeps across calls)."""
     n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, cin, cout))
-    return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
+    if dedicated or not WINO_ARENA:
+        return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(),
+           torch.cuda.current_stream(dev).cuda_stream)
+    buf = _ARENA.get(key)
+    if buf is None or buf.numel() * 4 < n + 4:
+        _ARENA.pop(key, None)          # the old one returns to the allocator, stream-ordered
+        buf = torch.empty(n // 4 + 1, device=dev, dtype=torch.float32)
+        _ARENA[key] = buf
+    return buf, n
+
+
+def release_wino_arena():
+    """Drop the Winograd workspace arenas (e.g. before torch.cuda.empty_cache())."""
+    _ARENA.clear()
 
 
 def same_out_pad(n, k, s):
@@ -399,6 +432,8 @@ class _ConvBNAct(torch.autograd.Function):
             nu = int(_L().m3d_conv3d_wino_u_bytes(B, H, W, OD, Cin)) // 4 \
                 if grads is not None and grads.get("kernel") is not None \
                 and min(Cin, Cout) >= WINO_WGRAD_MIN_C else 0
+            if nu * 4 > WINO_KEEP_MAX_BYTES:
+                nu = 0          # too large to hold until the backward: the weight gradient re-transforms x
             if pending is not None:
                 # phase 1 (weights + interior z tiles) overlaps the halo transfer
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
@@ -422,6 +457,8 @@ class _ConvBNAct(torch.autograd.Function):
                                                     1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u),
                                                     ptr(ws), wsb, stream()), "conv3d_fwd_wino_keep")
             else:
+                if wshare is not None:          # may be held across calls: not the arena
+                    ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
                 ws, wsb, v_ready = _shared_wino_ws(wshare, "fwd", ws, wsb, (w.data_ptr(), Cin, Cout))
                 check(_L().m3d_conv3d_fwd_wino_v(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
                                                  ptr(b), ptr(scale), ptr(shift), ptr(residual), 1 if relu else 0,
@@ -557,6 +594,8 @@ class _ConvBNAct(torch.autograd.Function):
                           "conv3d_bwd_data_wino_halo")
                     slab.return_halo_grads(dx, dh)
                 else:
+                    if ctx.wshare is not None:      # may be held across calls: not the arena
+                        ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
                     ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout))
                     check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                        geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, stream()),

@@ -532,6 +532,8 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
         except Exception as e:  # report, never hide
             out["step_roofline"] = {"error": repr(e)}
     del model, srpn, image
+    from m3d import nn as mnn
+    mnn.release_wino_arena()
     torch.cuda.empty_cache()
     return out
 
