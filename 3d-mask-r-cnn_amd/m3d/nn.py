@@ -57,6 +57,31 @@ _SIDE = {}
 _SIDE_USED = set()
 
 
+# Host throttle of the side stream under memory pressure: the tensors a
+# weight gradient reads (x, dz) are record_stream'ed to the side stream, so
+# the caching allocator can reuse their blocks only once the host sees the side
+# stream's events complete -- with the host enqueueing the whole backward far
+# ahead of the GPU (a 256^3 step is ~200 ms of GPU work) none are, every later
+# allocation takes new device memory, and reservations reach the device's
+# capacity (263-306 GB reserved for 115-141 GB allocated at 256^3) where the
+# allocator frees and re-allocates segments inside the step.  When more than
+# this fraction of the device is reserved, the host waits for the side stream
+# every WGRAD_THROTTLE_EVERY weight gradients (0: off).
+WGRAD_THROTTLE = float(os.environ.get("M3D_WGRAD_THROTTLE", "0.5"))
+WGRAD_THROTTLE_EVERY = int(os.environ.get("M3D_WGRAD_THROTTLE_EVERY", "4"))
+_THROTTLE = {}
+
+
+def _throttle(key, side):
+    if WGRAD_THROTTLE <= 0:
+        return
+    st = _THROTTLE.setdefault(key, {"total": torch.cuda.get_device_properties(key).total_memory, "n": 0})
+    st["n"] += 1
+    if st["n"] % max(1, WGRAD_THROTTLE_EVERY) == 0 and \
+            torch.cuda.memory_reserved(key) > WGRAD_THROTTLE * st["total"]:
+        side.synchronize()
+
+
 def _wgrad_stream(dev):
     if not WGRAD_STREAM:
         return None
@@ -65,6 +90,7 @@ def _wgrad_stream(dev):
         _SIDE[key] = torch.cuda.Stream(dev)
     _SIDE_USED.add(key)
     side = _SIDE[key]
+    _throttle(key, side)
     side.wait_stream(torch.cuda.current_stream(dev))
     return side
 

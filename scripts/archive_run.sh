@@ -5,6 +5,10 @@ set -e
 TAG=$1; O=gpurun_out/$TAG; O2=gpurun_out/${TAG}_256; P=profiles
 cp $O/bench.json $P/${TAG}_bench_128.json
 cp $O/pytest_gpu.log $P/${TAG}_pytest_gpu.log
+[ -f $O/step_roofline_128.json ] && cp $O/step_roofline_128.json $P/${TAG}_step_roofline_128.json
+[ -f $O/step_roofline_256.json ] && cp $O/step_roofline_256.json $P/${TAG}_step_roofline_256.json
+[ -f $O/host_overhead.txt ] && cp $O/host_overhead.txt $P/${TAG}_host_overhead.txt
+[ -f $O/smoke.log ] && cp $O/smoke.log $P/${TAG}_smoke.log
 cp $O/bench_kernels.txt $P/${TAG}_bench_kernels_128.txt
 cp $O/prof/run_kernel_stats.csv $P/${TAG}_bench_128_kernel_stats.csv
 for leg in gemm wgrad direct roi7 roi14; do
