@@ -4033,8 +4033,10 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
         return launch_stem_wgrad(p, dz, dw, st(s));
     // 1x1x1 stride-1 convs: im2col is x itself, the plain weight-gradient GEMM
     // dW += x^T dz -- on the exact bf16 split like the Winograd ones
+    // M3D_WGRAD1_X3_MIN_N: smallest Cout taking this path (A/B: 65 = round 2's Cout > 64)
+    static const int min_n = [] { const char* e = getenv("M3D_WGRAD1_X3_MIN_N"); return e ? atoi(e) : 65; }();
     if (vec && ((x3_mask() >> 3) & 1) && kh == 1 && kw == 1 && kd == 1 && sy == 1 && sx == 1 && sz == 1 &&
-        py == 0 && px == 0 && pz == 0 && OH == H && OW == W && OD == D && Cout > 64) {
+        py == 0 && px == 0 && pz == 0 && OH == H && OW == W && OD == D && Cout >= min_n) {
         launch_wgrad_x3(x, dz, dw, p.M, (int)Cin, (int)Cout, 1, 0, 0, 0, st(s));
         return check_launch("x3_wgrad_kernel (1x1x1)");
     }
