@@ -411,6 +411,103 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     }
 }
 
+// Producer / consumer form of line_fwd_sl_kernel<8> (M3D_ROI_PC=1): a
+// workgroup of 8 waves -- waves 0-3 gather and interpolate (loads only), waves
+// 4-7 store what their partner produced one z step earlier (stores only),
+// handing each z sample over through a double-buffered LDS slot with one
+// workgroup barrier per step.  Loads and stores then sit on different waves'
+// vmcnt counters: the gather never waits behind an output store.  Every wave
+// runs the same cd + 1 steps (uniform barriers; inactive waves / lanes idle).
+__global__ __launch_bounds__(512) void line_fwd_pc_kernel(LineArgs a, Pyr P, const int32_t* __restrict__ wperm) {
+    constexpr int SL = 8, LPL = 64 / SL;
+    __shared__ float4 slot[2][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool producer = wave < 4;
+    const int pw = wave & 3;
+    const int64_t items = a.lines;
+    const int64_t waves_per_slice = (items + SL - 1) / SL;
+    const int64_t bs8 = ((waves_per_slice + 3) / 4 + 7) / 8 * 8;
+    const int slice = (int)(blockIdx.x / bs8);
+    const int64_t lr = blockIdx.x - (int64_t)slice * bs8;
+    int64_t wv = ((lr % 8) * (bs8 / 8) + lr / 8) * 4 + pw;
+    bool active = slice < SL && wv < waves_per_slice;
+    if (active && wperm) wv = wperm[wv];
+    const int64_t line = wv * SL + lane / LPL;
+    active = active && line < items;
+    const int c = slice * LPL + (lane % LPL);
+    const int C4 = a.C >> 2;
+    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
+    // geometry of this lane's line (producers only read it; consumers need o)
+    float4* o = nullptr;
+    const float4* col[4] = {nullptr, nullptr, nullptr, nullptr};
+    float z1 = 0.f, z2 = 0.f, zsc = 0.f, yl = 0.f, xl = 0.f;
+    int D = 1;
+    bool yx_oob = true;
+    if (active) {
+        int64_t t = line;
+        const int x = (int)(t % a.cw); t /= a.cw;
+        const int y = (int)(t % a.ch);
+        const int64_t n = t / a.ch;
+        const int l = a.levels[n] - 2;
+        const int H = P.H[l], W = P.W[l];
+        D = P.D[l];
+        const float* box = a.boxes + n * 6;
+        const float y1 = box[0], x1 = box[1], y2 = box[3], x2 = box[4];
+        z1 = box[2]; z2 = box[5];
+        const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
+        const float in_x = axis_coord(x1, x2, W, a.cw, x, axis_scale(x1, x2, W, a.cw));
+        zsc = axis_scale(z1, z2, D, a.cd);
+        o = reinterpret_cast<float4*>(a.out + line * (int64_t)a.cd * a.C);
+        yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
+        if (!yx_oob) {
+            const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
+            const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
+            yl = in_y - (float)ty; xl = in_x - (float)lx;
+            const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
+            const float4* base = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)(n / a.N) * P.H[l] * W * D * a.C);
+            col[0] = base + ty * rowW + lx * rowD; col[1] = base + ty * rowW + rx * rowD;
+            col[2] = base + by * rowW + lx * rowD; col[3] = base + by * rowW + rx * rowD;
+        }
+    }
+    int pk = -1;
+    float4 kv[4];
+    for (int step = 0; step <= a.cd; ++step) {
+        if (producer && step < a.cd && active) {
+            const int z = step;
+            float4 r = ex;
+            const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
+            if (!yx_oob && !(in_z < 0 || in_z > (float)(D - 1))) {
+                const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
+                const float zl = in_z - (float)fz;
+                float4 fv[4];
+                if (fz == pk) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fv[q] = kv[q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
+                }
+                if (kz != fz) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) kv[q] = fv[q];
+                }
+                pk = kz;
+                r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
+                r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
+            }
+            slot[step & 1][pw][lane] = r;
+        }
+        if (!producer && step >= 1 && active) {
+            const int z = step - 1;
+            st_nt(o + (int64_t)z * C4 + c, slot[(step - 1) & 1][pw][lane]);
+        }
+        __syncthreads();
+    }
+}
+
 // Spatial order of the lines (m3d_pyramid_roi_align3d_fwd_ws): a counting sort
 // by the owner (y, x) column of each line -- bucket = level base + (b, ty, lx)
 // in raster order -- so lines of different, overlapping ROIs that read the
@@ -1498,6 +1595,11 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                                : (wperm ? 1 : std::max(1, std::min(zs_env, (int)pd)));
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
+            static const int pc_env = [] { const char* e = getenv("M3D_ROI_PC"); return e ? atoi(e) : 0; }();
+            if (pc_env && sl == 8 && zs == 1 && !spd && !perm) {
+                hipLaunchKernelGGL(line_fwd_pc_kernel, dim3(grid), dim3(512), 0, s, a, P, wperm);
+                return check_launch("line_fwd_pc_kernel");
+            }
             if (spd) {
                 if (spd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 else if (spd == 7) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
