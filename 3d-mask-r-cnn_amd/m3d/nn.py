@@ -163,11 +163,11 @@ CONV1_X3 = os.environ.get("M3D_CONV1_X3", "1") != "0"
 # split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
 SPLITK = os.environ.get("M3D_SPLITK", "1") != "0"
 # largest transformed input U a Winograd conv keeps from its forward for its
-# weight gradient (per layer): at 256^3 the P2 layers' U is 6.4 GB each, and
-# holding them through the backward pushed the caching allocator to the
-# device's capacity (263-306 GB reserved for 115-141 GB allocated, segments
-# freed and re-allocated inside the step)
-WINO_KEEP_MAX_BYTES = int(float(os.environ.get("M3D_WINO_KEEP_MAX_GB", "2")) * 2**30)
+# weight gradient (per layer; at 256^3 the P2 layers' U is 6.4 GB each).  With
+# the side-stream throttle below holding the allocator's reservations down,
+# keeping them is 4 ms faster per 256^3 step (177.6 vs 181.8 ms, 141 vs 133 GB
+# peak, r03r); above the cap the weight gradient re-transforms x
+WINO_KEEP_MAX_BYTES = int(float(os.environ.get("M3D_WINO_KEEP_MAX_GB", "8")) * 2**30)
 # largest Winograd workspace a shared kernel keeps across its calls
 SHARE_WINO_MAX_BYTES = int(float(os.environ.get("M3D_SHARE_WINO_MAX_GB", "6")) * 2**30)
 
