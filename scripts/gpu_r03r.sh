@@ -5,7 +5,7 @@ OUT=gpurun_out/r03r
 mkdir -p $OUT
 export TMPDIR=/tmp
 for rep in 1; do
-for e in "M3D_WINO_KEEP_MAX_GB=2" "M3D_WINO_KEEP_MAX_GB=8" "M3D_WINO_KEEP_MAX_GB=2" "M3D_WINO_KEEP_MAX_GB=8"; do
+for e in "M3D_WGRAD_THROTTLE_EVERY=4" "M3D_WGRAD_THROTTLE_EVERY=2" "M3D_WGRAD_THROTTLE_EVERY=8" "M3D_WGRAD_THROTTLE=0.4"; do
   env $e timeout -k 10 400 python -u - > $OUT/s.json 2> $OUT/s.err <<'PY' || { tail -20 $OUT/s.err; exit 1; }
 import json, sys, time
 sys.path[:0] = [".", "3d-mask-r-cnn_amd"]
