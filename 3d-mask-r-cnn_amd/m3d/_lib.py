@@ -119,6 +119,10 @@ _SIGS = {
                         c_p, c_i64, c_p, c_sz, c_p, c_p],
     "m3d_rpn_targets_async": [c_p, c_i64, c_p, c_i64, c_f, c_f, c_i32, c_f, c_i32, c_i32, c_p, ctypes.c_uint32,
                               c_p, c_p, c_i64, c_p, c_sz, c_p, c_p],
+    "m3d_rpn_loss_workspace_bytes": [c_i64],
+    "m3d_rpn_loss_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f, c_f, c_i64, c_i64, c_f, c_f, c_p, c_p, c_p,
+                         c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_rpn_loss_bwd": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p, c_p],
     "m3d_maxpool3d_bwd": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
@@ -152,6 +156,7 @@ _SIGS = {
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
              "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
+             "m3d_rpn_loss_workspace_bytes": c_sz,
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
              "m3d_get_deterministic": c_i32}

@@ -8,10 +8,15 @@ Mirrors core/models.py:3162-3387:
   the L2 term WEIGHT_DECAY*0.5*||w||^2/size(w) on every non-gamma/beta weight
   (3378-3384), optimised by the compiled Keras optimizer (m3d.optim: SGD,
   Adam or Adadelta with clipnorm and decay, 3349-3357).
-The two losses are tiny gathers over <= RPN_TRAIN_ANCHORS_PER_IMAGE anchors and
-run as torch ops on the GPU; all convolution / pooling / NMS work is libm3d.
+The two losses run on the GPU as one fused libm3d pass (m3d_rpn_loss_fwd: both
+terms and their gradients per anchor, fixed-order sums; rpn_losses) -- the
+framework-op form below (rpn_class_loss / rpn_bbox_loss) is kept for host
+tensors and as the GPU test's second reference; all convolution / pooling /
+NMS work is libm3d.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -48,6 +53,16 @@ class RPNTargets:
         self.n_cls, self.n_pos = len(cls_idx), len(pos_idx)
         # K.mean denominators (global counts; a depth slab holds only part of the anchors)
         self.cls_denom, self.pos_denom = self.n_cls, self.n_pos
+        self._dense(flat, device)
+
+    def _dense(self, flat_match, device):
+        """Per-anchor form for the fused loss kernel (m3d_rpn_loss_fwd):
+        match int8 [A] and each positive's row in gt_bbox (rank in flat order)."""
+        fm = np.asarray(flat_match).reshape(-1)
+        pos = fm == 1
+        row = np.cumsum(pos, dtype=np.int64) - 1
+        self.match8 = torch.from_numpy(np.sign(fm).astype(np.int8)).to(device)
+        self.row32 = torch.from_numpy(np.maximum(row, 0).astype(np.int32)).to(device)
 
     @classmethod
     def for_slab(cls, rpn_match, rpn_bbox, local_index, device):
@@ -73,6 +88,7 @@ class RPNTargets:
         t.gt_bbox = torch.from_numpy(rb[rows].reshape(-1, 6)).to(device)
         t.n_cls, t.n_pos = len(cls_idx), len(pos_idx)
         t.cls_denom, t.pos_denom = int((m != 0).sum()), len(gpos)
+        t._dense(lm, device)
         return t
 
 
@@ -155,6 +171,70 @@ def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     return (h_xy + h_z).sum() / (6 * t.pos_denom)
 
 
+FUSED_RPN_LOSS = os.environ.get("M3D_FUSED_RPN_LOSS", "1") != "0"   # 0: the framework-op form (A/B)
+
+
+class _RPNLossFused(torch.autograd.Function):
+    """Both RPN losses and their weighted total in two launches
+    (m3d_rpn_loss_fwd; the per-anchor gradients are computed in the same pass
+    and scaled in place by one launch in the backward), replacing ~100 small
+    framework launches the host issues between the forward and the backward."""
+
+    @staticmethod
+    def forward(ctx, logits, bbox, match, row, gt, den_cls, den_pos, w_cls, w_box, alpha, gamma):
+        A = match.numel()
+        if logits.numel() != 2 * A or bbox.numel() != 6 * A:
+            raise ValueError("rpn loss: logits / rpn_bbox do not match the targets' anchor count")
+        logits = logits.contiguous()
+        bbox = bbox.contiguous()
+        dev = logits.device
+        g_logits = torch.empty_like(logits)
+        g_bbox = torch.empty_like(bbox)
+        total, lc, lb = (torch.empty((), device=dev, dtype=torch.float32) for _ in range(3))
+        scales = torch.empty(2, device=dev, dtype=torch.float32)
+        L = _lib.load()
+        ws = torch.empty(max(int(L.m3d_rpn_loss_workspace_bytes(A)), 1), device=dev, dtype=torch.uint8)
+        if gt.shape[0] == 0:
+            gt = torch.zeros(1, 6, device=dev, dtype=torch.float32)
+        _lib.check(L.m3d_rpn_loss_fwd(_lib.ptr(logits), _lib.ptr(bbox), _lib.ptr(match),
+                             _lib.ptr(row), _lib.ptr(gt), int(gt.shape[0]), A, float(alpha), float(gamma),
+                             int(den_cls), int(den_pos), float(w_cls), float(w_box), _lib.ptr(g_logits),
+                             _lib.ptr(g_bbox), _lib.ptr(total), _lib.ptr(lc), _lib.ptr(lb), _lib.ptr(scales),
+                             _lib.ptr(ws), ws.numel(), _lib.stream()),
+                   "m3d_rpn_loss_fwd")
+        ctx.saved = (g_logits, g_bbox, scales, A)
+        ctx.mark_non_differentiable(lc, lb)
+        return total, lc, lb
+
+    @staticmethod
+    def backward(ctx, g_total, _g_lc, _g_lb):
+        g_logits, g_bbox, scales, A = ctx.saved
+        if g_total is None:
+            return (None,) * 11
+        g_total = g_total.contiguous().to(torch.float32)
+        _lib.check(_lib.load().m3d_rpn_loss_bwd(_lib.ptr(g_logits), _lib.ptr(g_bbox), A, _lib.ptr(g_total),
+                             _lib.ptr(scales), _lib.stream()), "m3d_rpn_loss_bwd")
+        return (g_logits, g_bbox) + (None,) * 9
+
+
+def rpn_losses(t, rpn_class_logits, rpn_bbox, w_cls=1.0, w_box=1.0, alpha=0.90, gamma=1.5):
+    """(total, rpn_class_loss, rpn_bbox_loss): core/models.py:1589-1673 weighted
+    as 3366-3376.  On the GPU through the fused libm3d kernel; host tensors
+    (the CPU depth-slab tests) take the framework-op form below."""
+    if rpn_class_logits.is_cuda and FUSED_RPN_LOSS:
+        if isinstance(t, DeviceRPNTargets):
+            pos = (t.match == 1).to(torch.int32)
+            match8, row32 = t.match.to(torch.int8), torch.cumsum(pos, 0, dtype=torch.int32) - 1
+            gt, den_c, den_p = t.bbox, 0, 0
+        else:
+            match8, row32, gt, den_c, den_p = t.match8, t.row32, t.gt_bbox, t.cls_denom, t.pos_denom
+        return _RPNLossFused.apply(rpn_class_logits, rpn_bbox, match8, row32, gt.contiguous(), den_c, den_p,
+                                   w_cls, w_box, alpha, gamma)
+    lc = rpn_class_loss(t, rpn_class_logits, alpha, gamma)
+    lb = rpn_bbox_loss(t, rpn_bbox)
+    return lc * w_cls + lb * w_box, lc.detach(), lb.detach()
+
+
 # ---------------------------------------------------------------------------
 # model
 # ---------------------------------------------------------------------------
@@ -202,6 +282,11 @@ class RPN:
         lb = rpn_bbox_loss(targets, out["rpn_bbox"])
         return lc, lb
 
+    def loss_total(self, out, targets: RPNTargets):
+        """(weighted total, rpn_class_loss, rpn_bbox_loss) -- the fused kernel on the GPU."""
+        return rpn_losses(targets, out["rpn_class_logits"], out["rpn_bbox"],
+                          self.LOSS_WEIGHTS["rpn_class_loss"], self.LOSS_WEIGHTS["rpn_bbox_loss"])
+
     # -- one fit step -----------------------------------------------------
     @property
     def iterations(self):
@@ -239,8 +324,7 @@ class RPN:
         self.store.zero_grad()
         out = self.forward(image, proposals=False)
         join = self.proposals_async(out)[1] if proposals else None
-        lc, lb = self.losses(out, targets)
-        total = lc * self.LOSS_WEIGHTS["rpn_class_loss"] + lb * self.LOSS_WEIGHTS["rpn_bbox_loss"]
+        total, lc, lb = self.loss_total(out, targets)
         total.backward()
         self.rpn.finish_backward()
         return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),

@@ -151,8 +151,7 @@ def data_parallel_train_step(model, image, targets, world, proposals=True, overl
     try:
         out = model.forward(image, proposals=False)
         join = model.proposals_async(out)[1] if proposals else None   # overlaps the backward
-        lc, lb = model.losses(out, targets)
-        total = lc * model.LOSS_WEIGHTS["rpn_class_loss"] + lb * model.LOSS_WEIGHTS["rpn_bbox_loss"]
+        total, lc, lb = model.loss_total(out, targets)
         total.backward()
     finally:
         mnn.GRAD_HOOK = None
@@ -260,8 +259,7 @@ class SlabRPN:
         try:
             out = self.forward(image_slab, proposals=False)
             join = self._proposals_async(out) if proposals else None     # overlaps the backward
-            lc, lb = m.losses(out, self.targets)
-            total = lc * m.LOSS_WEIGHTS["rpn_class_loss"] + lb * m.LOSS_WEIGHTS["rpn_bbox_loss"]
+            total, lc, lb = m.loss_total(out, self.targets)
             with slab.active(self.sg):          # halo gradients flow during backward
                 total.backward()
         finally:

@@ -507,6 +507,28 @@ int m3d_rpn_targets_async(const float* anchors, int64_t A, const float* gt_boxes
                           uint32_t seed, int8_t* rpn_match, float* rpn_bbox, int64_t list_cap,
                           void* workspace, size_t ws_bytes, int32_t* counts_dev, m3d_stream_t s);
 
+/* RPN training losses with their gradients in one pass: rpn_class_loss_graph
+ * (core/models.py:1589-1625, focal CE, alpha / gamma) and rpn_bbox_loss_graph
+ * (core/models.py:1629-1673, clipped XY/Z Huber), weighted (core/models.py:
+ * 3366-3376).  logits [A,2], pred [A,6] (A = all anchors of the batch,
+ * flattened), match [A] int8 (1 / -1 / 0), row [A] int32 = the positive's row
+ * in gt_bbox [n_gt,6] (n_gt >= 1; read for match == 1 only, clamped).
+ * den_cls / den_pos: the K.mean denominators (anchors with match != 0,
+ * positives) when > 0, else counted here.  Writes the scalars total (=
+ * w_cls * class + w_box * bbox), cls_loss, box_loss, scales[2] = {w_cls /
+ * den_cls, w_box / (6 den_pos)} and the unnormalised gradients g_logits [A,2],
+ * g_pred [A,6]; m3d_rpn_loss_bwd scales them in place by *g_total * scales[0]
+ * (logits) / scales[1] (pred).  Fixed-order sums.
+ * workspace: m3d_rpn_loss_workspace_bytes(A). */
+size_t m3d_rpn_loss_workspace_bytes(int64_t A);
+int m3d_rpn_loss_fwd(const float* logits, const float* pred, const int8_t* match, const int32_t* row,
+                     const float* gt_bbox, int64_t n_gt, int64_t A, float alpha, float gamma,
+                     int64_t den_cls, int64_t den_pos, float w_cls, float w_box, float* g_logits,
+                     float* g_pred, float* total, float* cls_loss, float* box_loss, float* scales,
+                     void* workspace, size_t ws_bytes, m3d_stream_t s);
+int m3d_rpn_loss_bwd(float* g_logits, float* g_pred, int64_t A, const float* g_total, const float* scales,
+                     m3d_stream_t s);
+
 /* ---------------------------------------------------------------------------
  * Elementwise / reduction kernels of the backbone-FPN-RPN graph.
  * ------------------------------------------------------------------------- */
