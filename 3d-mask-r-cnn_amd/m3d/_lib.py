@@ -151,6 +151,7 @@ _SIGS = {
                        c_p],
     "m3d_adadelta_keras": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_p, c_p],
     "m3d_set_deterministic": [c_i32, c_p, c_sz],
+    "m3d_stream_fork": [c_p, c_p, c_i32],
     "m3d_get_deterministic": [],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,

@@ -82,6 +82,23 @@ def _throttle(key, side):
         side.synchronize()
 
 
+# Fork / join events of the weight-gradient stream (m3d_stream_fork): "2" no
+# system-scope fence (default; both streams are on one device, agent scope is
+# all the consumer needs), "1" device-scope release, "0" plain event, "torch":
+# Stream.wait_stream.  The fork showed as a ~7.5 us compute-queue bubble per
+# layer in the 128^3 kernel trace; A/B (scripts/gpu_r03x.sh, same box): mode 2
+# 29.80 / 29.90 ms per step, torch / 0 / 1 30.05-30.10 ms.
+FORK_EVENT = os.environ.get("M3D_FORK_EVENT", "2")
+
+
+def _fork(src, dst):
+    """dst waits for the work enqueued on src so far."""
+    if FORK_EVENT == "torch":
+        dst.wait_stream(src)
+        return
+    check(_lib.load().m3d_stream_fork(src.cuda_stream, dst.cuda_stream, int(FORK_EVENT)), "stream_fork")
+
+
 def _wgrad_stream(dev):
     if not WGRAD_STREAM:
         return None
@@ -91,7 +108,7 @@ def _wgrad_stream(dev):
     _SIDE_USED.add(key)
     side = _SIDE[key]
     _throttle(key, side)
-    side.wait_stream(torch.cuda.current_stream(dev))
+    _fork(torch.cuda.current_stream(dev), side)
     return side
 
 
@@ -99,7 +116,7 @@ def join_wgrad(dev=None):
     """Make the current stream wait for the weight gradients launched on the side stream."""
     for key in list(_SIDE_USED):
         if dev is None or key == (dev.index if dev.index is not None else torch.cuda.current_device()):
-            torch.cuda.current_stream(torch.device("cuda", key)).wait_stream(_SIDE[key])
+            _fork(_SIDE[key], torch.cuda.current_stream(torch.device("cuda", key)))
             _SIDE_USED.discard(key)
 
 
@@ -109,7 +126,7 @@ def _grad_done(grads, side=None):
         if side is not None:
             # the bucket all-reduce must follow this layer's weight gradients
             # (side) and its BN/bias gradients (compute stream)
-            side.wait_stream(torch.cuda.current_stream())
+            _fork(torch.cuda.current_stream(), side)
             with torch.cuda.stream(side):
                 h[0].done(h[1])
         else:

@@ -49,6 +49,13 @@ int m3d_abi_version(void);
 int m3d_set_deterministic(int32_t on, void* scratch, size_t bytes);
 int32_t m3d_get_deterministic(void);
 
+/* Stream fork / join of the training step (weight gradients on a side stream):
+ * `to` waits for everything enqueued on `from` so far, through a pooled event
+ * (hipEventDisableTiming; mode 1: + hipEventReleaseToDevice, mode 2: +
+ * hipEventDisableSystemFence, mode 0: neither).  Both streams must be on the
+ * same device: the event's release need not reach the host. */
+int m3d_stream_fork(m3d_stream_t from, m3d_stream_t to, int32_t mode);
+
 /* ---------------------------------------------------------------------------
  * CropAndResize3D family.  Replaces the TF custom ops of the vendored wheel
  * tensorflow_nms_car_3d==0.1.0 imported at core/custom_op/custom_op.py:22-24:
