@@ -1610,7 +1610,17 @@ struct WinoGeom {
     // exchange): 0 all tiles, 1 interior only (tz in [1, TZ-1): no halo plane in
     // the window), 2 the first / last z tile only
     int tz_mode;
+    // XCD-aware block order of the transform kernels (M3D_WINO_XCD=1): the
+    // round-robin XCD dispatch gets contiguous tile ranges per XCD, so the
+    // windows that overlap neighbouring tiles' stay in one L2
+    int xcd;
 };
+
+__device__ __forceinline__ int64_t wino_block(const WinoGeom& g) {
+    const unsigned nb = gridDim.x, b = blockIdx.x;
+    if (g.xcd && (nb & 7u) == 0) return (int64_t)(b & 7u) * (nb >> 3) + (b >> 3);
+    return b;
+}
 
 __device__ __forceinline__ void bt4(float& a0, float& a1, float& a2, float& a3) {
     const float t0 = a0 - a2, t1 = a1 + a2, t2 = a2 - a1, t3 = a1 - a3;
@@ -1731,7 +1741,7 @@ template <int NZ, bool X3O = false, bool HALO = false>
 __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
                                                          int C, float* __restrict__ U) {
     constexpr int P = ZT<NZ>::P;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = wino_block(g) * blockDim.x + threadIdx.x;
     if (i >= g.T * C) return;
     const int c = (int)(i % C);
     const int64_t t = i / C;
@@ -1931,7 +1941,7 @@ template <int NZ, bool HALO>
 __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, const WinoGeom& g,
                                                  int N, const Epi& e) {
     constexpr int P = ZT<NZ>::P;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = wino_block(g) * blockDim.x + threadIdx.x;
     if (i >= g.T * N) return;
     const int n = (int)(i % N);
     const int64_t t = i / N;
@@ -2869,6 +2879,8 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
     g.tz_mode = 0;
+    static const int xcd = [] { const char* e = getenv("M3D_WINO_XCD"); return e ? atoi(e) : 0; }();
+    g.xcd = xcd;
     return g;
 }
 

@@ -1,0 +1,37 @@
+"""m3d_stream_fork (the weight-gradient stream's fork / join, m3d.nn._fork):
+work enqueued on the destination after the fork sees everything the source
+stream wrote before it, for every event kind; a bad mode is rejected."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_stream_fork_orders_work(cuda, mode):
+    import m3d._lib as lib
+    L = lib.load()
+    a, b = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    n = 1 << 24
+    for it in range(4):
+        with torch.cuda.stream(a):
+            x = torch.empty(n, device=cuda)
+            x.fill_(float(it + 1))
+            for _ in range(8):                         # keep stream a busy past the fork
+                x.mul_(1.0000001)
+            y = x * 2.0
+        lib.check(L.m3d_stream_fork(a.cuda_stream, b.cuda_stream, mode), "stream_fork")
+        with torch.cuda.stream(b):
+            s = y.sum()
+        y.record_stream(b)
+        lib.check(L.m3d_stream_fork(b.cuda_stream, torch.cuda.current_stream(cuda).cuda_stream, mode),
+                  "stream_fork")
+        want = 2.0 * (it + 1) * (1.0000001 ** 8) * n
+        assert abs(float(s) - want) <= 1e-5 * want
+
+
+def test_stream_fork_bad_mode(cuda):
+    import m3d._lib as lib
+    s = torch.cuda.current_stream(cuda).cuda_stream
+    with pytest.raises(ValueError):
+        lib.check(lib.load().m3d_stream_fork(s, s, 3), "stream_fork")
