@@ -29,7 +29,8 @@ with warnings.catch_warnings(record=True) as w:
     torch.cuda.set_sync_debug_mode("warn")
     model.train_step(image, targets)
     torch.cuda.set_sync_debug_mode(0)
-    syncs = [str(x.message).split("\n")[0][:160] for x in w]
+    syncs = [str(x.message).split("\n")[0][:160] for x in w
+             if "prototype feature" not in str(x.message)]        # the mode's own notice
 torch.cuda.synchronize()
 print(f"synchronising calls in one step: {len(syncs)}")
 for s in syncs[:12]:
