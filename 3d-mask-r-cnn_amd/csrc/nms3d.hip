@@ -22,6 +22,7 @@
 //              all threads OR the kept rows into the LDS-resident removed
 //              mask.  Kept original indices are written in selection order.
 #include <float.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -245,6 +246,108 @@ __global__ __launch_bounds__(1024) void nms_reduce_kernel(const uint64_t* __rest
     if (tid == 0) *num_keep = nkeep_sh;
 }
 
+// Greedy reduction for cb <= 256 (N <= 16384, every ProposalLayer shape of the
+// configs): thread (g, w) owns mask word w of the block rows g, g+G, ... (G =
+// 1024 / cb row groups), so the OR phase needs no index arithmetic beyond the
+// launch, and the NEXT block's rows are loaded into the second register buffer
+// while wave 0 resolves the current block -- one global round trip per block
+// is hidden instead of paid.  Same greedy result as nms_reduce_kernel.
+constexpr int NR_RPG = 16;   // rows per group held per buffer (G >= 4)
+
+__device__ __forceinline__ void nr_load(const uint64_t* __restrict__ mask, int64_t N, int64_t cb, int64_t blk,
+                                        int g, int G, int w, bool own, uint64_t (&v)[NR_RPG]) {
+#pragma unroll
+    for (int k = 0; k < NR_RPG; ++k) {
+        const int r = g + G * k;
+        const int64_t row = blk * 64 + r;
+        v[k] = (own && r < 64 && row < N && w > blk) ? mask[row * cb + w] : 0ull;
+    }
+}
+
+__global__ __launch_bounds__(1024) void nms_reduce_pf_kernel(const uint64_t* __restrict__ mask,
+                                                             const uint64_t* __restrict__ keys,
+                                                             int64_t N, int64_t cb, int max_out,
+                                                             int32_t* __restrict__ keep,
+                                                             int32_t* __restrict__ num_keep) {
+    __shared__ uint64_t removed[256];
+    __shared__ uint64_t kept_sh;
+    __shared__ int nkeep_sh, stop_sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int G = 1024 / (int)cb < 64 ? 1024 / (int)cb : 64;
+    const int g = tid / (int)cb, w = tid % (int)cb;
+    const bool own = g < G;
+    for (int64_t q = tid; q < cb; q += blockDim.x) removed[q] = 0;
+    if (tid == 0) { nkeep_sh = 0; stop_sh = 0; kept_sh = 0; }
+    uint64_t va[NR_RPG], vb[NR_RPG];
+    nr_load(mask, N, cb, 0, g, G, w, own, va);
+    __syncthreads();
+    uint64_t key_n = 0, diag_n = 0;
+    if (wave == 0) {
+        key_n = lane < N ? keys[lane] : ~0ull;
+        diag_n = lane < N ? mask[(int64_t)lane * cb] : 0ull;
+    }
+    // one block: resolve (wave 0), then OR the kept rows of cur into removed[]
+    auto block = [&](int64_t blk, const uint64_t (&cur)[NR_RPG]) -> bool {
+        if (wave == 0) {
+            const int64_t row = blk * 64 + lane;
+            const uint64_t key = key_n;
+            const bool valid = row < N && (key >> 32) != 0xFFFFFFFFull;
+            const uint64_t diag = valid ? diag_n : 0ull;
+            if (blk + 1 < cb) {
+                const int64_t rn = row + 64;
+                key_n = rn < N ? keys[rn] : ~0ull;
+                diag_n = rn < N ? mask[rn * cb + blk + 1] : 0ull;
+            }
+            const uint64_t vmask = __ballot(valid);
+            uint64_t rem = removed[blk];
+            uint64_t kept = 0;
+            const int nk0 = nkeep_sh;
+            int nk = nk0;
+            const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+            for (int r = 0; r < 64; ++r) {
+                if (!((vmask >> r) & 1ull)) break;
+                if (nk >= max_out) break;
+                if (!((rem >> r) & 1ull)) {
+                    kept |= (1ull << r);
+                    ++nk;
+                    const uint64_t d = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(dlo, r) |
+                                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(dhi, r) << 32);
+                    rem |= d;
+                }
+            }
+            if ((kept >> lane) & 1ull) {
+                const int j = __popcll(kept & ((1ull << lane) - 1ull));
+                keep[nk0 + j] = (int32_t)(uint32_t)key;
+            }
+            if (lane == 0) {
+                kept_sh = kept;
+                nkeep_sh = nk;
+                if (nk >= max_out || vmask != ~0ull) stop_sh = 1;
+            }
+        }
+        __syncthreads();
+        if (stop_sh) return false;
+        const uint64_t kept = kept_sh;
+        uint64_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < NR_RPG; ++k) {
+            const int r = g + G * k;
+            if (r < 64 && ((kept >> r) & 1ull)) acc |= cur[k];
+        }
+        if (own && acc) atomicOr((unsigned long long*)&removed[w], (unsigned long long)acc);
+        __syncthreads();
+        return true;
+    };
+    for (int64_t blk = 0; blk < cb; blk += 2) {
+        if (blk + 1 < cb) nr_load(mask, N, cb, blk + 1, g, G, w, own, vb);
+        if (!block(blk, va)) break;
+        if (blk + 1 >= cb) break;
+        if (blk + 2 < cb) nr_load(mask, N, cb, blk + 2, g, G, w, own, va);
+        if (!block(blk + 1, vb)) break;
+    }
+    if (tid == 0) *num_keep = nkeep_sh;
+}
+
 // ---- ProposalLayer ----------------------------------------------------------
 // gidx (optional): the anchor's index in the whole volume's anchor list when
 // this rank holds a depth slab of it (the key then sorts in global order).
@@ -396,6 +499,13 @@ extern "C" int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int
                        w.sboxes, N, cb, iou_thr, mode, w.mask);
     rc = check_launch("nms_mask_kernel");
     if (rc) return rc;
+    // M3D_NMS_REDUCE=0: the general kernel at every size (A/B)
+    static const int pf = [] { const char* e = getenv("M3D_NMS_REDUCE"); return e ? atoi(e) : 1; }();
+    if (pf && cb <= 256) {
+        hipLaunchKernelGGL(nms_reduce_pf_kernel, dim3(1), dim3(1024), 0, st(s), w.mask, w.keys, N, cb, max_out,
+                           keep, num_keep);
+        return check_launch("nms_reduce_pf_kernel");
+    }
     hipLaunchKernelGGL(nms_reduce_kernel, dim3(1), dim3(1024), sizeof(uint64_t) * cb, st(s),
                        w.mask, w.keys, N, cb, max_out, keep, num_keep);
     return check_launch("nms_reduce_kernel");

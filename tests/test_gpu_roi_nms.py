@@ -106,7 +106,10 @@ def test_nms_bit_exact(cuda):
 
 
 @pytest.mark.parametrize("n,thr,max_out", [(0, 0.5, 10), (1, 0.5, 10), (64, 0.5, 64), (65, 0.1, 3),
-                                           (15000, 0.7, 6000), (20000, 0.5, 20000)])
+                                           (15000, 0.7, 6000), (20000, 0.5, 20000),
+                                           # the prefetching reduction (cb <= 256): G = 64, 15, 6, 4 row groups
+                                           (1000, 0.3, 1000), (4097, 0.05, 4097), (10000, 0.9, 3000),
+                                           (16384, 0.5, 16384)])
 def test_nms_sizes_vs_oracle(cuda, n, thr, max_out):
     from m3d import ops
     rng = np.random.default_rng(n)
