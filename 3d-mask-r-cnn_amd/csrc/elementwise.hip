@@ -252,6 +252,12 @@ __global__ void subsample221_kernel(const float4* __restrict__ src, int B, int H
     }
 }
 
+// rows per loop iteration with all their loads first (A/B builds: 2 and 4
+// measured 28.42-28.46 / 28.57-28.59 ms per 128^3 step against 28.31-28.42
+// for 1, scripts/gpu_bn_unroll.sh -- the kernel is not latency-bound there)
+#ifndef BN_UNROLL
+#define BN_UNROLL 1
+#endif
 // Thread layout: T threads per row cover T channel quads; R = 256/T rows per
 // block pass; gridDim.y channel groups of 4*T channels.  Each block writes its
 // per-channel partial sums to part[3][gridDim.x][C] (no contended atomics);
@@ -270,35 +276,47 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
         if (scale) { const float4 v = *(const float4*)(scale + c); sc[0] = v.x; sc[1] = v.y; sc[2] = v.z; sc[3] = v.w; }
         if (mean) { const float4 v = *(const float4*)(mean + c); mu[0] = v.x; mu[1] = v.y; mu[2] = v.z; mu[3] = v.w; }
         if (rstd) { const float4 v = *(const float4*)(rstd + c); rs[0] = v.x; rs[1] = v.y; rs[2] = v.z; rs[3] = v.w; }
-        for (int64_t r = (int64_t)blockIdx.x * R + ty; r < M; r += (int64_t)gridDim.x * R) {
-            const int64_t off = r * C + c;
-            const float4 g4 = *(const float4*)(dy + off);
-            float g[4] = {g4.x, g4.y, g4.z, g4.w};
-            if (relu) {
-                const float4 y4 = *(const float4*)(y + off);
-                if (!(y4.x > 0.f)) g[0] = 0.f;
-                if (!(y4.y > 0.f)) g[1] = 0.f;
-                if (!(y4.z > 0.f)) g[2] = 0.f;
-                if (!(y4.w > 0.f)) g[3] = 0.f;
-            }
-            float zz[4] = {0, 0, 0, 0};
-            if (want_xhat) { const float4 v = *(const float4*)(z + off); zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w; }
-            float d[4];
+        // BN_UNROLL rows per iteration, all their loads issued before any use
+        const int64_t step = (int64_t)gridDim.x * R;
+        for (int64_t r0 = (int64_t)blockIdx.x * R + ty; r0 < M; r0 += BN_UNROLL * step) {
+            float4 g4[BN_UNROLL], y4[BN_UNROLL], z4[BN_UNROLL], a4[BN_UNROLL];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                d[q] = g[q] * sc[q];
-                s_p[q] += g[q];
-                s_x[q] += g[q] * ((zz[q] - mu[q]) * rs[q]);
-                s_z[q] += d[q];
+            for (int u = 0; u < BN_UNROLL; ++u) {
+                const int64_t r = r0 + u * step;
+                const bool in = r < M;
+                const int64_t off = (in ? r : r0) * C + c;
+                g4[u] = *(const float4*)(dy + off);
+                y4[u] = relu ? *(const float4*)(y + off) : make_float4(1.f, 1.f, 1.f, 1.f);
+                z4[u] = want_xhat ? *(const float4*)(z + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+                a4[u] = (dres && accumulate_res) ? *(const float4*)(dres + off) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            if (dz) *(float4*)(dz + off) = make_float4(d[0], d[1], d[2], d[3]);
-            if (dres) {
-                float4 o = make_float4(g[0], g[1], g[2], g[3]);
-                if (accumulate_res) {
-                    const float4 a = *(const float4*)(dres + off);
-                    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+#pragma unroll
+            for (int u = 0; u < BN_UNROLL; ++u) {
+                const int64_t r = r0 + u * step;
+                if (r >= M) break;
+                const int64_t off = r * C + c;
+                float g[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
+                if (relu) {
+                    if (!(y4[u].x > 0.f)) g[0] = 0.f;
+                    if (!(y4[u].y > 0.f)) g[1] = 0.f;
+                    if (!(y4[u].z > 0.f)) g[2] = 0.f;
+                    if (!(y4[u].w > 0.f)) g[3] = 0.f;
                 }
-                *(float4*)(dres + off) = o;
+                const float zz[4] = {z4[u].x, z4[u].y, z4[u].z, z4[u].w};
+                float d[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    d[q] = g[q] * sc[q];
+                    s_p[q] += g[q];
+                    s_x[q] += g[q] * ((zz[q] - mu[q]) * rs[q]);
+                    s_z[q] += d[q];
+                }
+                if (dz) *(float4*)(dz + off) = make_float4(d[0], d[1], d[2], d[3]);
+                if (dres) {
+                    float4 o = make_float4(g[0], g[1], g[2], g[3]);
+                    if (accumulate_res) { o.x += a4[u].x; o.y += a4[u].y; o.z += a4[u].z; o.w += a4[u].w; }
+                    *(float4*)(dres + off) = o;
+                }
             }
         }
     }
