@@ -1521,7 +1521,14 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
     const int64_t cus = num_cus();
     int64_t splits = (cus + tiles - 1) / tiles;
-    const int64_t max_splits = (M + 63) / 64;              // >= 4 k-steps per workgroup
+    // M3D_X3W_TR_MINM: fewest m rows per workgroup.  Every split adds a 256x256
+    // fp32 atomic epilogue: the small-m 1x1x1 gradients of res4 / res5 (m = 8192
+    // / 2048 at 128^3, 4 output tiles) split 64 ways at the old floor of 64 rows,
+    // and their 16.7 M atomics per launch slowed the data-gradient stream beside
+    // them.  256: 128^3 step 28.73 -> 27.8 ms (scripts/gpu_wgrad1b.sh, wg1c/d A/B:
+    // 256 / 384 / 512 equal within noise, 1024 28.2-28.5 ms); alone 73 -> 64 us.
+    static const int64_t minm = [] { const char* e = getenv("M3D_X3W_TR_MINM"); return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256; }();
+    const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     const WgOut wo = wg_out(splits, nbatch, K, N);
@@ -1547,7 +1554,10 @@ static int wgrad_x3_env() { return (x3_mask() >> 2) & 1; }
 // C[b] += A[b]^T B[b]: A [M][K], B [M][N], C [K][N], batch strides bsa/bsb/bsc
 static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M, int K, int N, int nbatch,
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
-    if (wgrad_tr_env() && K >= 192 && N >= 192) {
+    // M3D_X3W_TR_MIN_M: smallest m (per batch) taking the 256x256 kernel (small-m
+    // gradients split m finely to fill the chip, one atomic epilogue per split)
+    static const int64_t tr_min_m = [] { const char* e = getenv("M3D_X3W_TR_MIN_M"); return e ? (int64_t)atoll(e) : (int64_t)0; }();
+    if (wgrad_tr_env() && K >= 192 && N >= 192 && M >= tr_min_m) {
         launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
         return;
     }
