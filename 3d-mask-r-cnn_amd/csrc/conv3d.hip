@@ -1563,7 +1563,10 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     }
     const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;
-    const int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
+    // M3D_X3W_MINM: this kernel's m-split floor (default: M3D_WGRAD_MINM's)
+    static const int x3w_minm = [] { const char* e = getenv("M3D_X3W_MINM"); return e ? atoi(e) : 0; }();
+    const int64_t mfloor = x3w_minm > 0 ? x3w_minm : wgrad_minm_env();
+    const int64_t minm = mfloor > 32 ? mfloor : 32;
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
