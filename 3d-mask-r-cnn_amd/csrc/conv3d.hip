@@ -1520,7 +1520,10 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
     const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
     const int64_t cus = num_cus();
-    int64_t splits = (cus + tiles - 1) / tiles;
+    // M3D_X3W_TR_FLOOR=1: splits = floor(CUs / tiles) (one wave of workgroups at
+    // one per CU) instead of the ceiling (e.g. 96 tiles: 2 x 96 vs 3 x 96 = 288)
+    static const int fl = [] { const char* e = getenv("M3D_X3W_TR_FLOOR"); return e ? atoi(e) : 0; }();
+    int64_t splits = fl ? cus / tiles : (cus + tiles - 1) / tiles;
     // M3D_X3W_TR_MINM: fewest m rows per workgroup.  Every split adds a 256x256
     // fp32 atomic epilogue: the small-m 1x1x1 gradients of res4 / res5 (m = 8192
     // / 2048 at 128^3, 4 output tiles) split 64 ways at the old floor of 64 rows,
