@@ -19,7 +19,7 @@ const DetState& det() { return g_det; }
 }  // namespace m3d
 
 extern "C" const char* m3d_last_error(void) { return m3d::g_err; }
-extern "C" int m3d_abi_version(void) { return 1; }
+extern "C" int m3d_abi_version(void) { return 2; }  // 2: m3d_proposal_decode(n_anchors, err)
 
 extern "C" int m3d_set_deterministic(int32_t on, void* scratch, size_t bytes) {
     if (on && (!scratch || bytes < 4096 || (reinterpret_cast<uintptr_t>(scratch) & 15)))

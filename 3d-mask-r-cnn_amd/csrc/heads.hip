@@ -58,12 +58,13 @@ __global__ void refine_kernel(const float* __restrict__ rois, const float* __res
     float dh = dl[3] * sd.v[3], dw = dl[4] * sd.v[4], dd = dl[5] * sd.v[5];
     const float h = y2 - y1, w = x2 - x1, d = z2 - z1;
     const float cy = y1 + 0.5f * h, cx = x1 + 0.5f * w, cz = z1 + 0.5f * d;
-    const float lim = logf(1000.0f / 16.0f);                   // LOG_SCALE_LIMIT
+    const float lim = (float)log(1000.0 / 16.0);                // LOG_SCALE_LIMIT (float64 log, as the oracle)
     dh = smin(smax(dh, -lim), lim);
     dw = smin(smax(dw, -lim), lim);
     dd = smin(smax(dd, -lim), lim);
     const float cy2 = cy + dy * h, cx2 = cx + dx * w, cz2 = cz + dz * d;
-    const float h2 = h * expf(dh), w2 = w * expf(dw), d2 = d * expf(dd);
+    // exp through float64 (the oracle's form, oracle/heads_ref.py): bit-identical boxes
+    const float h2 = h * (float)exp((double)dh), w2 = w * (float)exp((double)dw), d2 = d * (float)exp((double)dd);
     const float ny1 = cy2 - 0.5f * h2, nx1 = cx2 - 0.5f * w2, nz1 = cz2 - 0.5f * d2;
     float b[6] = {ny1, nx1, nz1, ny1 + h2, nx1 + w2, nz1 + d2};
     const float lo[6] = {H, W, D, H, W, D};

@@ -365,16 +365,33 @@ __global__ void score_keys_kernel(const float* __restrict__ probs, int64_t A,
 
 struct Std6 { float v[6]; };
 
-// core/models.py:391-447 with apply_box_deltas_graph (280-337).
+// exp of a float32 through float64: (float)exp((double)x).  The oracle
+// (oracle/ops_ref.py) computes the same expression with numpy's float64 exp, so
+// the decoded boxes -- and the NMS keep set on them -- agree bit for bit (the
+// two double exps differ at most in the last double bit, which changes the
+// float rounding only within 2^-29 of a float tie).
+__device__ __forceinline__ float exp_via_f64(float x) { return (float)exp((double)x); }
+
+// core/models.py:391-447 with apply_box_deltas_graph (280-337).  order[j] must
+// be < A (the anchor rows): an index outside [0, A) is never read; its row is
+// written as a zero box with score -FLT_MAX (NMS never selects it) and *err is
+// set to 1 for the caller's next synchronisation point.
 __global__ void proposal_decode_kernel(const float* __restrict__ probs,
                                        const float* __restrict__ deltas,
-                                       const float* __restrict__ anchors,
+                                       const float* __restrict__ anchors, int64_t A,
                                        const int64_t* __restrict__ order, int64_t k, Std6 sd,
                                        float image_depth, float* __restrict__ boxes,
-                                       float* __restrict__ scores) {
+                                       float* __restrict__ scores, int32_t* __restrict__ err) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= k) return;
     const int64_t a = order[j];
+    if (a < 0 || a >= A) {
+        scores[j] = -3.402823466e38f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) boxes[j * 6 + q] = 0.0f;
+        if (err) *err = 1;
+        return;
+    }
     scores[j] = probs[a * 2 + 1];
     float d[6], an[6];
 #pragma unroll
@@ -389,9 +406,9 @@ __global__ void proposal_decode_kernel(const float* __restrict__ probs,
     cy = cy + d[0] * height;
     cx = cx + d[1] * width;
     cz = cz + d[2] * depth;
-    height = height * expf(d[3]);
-    width = width * expf(d[4]);
-    depth = depth * expf(d[5]);
+    height = height * exp_via_f64(d[3]);
+    width = width * exp_via_f64(d[4]);
+    depth = depth * exp_via_f64(d[5]);
     const float y1 = cy - 0.5f * height, x1 = cx - 0.5f * width, z1 = cz - 0.5f * depth;
     float r[6] = {y1, x1, z1, y1 + height, x1 + width, z1 + depth};
 #pragma unroll
@@ -526,15 +543,19 @@ extern "C" int m3d_score_keys_mapped(const float* probs, int64_t A, const int64_
 }
 
 extern "C" int m3d_proposal_decode(const float* probs, const float* deltas, const float* anchors,
-                                   const int64_t* order, int64_t k, const float std_dev[6],
-                                   float image_depth, float* boxes, float* scores,
-                                   m3d_stream_t s) {
+                                   int64_t n_anchors, const int64_t* order, int64_t k,
+                                   const float std_dev[6], float image_depth, float* boxes,
+                                   float* scores, int32_t* err, m3d_stream_t s) {
     if (k < 0) return einval("proposal_decode: negative proposal count");
+    if (n_anchors < 0) return einval("proposal_decode: negative anchor count");
+    if (k > n_anchors) return einval("proposal_decode: more proposals than anchors");
     if (k == 0) return M3D_OK;
+    if (!probs || !deltas || !anchors || !order || !boxes || !scores || !std_dev)
+        return einval("proposal_decode: null pointer");
     Std6 sd;
     for (int q = 0; q < 6; ++q) sd.v[q] = std_dev[q];
     hipLaunchKernelGGL(proposal_decode_kernel, dim3(grid_for(k, 256)), dim3(256), 0, st(s), probs,
-                       deltas, anchors, order, k, sd, image_depth, boxes, scores);
+                       deltas, anchors, n_anchors, order, k, sd, image_depth, boxes, scores, err);
     return check_launch("proposal_decode_kernel");
 }
 

@@ -49,7 +49,7 @@ _SIGS = {
     "m3d_nms3d": [c_p, c_p, c_i64, c_i32, c_f, c_i32, c_p, c_p, c_p, c_sz, c_p],
     "m3d_score_keys": [c_p, c_i64, c_p, c_p],
     "m3d_score_keys_mapped": [c_p, c_i64, c_p, c_p, c_p],
-    "m3d_proposal_decode": [c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_p, c_p, c_p],
+    "m3d_proposal_decode": [c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
     "m3d_proposal_gather": [c_p, c_p, c_p, c_i32, c_p, c_p],
     "m3d_conv3d_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_i32, c_i64,
                        c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p,

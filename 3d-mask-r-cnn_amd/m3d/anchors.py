@@ -95,6 +95,66 @@ def generate_pyramid_anchors(scales, ratios, feature_shapes, feature_strides, an
     return np.concatenate(out, axis=0)
 
 
+FEATURE_STRIDES_YX = (4, 8, 16, 32, 64)   # P2..P6 of resnet_graph + FPN (strides (2,2,1), P6 subsample)
+
+
+def patch_backbone_strides(config):
+    """RPN.train's stride patch (core/models.py:3408-3419): every
+    BACKBONE_STRIDES entry becomes (sy, sx, 1), because the network never
+    strides depth (resnet_graph strides (2,2,1), core/models.py:242-267; FPN
+    upsample (2,2,1), 3193; P6 = subsample (2,2,1), 3211).  The reference
+    applies it only in RPN.train, after build() made the anchors (3225), so a
+    preset with z-strides != 1 (core/config.py:40, configs/rpn/scp_rpn_hela.json)
+    builds anchors that disagree with its own RPN head rows (SURVEY.md App.
+    B.2).  Here it is applied before the anchors are made; returns True when
+    the config changed (ANCHOR_NB is re-derived, core/config.py:235-241)."""
+    fixed = []
+    for s in config.BACKBONE_STRIDES:
+        if isinstance(s, (tuple, list, np.ndarray)):
+            fixed.append((int(s[0]), int(s[1]), 1))
+        else:
+            fixed.append((int(s), int(s), 1))
+    old = [tuple(int(v) for v in s) if isinstance(s, (tuple, list, np.ndarray)) else (int(s),) * 3
+           for s in config.BACKBONE_STRIDES]
+    config.BACKBONE_STRIDES = fixed
+    if hasattr(config, "IMAGE_SHAPE") and hasattr(config, "ANCHOR_NB"):
+        H, W, D = (int(v) for v in config.IMAGE_SHAPE[:3])
+        config.ANCHOR_NB = int(sum((H / sy) * (W / sx) * (D / sz) for sy, sx, sz in fixed[:5]))
+    return fixed != old
+
+
+def rpn_row_count(config, image_shape=None):
+    """Rows of the shared RPN head's concatenated outputs (core/models.py:
+    3250-3263): P2..P6 are (ceil(H/s), ceil(W/s), D) for s = 4..64 and the head
+    emits len(RPN_ANCHOR_RATIOS) anchors per location (build_rpn_model,
+    core/models.py:3244-3248)."""
+    image_shape = config.IMAGE_SHAPE if image_shape is None else image_shape
+    H, W, D = (int(v) for v in image_shape[:3])
+    apl = len(config.RPN_ANCHOR_RATIOS)
+    return int(sum(-(-H // s) * -(-W // s) * D * apl for s in FEATURE_STRIDES_YX))
+
+
+def model_anchors(config, image_shape=None):
+    """The anchors a model built from ``config`` uses: the z-stride patch
+    (patch_backbone_strides), then RPN.get_anchors, checked against the RPN
+    head's row count.  Raises ValueError when the preset cannot give one anchor
+    per RPN row (y/x strides other than 4..64, several scales per level), where
+    the reference would gather past its anchor constant."""
+    import warnings
+    if patch_backbone_strides(config):
+        warnings.warn("BACKBONE_STRIDES z-components set to 1 as RPN.train does "
+                      "(core/models.py:3408-3419): the network never strides depth", stacklevel=3)
+    a = get_anchors(config, image_shape)
+    rows = rpn_row_count(config, image_shape)
+    if a.shape[0] != rows:
+        raise ValueError(
+            f"anchor count {a.shape[0]} != RPN head rows {rows}: BACKBONE_STRIDES {config.BACKBONE_STRIDES} "
+            f"and {len(config.RPN_ANCHOR_SCALES)} RPN_ANCHOR_SCALES x {len(config.RPN_ANCHOR_RATIOS)} ratios "
+            f"do not give one anchor per (y, x, z, ratio) of P2..P6 (y/x strides must be {FEATURE_STRIDES_YX}, "
+            f"one scale per level; SURVEY.md App. B.2)")
+    return a
+
+
 def get_anchors(config, image_shape=None):
     """RPN.get_anchors: normalised float32 anchors [A,6] (core/models.py:3475-3528)."""
     image_shape = config.IMAGE_SHAPE if image_shape is None else image_shape

@@ -31,7 +31,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import check, ptr, stream
-from .anchors import get_anchors
+from .anchors import model_anchors
 from .backbone import FPN, ResNet3D, RPNHead
 from .layers import ProposalLayer, PyramidROIAlign
 from .nn import conv_bn_act, conv_geom
@@ -236,6 +236,7 @@ class MaskRCNN:
     mrcnn_bbox, mrcnn_mask [B,max_inst,2M,2M,2M,C], rpn_rois."""
 
     def __init__(self, config, device="cuda", seed=1):
+        anchors = model_anchors(config)          # z-stride patch + row-count check (m3d.anchors)
         _lib.load()
         self.config = c = config
         self.device = torch.device(device)
@@ -248,7 +249,7 @@ class MaskRCNN:
         self.classifier = ClassifierHead(self.store, c.POOL_SIZE, c.NUM_CLASSES, fc, c.TOP_DOWN_PYRAMID_SIZE)
         self.mask_head = MaskHead(self.store, c.NUM_CLASSES, mask_ch, c.TOP_DOWN_PYRAMID_SIZE)
         self.store.finalize(self.device, seed=seed)
-        self.anchors = torch.from_numpy(get_anchors(c)).to(self.device)[None]
+        self.anchors = torch.from_numpy(anchors).to(self.device)[None]
         self.proposal_layer = ProposalLayer(
             proposal_count=c.POST_NMS_ROIS_INFERENCE, nms_threshold=c.RPN_NMS_THRESHOLD,
             pre_nms_limit=c.PRE_NMS_LIMIT, images_per_gpu=c.IMAGES_PER_GPU,

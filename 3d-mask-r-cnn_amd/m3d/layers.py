@@ -29,7 +29,13 @@ class ProposalLayer:
     def __call__(self, inputs, return_counts=False):
         probs, deltas, anchors = inputs
         B, A = probs.shape[:2]
-        k = min(self.pre_nms_limit, anchors.shape[1])
+        if anchors.shape[1] != A or deltas.shape[1] != A:
+            # the reference would gather past its anchor constant
+            raise ValueError(f"ProposalLayer: {anchors.shape[1]} anchors, {deltas.shape[1]} deltas rows "
+                             f"and {A} rpn_class rows must be equal")
+        if anchors.shape[0] not in (1, B):
+            raise ValueError("ProposalLayer: anchors batch must be 1 or IMAGES_PER_GPU")
+        k = min(self.pre_nms_limit, A)
         out = torch.empty((B, self.proposal_count, 6), device=probs.device, dtype=torch.float32)
         counts = []
         with torch.no_grad():
@@ -39,7 +45,7 @@ class ProposalLayer:
                 ab = anchors[b if anchors.shape[0] > 1 else 0].detach().float().contiguous()
                 order = ops.topk_order(pb, k)
                 boxes, scores = ops.proposal_decode(pb, db, ab, order, self.rpn_bbox_std_dev,
-                                                    self.image_depth)
+                                                    self.image_depth, check_indices=False)
                 keep, num = ops.non_max_suppression_3d_padded(boxes, scores, self.proposal_count,
                                                               self.nms_threshold)
                 out[b] = ops.proposal_gather(boxes, keep, num, self.proposal_count)
@@ -81,7 +87,7 @@ class ProposalLayer:
             sel_a = anchors[0].detach().float().index_select(0, gidx).contiguous()
             order = torch.arange(k, device=pb.device, dtype=torch.int64)
             boxes, scores = ops.proposal_decode(sel_p, sel_d, sel_a, order, self.rpn_bbox_std_dev,
-                                                self.image_depth)
+                                                self.image_depth, check_indices=False)
             keep, num = ops.non_max_suppression_3d_padded(boxes, scores, self.proposal_count,
                                                           self.nms_threshold)
             return ops.proposal_gather(boxes, keep, num, self.proposal_count)[None]

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .anchors import get_anchors
+from .anchors import model_anchors
 from .backbone import FPN, ResNet3D, RPNHead
 from .layers import ProposalLayer
 from .optim import KerasOptimizer
@@ -207,10 +207,15 @@ class _RPNLossFused(torch.autograd.Function):
         return total, lc, lb
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g_total, _g_lc, _g_lb):
         g_logits, g_bbox, scales, A = ctx.saved
         if g_total is None:
             return (None,) * 11
+        if g_logits is None:
+            raise RuntimeError("rpn loss: backward called twice on one forward (the kept per-anchor "
+                               "gradients were scaled in place by the first call)")
+        ctx.saved = (None, None, scales, A)
         g_total = g_total.contiguous().to(torch.float32)
         _lib.check(_lib.load().m3d_rpn_loss_bwd(_lib.ptr(g_logits), _lib.ptr(g_bbox), A, _lib.ptr(g_total),
                              _lib.ptr(scales), _lib.stream()), "m3d_rpn_loss_bwd")
@@ -247,6 +252,7 @@ class RPN:
         h, w = int(config.IMAGE_SHAPE[0]), int(config.IMAGE_SHAPE[1])
         if h % 64 or w % 64:
             raise ValueError("IMAGE_SHAPE height & width must be multiples of 64")
+        anchors = model_anchors(config)          # z-stride patch + row-count check, before any device work
         _lib.load()
         self.config = config
         self.device = torch.device(device)
@@ -256,7 +262,7 @@ class RPN:
         self.rpn = RPNHead(self.store, config.RPN_ANCHOR_STRIDE, len(config.RPN_ANCHOR_RATIOS),
                            config.TOP_DOWN_PYRAMID_SIZE, backbone=self.backbone)
         self.store.finalize(self.device, seed=seed, weight_decay=float(config.WEIGHT_DECAY))
-        self.anchors = torch.from_numpy(get_anchors(config)).to(self.device)[None]
+        self.anchors = torch.from_numpy(anchors).to(self.device)[None]
         self.proposal_layer = ProposalLayer(
             proposal_count=config.POST_NMS_ROIS_TRAINING, nms_threshold=config.RPN_NMS_THRESHOLD,
             pre_nms_limit=config.PRE_NMS_LIMIT, images_per_gpu=config.IMAGES_PER_GPU,

@@ -75,6 +75,10 @@ _THROTTLE = {}
 def _throttle(key, side):
     if WGRAD_THROTTLE <= 0:
         return
+    if torch.cuda.is_current_stream_capturing():
+        # a host wait on a stream under graph capture is illegal (it would
+        # invalidate the capture); a replayed graph allocates nothing anyway
+        return
     st = _THROTTLE.setdefault(key, {"total": torch.cuda.get_device_properties(key).total_memory, "n": 0})
     st["n"] += 1
     if st["n"] % max(1, WGRAD_THROTTLE_EVERY) == 0 and \
@@ -84,7 +88,12 @@ def _throttle(key, side):
 
 # Fork / join events of the weight-gradient stream (m3d_stream_fork): "2" no
 # system-scope fence (default; both streams are on one device, agent scope is
-# all the consumer needs), "1" device-scope release, "0" plain event, "torch":
+# all the consumer needs: on gfx950 an agent-scope release writes back every
+# XCD's L2 to the device-coherent level, and each kernel's completion signal
+# carries its own agent-scope release, so the consumer's acquire sees the
+# producer's stores -- the system-scope part only adds visibility to the host
+# and peer devices, which no consumer of these events needs), "1" device-scope
+# release, "0" plain event, "torch":
 # Stream.wait_stream.  The fork showed as a ~7.5 us compute-queue bubble per
 # layer in the 128^3 kernel trace; A/B (scripts/gpu_r03x.sh, same box): mode 2
 # 29.80 / 29.90 ms per step, torch / 0 / 1 30.05-30.10 ms.

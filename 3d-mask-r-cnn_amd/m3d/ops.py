@@ -298,14 +298,31 @@ def score_keys(probs, global_index=None):
     return keys
 
 
-def proposal_decode(probs, deltas, anchors, order, std_dev, image_depth):
+def proposal_decode(probs, deltas, anchors, order, std_dev, image_depth, check_indices=True):
+    """Top-k gather + apply_box_deltas_graph + clips + min sizes
+    (core/models.py:391-447) for one image: probs [A,2], deltas [A,6], anchors
+    [A,6], order [k] int64 anchor indices.  An order index outside [0, A) is
+    the reference's tf.gather InvalidArgument: the kernel never reads it and
+    raises a device flag; with check_indices (default) the flag is read back
+    here (one sync) and ValueError raised.  ProposalLayer passes False: its
+    order comes from top-k over the same A rows, checked on the host."""
+    A = anchors.shape[0]
+    if probs.shape[0] != A or deltas.shape[0] != A:
+        raise ValueError(f"proposal_decode: probs {tuple(probs.shape)} / deltas {tuple(deltas.shape)} "
+                         f"rows differ from the {A} anchors")
     k = order.shape[0]
+    if k > A:
+        raise ValueError(f"proposal_decode: {k} indices for {A} anchors")
     boxes = torch.empty((k, 6), device=probs.device, dtype=torch.float32)
     scores = torch.empty((k,), device=probs.device, dtype=torch.float32)
+    err = torch.zeros((1,), device=probs.device, dtype=torch.int32) if check_indices else None
     sd = (_lib.c_f * 6)(*[float(torch.tensor(v, dtype=torch.float32)) for v in std_dev])
-    check(_L().m3d_proposal_decode(ptr(probs), ptr(deltas), ptr(anchors), ptr(order), k, sd,
-                                   float(image_depth), ptr(boxes), ptr(scores), stream()),
+    check(_L().m3d_proposal_decode(ptr(probs), ptr(deltas), ptr(anchors), A, ptr(order), k, sd,
+                                   float(image_depth), ptr(boxes), ptr(scores), ptr(err), stream()),
           "proposal_decode")
+    if err is not None and int(err.item()) != 0:
+        raise ValueError(f"indices[...] is not in [0, {A}): a top-k index names no anchor "
+                         "(GatherV2 InvalidArgument in the reference graph)")
     return boxes, scores
 
 

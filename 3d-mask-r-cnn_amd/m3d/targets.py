@@ -149,7 +149,11 @@ class RPNTargetBuilder:
     so no list can be truncated.  With a smaller explicit cap, each call queues
     a copy of its flag to pinned host memory, and the next call (or
     ``check()``, which waits for it) raises RuntimeError when it was set --
-    truncated lists would label from an atomic-order-dependent subset."""
+    truncated lists would label from an atomic-order-dependent subset.
+    The error therefore arrives ONE STEP LATE by default: the training step
+    that used the truncated targets has already run.  A caller that must not
+    apply such a step calls ``check()`` at a sync point it already has in the
+    same step (e.g. where it reads the loss back) before the optimizer."""
 
     def __init__(self, anchors, config, max_gt=64, list_cap=None):
         ops._dev(anchors)

@@ -167,7 +167,13 @@ int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int32_t max_ou
  *   (score desc, lower index first) for scores = probs[:, :, 1].
  * m3d_proposal_decode: gather the top-k anchors/deltas, de-normalise by
  *   rpn_bbox_std_dev, clip +-3, apply_box_deltas_graph, clip to [0,1], enforce
- *   min sizes.  order[k] are int64 anchor indices.
+ *   min sizes.  order[k] are int64 anchor indices into anchors [n_anchors,6]
+ *   (and probs [n_anchors,2], deltas [n_anchors,6]); k > n_anchors is
+ *   M3D_EINVAL.  An index outside [0, n_anchors) is never read: its row gets a
+ *   zero box and score -FLT_MAX (never selected by NMS) and the DEVICE int32
+ *   *err (may be NULL; the caller zeroes it) is set to 1, checked by the caller
+ *   at its next synchronisation (the reference's tf.gather InvalidArgument).
+ *   exp is evaluated as (float)exp((double)x).  ABI 2 added n_anchors / err.
  * m3d_proposal_gather: proposals[P,6] = boxes[keep[i]] for i < *num_keep,
  *   zero rows after (core/models.py:476-485).
  * ------------------------------------------------------------------------- */
@@ -178,9 +184,9 @@ int m3d_score_keys(const float* probs /*[A,2]*/, int64_t A, int64_t* keys, m3d_s
 int m3d_score_keys_mapped(const float* probs, int64_t A, const int64_t* gidx, int64_t* keys,
                           m3d_stream_t s);
 int m3d_proposal_decode(const float* probs, const float* deltas, const float* anchors,
-                        const int64_t* order, int64_t k, const float std_dev[6],
+                        int64_t n_anchors, const int64_t* order, int64_t k, const float std_dev[6],
                         float image_depth, float* boxes /*[k,6]*/, float* scores /*[k]*/,
-                        m3d_stream_t s);
+                        int32_t* err /*device, nullable*/, m3d_stream_t s);
 int m3d_proposal_gather(const float* boxes, const int32_t* keep, const int32_t* num_keep,
                         int32_t P, float* proposals, m3d_stream_t s);
 

@@ -26,6 +26,11 @@ from . import ops_ref as R
 from .model_ref import batchnorm, conv3d
 
 
+def _exp32(x):
+    """(float)exp((double)x): float64 exp rounded to float32, the kernels' form."""
+    return np.exp(np.asarray(x, np.float64)).astype(np.float32)
+
+
 def _t(p, k, dtype):
     return torch.as_tensor(np.asarray(p[k])).to(dtype)
 
@@ -108,10 +113,10 @@ def refine_detections(rois, probs, deltas, image_meta, bbox_std_dev, min_conf, n
     dy, dx, dz, dh, dw, dd = (d[:, q] for q in range(6))
     h, w, dep = y2 - y1, x2 - x1, z2 - z1
     cy, cx, cz = y1 + f(0.5) * h, x1 + f(0.5) * w, z1 + f(0.5) * dep
-    lim = np.log(f(1000.0 / 16.0))
+    lim = f(np.log(1000.0 / 16.0))          # float64 log rounded to float32 (= the kernel's)
     dh, dw, dd = (np.minimum(np.maximum(v, -lim), lim) for v in (dh, dw, dd))
     cy2, cx2, cz2 = cy + dy * h, cx + dx * w, cz + dz * dep
-    h2, w2, d2 = h * np.exp(dh), w * np.exp(dw), dep * np.exp(dd)
+    h2, w2, d2 = (v * _exp32(e) for v, e in ((h, dh), (w, dw), (dep, dd)))
     ny1, nx1, nz1 = cy2 - f(0.5) * h2, cx2 - f(0.5) * w2, cz2 - f(0.5) * d2
     b = np.stack([ny1, nx1, nz1, ny1 + h2, nx1 + w2, nz1 + d2], 1).astype(f)
     hi = np.array([H, W, D, H, W, D], f)

@@ -163,9 +163,10 @@ def apply_box_deltas(boxes, deltas):
     cy = cy + deltas[:, 0] * height
     cx = cx + deltas[:, 1] * width
     cz = cz + deltas[:, 2] * depth
-    height = height * np.exp(deltas[:, 3])
-    width = width * np.exp(deltas[:, 4])
-    depth = depth * np.exp(deltas[:, 5])
+    # exp in float64 rounded to float32: csrc/nms3d.hip computes (float)exp((double)d)
+    height = height * np.exp(deltas[:, 3].astype(np.float64)).astype(f)
+    width = width * np.exp(deltas[:, 4].astype(np.float64)).astype(f)
+    depth = depth * np.exp(deltas[:, 5].astype(np.float64)).astype(f)
     y1 = cy - f(0.5) * height
     x1 = cx - f(0.5) * width
     z1 = cz - f(0.5) * depth

@@ -36,7 +36,7 @@ int main() {
     const int64_t fshape[4][3] = {{8, 8, 8}, {4, 4, 8}, {2, 2, 8}, {1, 1, 8}};
     const int64_t bad_fshape[4][3] = {{8, 8, 8}, {0, 4, 8}, {2, 2, 8}, {1, 1, 8}};
 
-    if (m3d_abi_version() != 1) { std::printf("FAIL abi version\n"); return 1; }
+    if (m3d_abi_version() != 2) { std::printf("FAIL abi version\n"); return 1; }
 
     // CropAndResize3D family (wheel ops)
     EXPECT_EINVAL(m3d_crop_and_resize3d_fwd(nf, 1, 4, 4, 4, 1, nf, ni, 1, 0, 2, 2, 0, 0.f, of, s));
@@ -60,7 +60,9 @@ int main() {
     EXPECT_EINVAL(m3d_nms3d(nf, nf, 100, 5, 0.5f, 0, oi, oi, nullptr, 8, s));   // workspace too small
     EXPECT_EINVAL(m3d_score_keys(nf, -3, nullptr, s));
     EXPECT_EINVAL(m3d_score_keys_mapped(nf, -3, nullptr, nullptr, s));
-    EXPECT_EINVAL(m3d_proposal_decode(nf, nf, nf, nullptr, -1, sd, 8.f, of, of, s));
+    EXPECT_EINVAL(m3d_proposal_decode(nf, nf, nf, 10, nullptr, -1, sd, 8.f, of, of, nullptr, s));
+    EXPECT_EINVAL(m3d_proposal_decode(nf, nf, nf, -1, nullptr, 0, sd, 8.f, of, of, nullptr, s));
+    EXPECT_EINVAL(m3d_proposal_decode(nf, nf, nf, 4, nullptr, 5, sd, 8.f, of, of, nullptr, s));
     EXPECT_EINVAL(m3d_proposal_gather(nf, ni, ni, -1, of, s));
 
     // convolutions

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 def test_error_string_and_version():
     import m3d._lib as lib
     L = lib.load()
-    assert L.m3d_abi_version() == 1
+    assert L.m3d_abi_version() == 2
     assert isinstance(L.m3d_last_error(), bytes)
 
 

@@ -143,3 +143,45 @@ def test_graphed_step_matches_eager(cuda):
     (l0, rois0, w0), (l1, rois1, w1) = res
     assert abs(l0 - l1) <= 1e-5 * abs(l0)
     assert float((w0 - w1).abs().max()) <= 1e-5 * float(w0.abs().max())
+
+
+def test_graphed_step_with_throttle_forced(cuda, monkeypatch):
+    """The side-stream throttle (m3d.nn._throttle) must not synchronise a stream
+    under graph capture: with M3D_WGRAD_THROTTLE forced so its host
+    wait would fire at every weight gradient, the graphed step still captures
+    and replays, and its loss matches the eager step's within the atomics' order."""
+    import m3d.nn as mnn
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
+    monkeypatch.setattr(mnn, "WGRAD_THROTTLE", 1e-12)
+    monkeypatch.setattr(mnn, "WGRAD_THROTTLE_EVERY", 1)
+    cfg = synthetic_rpn_config(64, depth=16, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=500)
+    image = synthetic_volume(64, 16, seed=0).to(cuda)
+    losses = []
+    for graphed in (False, True):
+        model = RPN(cfg, device=cuda, seed=5)
+        match, bbox = synthetic_rpn_targets(model.anchors.shape[1], 256, seed=2)
+        targets = RPNTargets(match, bbox, cuda)
+        if graphed:
+            step = model.graphed_train_step(image, targets, proposals=True, warmup=2)
+            r = step()
+        else:
+            for _ in range(3):
+                r = model.train_step(image, targets, proposals=True)
+        torch.cuda.synchronize()
+        losses.append(float(r["loss"]))
+    assert abs(losses[0] - losses[1]) <= 1e-5 * abs(losses[0]), losses
+
+
+def test_rpn_loss_double_backward_raises(cuda):
+    """The fused loss scales its kept gradients in place: a second backward
+    through the same forward raises instead of returning rescaled gradients."""
+    from m3d.model import RPNTargets, rpn_losses, synthetic_rpn_targets
+    A = 4096
+    logits = torch.randn((1, A, 2), device=cuda, requires_grad=True)
+    bbox = torch.randn((1, A, 6), device=cuda, requires_grad=True)
+    match, gt = synthetic_rpn_targets(A, 256, seed=1)
+    total, _, _ = rpn_losses(RPNTargets(match, gt, cuda), logits, bbox)
+    total.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="backward called twice"):
+        total.backward()
