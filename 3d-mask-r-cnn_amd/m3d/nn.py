@@ -152,16 +152,29 @@ def _span():
     return e
 
 
-def _log(kind, direct_flops, exec_flops, nbytes, phase="fwd", name="", t0=None):
+def _log(kind, direct_flops, exec_flops, nbytes, phase="fwd", name="", t0=None, engine="f32"):
     """Append (kind, direct_flops, executed_flops, compulsory_bytes, phase, name,
-    start_event, end_event) to LAYER_LOG; the end event is recorded on the
-    current stream right after the group's launches (both None when not timing)."""
+    start_event, end_event, engine) to LAYER_LOG; the end event is recorded on
+    the current stream right after the group's launches (both None when not
+    timing).  engine: the MFMA form the group's GEMM ran on -- "x3" (fp32 as six
+    bf16 MFMAs on the exact split: ceiling bf16 peak / 6) or "f32"
+    (v_mfma_f32_32x32x2_f32) -- so the step roofline prices it at the ceiling of
+    the kernel that ran it."""
     if LAYER_LOG is not None:
         t1 = None
         if t0 is not None:
             t1 = torch.cuda.Event(enable_timing=True)
             t1.record()
-        LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes), phase, name, t0, t1))
+        LAYER_LOG.append((kind, float(direct_flops), float(exec_flops), float(nbytes), phase, name, t0, t1,
+                          engine))
+
+
+def _wgrad1_x3(geo, cin, cout, in_sp):
+    """Does m3d_conv3d_bwd_weight run this conv's weight gradient on the x3
+    GEMM?  (1x1x1 stride-1 convs with Cin % 4 == 0 and Cout >= 65:
+    csrc/conv3d.hip, m3d_conv3d_bwd_weight.)"""
+    return (geo.k == (1, 1, 1) and geo.stride == (1, 1, 1) and geo.pad == (0, 0, 0)
+            and tuple(geo.out) == tuple(in_sp) and cin % 4 == 0 and cout >= 65)
 
 
 def _wino_exec(B, OH, OW, OD, cin, cout, nz):
@@ -540,7 +553,8 @@ class _ConvBNAct(torch.autograd.Function):
             if ctx.wino:
                 exe = _wino_exec(B, OH, OW, OD, Cin, Cout, int(_L().m3d_conv3d_wino_tile_z()))
             nb = 4.0 * (x.numel() + w.numel() + y.numel() + (residual.numel() if residual is not None else 0))
-            _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb, "fwd", name, t0)
+            x3 = ctx.wino or (res_mode <= 2 and halo is None and _conv1_x3(x.shape, geo, Cin, Cout))
+            _log("wino" if ctx.wino else f"conv{kh}", direct, exe, nb, "fwd", name, t0, "x3" if x3 else "f32")
         ctx.save_for_backward(x, w, y, z)
         ctx.wshare = wshare
         if wshare is not None and ctx.wino and halo is None and need_dx:
@@ -630,7 +644,7 @@ class _ConvBNAct(torch.autograd.Function):
                         exe = direct if min(Cin, Cout) < WINO_WGRAD_MIN_C else \
                             _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_wgrad_tile_z()))
                         _log("wino_wgrad", direct, exe, 4.0 * (x.numel() + dz.numel() + w.numel()),
-                             "bwd_weight", ctx.name, tw)
+                             "bwd_weight", ctx.name, tw, "f32" if min(Cin, Cout) < WINO_WGRAD_MIN_C else "x3")
                 ctx.u = None
             td = _span()
             ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
@@ -655,7 +669,7 @@ class _ConvBNAct(torch.autograd.Function):
                     _shared_wino_release(ctx.wshare)
                 if logging:
                     _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_tile_z())),
-                         4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)), "bwd_data", ctx.name, td)
+                         4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)), "bwd_data", ctx.name, td, "x3")
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             ctx.halo = None
@@ -677,7 +691,8 @@ class _ConvBNAct(torch.autograd.Function):
                                                   stream()), "conv3d_bwd_weight")
                 if logging:
                     _log(f"conv{kh}_wgrad", direct, direct, 4.0 * (x.numel() + dz.numel() + w.numel()),
-                         "bwd_weight", ctx.name, tw)
+                         "bwd_weight", ctx.name, tw,
+                         "x3" if halo is None and _wgrad1_x3(geo, Cin, Cout, (H, W, D)) else "f32")
         dx = None
         link = ctx.link
         acc = 0
@@ -695,7 +710,8 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
-            if cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin):
+            dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin)
+            if dx_x3:
                 planes = _x3_planes(w, Cin, Cout, False)
                 check(L.m3d_conv3d_bwd_data_x3(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), stream()),
                       "conv3d_bwd_data_x3")
@@ -710,7 +726,7 @@ class _ConvBNAct(torch.autograd.Function):
                       "conv3d_bwd_data")
             if logging:
                 _log(f"conv{kh}_dgrad", direct, direct, 4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)),
-                     "bwd_data", ctx.name, td)
+                     "bwd_data", ctx.name, td, "x3" if dx_x3 else "f32")
             dx = _link_park(link, dx, acc)
         _grad_done(grads, side)
         dr = None

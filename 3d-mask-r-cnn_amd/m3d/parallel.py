@@ -19,23 +19,68 @@ import torch.distributed as dist
 BUCKET_FLOATS = 16 * 1024 * 1024        # 64 MiB per all-reduce
 
 
-def init_from_env(backend=None):
-    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...)."""
+def init_from_env(backend=None, timeout_s=None):
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...).
+    Collectives time out after ``timeout_s`` (M3D_DIST_TIMEOUT, default 600 s),
+    so a deadlocked halo exchange or all-reduce ends the process with an error
+    instead of hanging the node."""
+    import datetime
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1:
         return 0, 1
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
+        to = datetime.timedelta(seconds=float(timeout_s or os.environ.get("M3D_DIST_TIMEOUT", "600")))
         if backend == "nccl":
             # bind this rank to its GPU before the communicator exists (eager
             # RCCL init on that device; barriers need not guess the device)
             local = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
             torch.cuda.set_device(local)
-            dist.init_process_group(backend=backend, device_id=local)
+            dist.init_process_group(backend=backend, device_id=local, timeout=to)
         else:
-            dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend, timeout=to)
     return dist.get_rank(), dist.get_world_size()
+
+
+# ---------------------------------------------------------------------------
+# self-validation of a multi-rank run (bench.py N > 1)
+# ---------------------------------------------------------------------------
+def tensor_digest(t: torch.Tensor) -> torch.Tensor:
+    """Bit-level digest of a tensor: int64 [3] = (element count, sum of its
+    32-bit words, sum of word * (i mod 65521 + 1)) -- equal digests for
+    bit-identical tensors; any single changed word changes both sums."""
+    w = t.detach().contiguous().reshape(-1)
+    if w.element_size() == 4:
+        w = w.view(torch.int32)
+    w = w.to(torch.int64)
+    idx = (torch.arange(w.numel(), device=w.device, dtype=torch.int64) % 65521) + 1
+    return torch.stack([torch.tensor(w.numel(), device=w.device, dtype=torch.int64), w.sum(), (w * idx).sum()])
+
+
+def ranks_identical(tensors: dict, group=None) -> dict:
+    """For each named tensor: is it bit-identical on every rank of ``group``?
+    One all_gather of the digests (works on gloo and RCCL)."""
+    names = sorted(tensors)
+    if not names:
+        return {}
+    d = torch.stack([tensor_digest(tensors[n]) for n in names])
+    world = dist.get_world_size(group)
+    out = [torch.empty_like(d) for _ in range(world)]
+    dist.all_gather(out, d, group=group)
+    return {n: bool(all(torch.equal(o[i], out[0][i]) for o in out)) for i, n in enumerate(names)}
+
+
+def validate_replicas(named: dict, group=None) -> dict:
+    """{"ok", "identical": {name: bool}}: the replicated state of a multi-rank
+    step (weights after the all-reduce + optimizer; the merged proposals and
+    the all-reduced loss of a depth-slab step) must agree bit for bit."""
+    same = ranks_identical(named, group)
+    return {"ok": all(same.values()), "identical": same}
+
+
+def rel_close(a: float, b: float, rtol: float) -> bool:
+    return abs(a - b) <= rtol * max(abs(a), abs(b), 1e-30)
 
 
 def allreduce_mean_(flat: torch.Tensor, world: int, bucket=BUCKET_FLOATS):

@@ -501,7 +501,12 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     sg = slab.SlabGroup(S, rank, world)
     match, bbox = synthetic_rpn_targets(model.anchors.shape[1], cfg.RPN_TRAIN_ANCHORS_PER_IMAGE, seed=2)
     srpn = SlabRPN(model, sg, match, bbox)
-    image = srpn.slice(synthetic_volume(S, seed=100)).to(dev)
+    vol = synthetic_volume(S, seed=100)
+    image = srpn.slice(vol).to(dev)
+    validation = None
+    if world > 1:
+        validation = validate_slab(srpn, image, vol, cfg, match, bbox, rank, dev, proposals)
+    del vol
     for _ in range(warmup):
         r = srpn.train_step(image, proposals=proposals)
     torch.cuda.synchronize()
@@ -525,6 +530,13 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
            "volumes_per_s": round(steps / el, 4), "scaling": "strong",
            "loss": round(float(r["loss"]), 6),
            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    if validation is not None:
+        from m3d.parallel import validate_replicas
+        after = validate_replicas({"weights": model.store.flat})
+        validation["weights_after_steps_identical"] = after["ok"]
+        validation["ok"] = bool(validation["ok"] and after["ok"])
+        out["validation"] = validation
+        log(f"[bench] depth_slab validation: {json.dumps(validation)}")
     if world == 1:
         try:
             out["step_roofline"] = step_roofline(model, lambda: srpn.train_step(image, proposals=proposals),
@@ -538,7 +550,70 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     return out
 
 
+def validate_slab(srpn, image, vol, cfg, match, bbox, rank, dev, proposals):
+    """First multi-rank depth-slab step, checked before timing (nothing in it
+    is timed): one sharded forward + backward without the optimizer; every
+    rank must hold bit-identical merged proposals and all-reduced loss, and
+    rank 0 reruns the UNSHARDED forward + loss of the same volume on its GPU
+    (the N = 1 path): the proposals must be bit-identical (the slab forward is
+    exact: same Winograd tiles, halo planes beside the slab) and the loss equal
+    within the fp32 summation-order tolerance 1e-5 (per-slab partial sums)."""
+    from m3d.model import RPN, RPNTargets
+    from m3d.parallel import rel_close, validate_replicas
+    r = srpn.train_step(image, proposals=proposals, apply=False)
+    torch.cuda.synchronize()
+    named = {"loss": r["loss"]}
+    if proposals:
+        named["rpn_rois"] = r["rpn_rois"]
+    v = validate_replicas(named)
+    v["loss"] = float(r["loss"])
+    if rank == 0:
+        ref = RPN(cfg, device=dev, seed=1)
+        with torch.no_grad():
+            o = ref.forward(vol.to(dev), proposals=proposals)
+            tot, _, _ = ref.loss_total(o, RPNTargets(match, bbox, dev))
+        v["loss_n1"] = float(tot)
+        v["loss_matches_n1"] = rel_close(v["loss"], v["loss_n1"], 1e-5)
+        if proposals:
+            v["rois_match_n1"] = bool(torch.equal(o["rpn_rois"], r["rpn_rois"]))
+        v["ok"] = bool(v["ok"] and v["loss_matches_n1"] and v.get("rois_match_n1", True))
+        del ref, o
+        torch.cuda.empty_cache()
+    flag = torch.tensor([1 if v["ok"] else 0], device=dev, dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    v["ok"] = bool(int(flag.item()))
+    return v
+
+
+def validate_dp(model, world):
+    """Data-parallel run (weak scaling): after the timed steps the weights --
+    each rank's own update from the averaged gradient -- must be bit-identical
+    on every rank."""
+    from m3d.parallel import validate_replicas
+    v = validate_replicas({"weights": model.store.flat, "sgd_moments": model.store.moments})
+    v["world"] = world
+    return v
+
+
 # ---------------------------------------------------------------- forward roofline
+def _peak_flops(engine):
+    """FLOP/s ceiling of the kernel that ran a logged launch group: the x3
+    kernels (fp32 as six bf16 MFMAs) at bf16 peak / 6, the rest at the f32 MFMA peak."""
+    return (X3_PEAK_TFLOPS if engine == "x3" else F32_MFMA_PEAK_TFLOPS) * 1e12
+
+
+def _roof_s(rec_row, f32_only=False):
+    eng = "f32" if f32_only else (rec_row[8] if len(rec_row) > 8 else "f32")
+    return max(rec_row[2] / _peak_flops(eng), rec_row[3] / (HBM_PEAK_GBS * 1e9))
+
+
+def _host_ahead(seconds=0.5):
+    """Let the host run ahead of the GPU before an instrumented pass: a spin
+    kernel on the current stream holds the GPU while the host enqueues the pass,
+    so the HIP events around each launch group time the GPU's work, not the
+    host's enqueue gaps (the brackets of a GPU waiting for the host measured
+    e.g. conv1 fwd 2.2 ms vs its 0.32 ms kernel)."""
+    torch.cuda._sleep(int(seconds * 2.0e9))
 def fwd_roofline(model, image, reps=3):
     """Per-stage forward roofline: every conv / pool of the
     backbone, FPN and RPN head is logged once (m3d.nn.LAYER_LOG) with its
@@ -559,7 +634,8 @@ def fwd_roofline(model, image, reps=3):
         rec, mnn.LAYER_LOG = mnn.LAYER_LOG, None
         with torch.no_grad():
             t = _event_time(fn, reps)
-        t_exec = sum(max(r_[2] / (F32_MFMA_PEAK_TFLOPS * 1e12), r_[3] / (HBM_PEAK_GBS * 1e9)) for r_ in rec)
+        t_exec = sum(_roof_s(r_) for r_ in rec)
+        t_exec32 = sum(_roof_s(r_, f32_only=True) for r_ in rec)
         t_dir = sum(max(r_[1] / (F32_MFMA_PEAK_TFLOPS * 1e12), r_[3] / (HBM_PEAK_GBS * 1e9)) for r_ in rec)
         nb = sum(r_[3] for r_ in rec)
         stages[name] = {"ms": round(t * 1e3, 3), "layers": len(rec),
@@ -567,6 +643,7 @@ def fwd_roofline(model, image, reps=3):
                         "executed_tflop": round(sum(r_[2] for r_ in rec) / 1e12, 4),
                         "compulsory_gb": round(nb / 1e9, 3),
                         "roofline_ms": round(t_exec * 1e3, 3), "frac_roofline": round(t_exec / t, 4),
+                        "frac_roofline_f32_priced": round(t_exec32 / t, 4),
                         "frac_roofline_direct_flops": round(t_dir / t, 4),
                         "hbm_frac": round(nb / t / (HBM_PEAK_GBS * 1e9), 4)}
         return r
@@ -587,52 +664,75 @@ def step_roofline(model, run_step, ms_per_step, table_path=None):
     SURVEY.md 8d per-layer form): one extra instrumented step logs every
     launch group (m3d.nn.LAYER_LOG with LAYER_TIMING: conv forward, BN/ReLU
     backward, data gradient, weight gradient, pooling / resampling, the fused
-    RPN output heads, the optimizer) with its executed MFMA FLOPs and
-    compulsory HBM bytes, bracketed by HIP events on the stream it runs on.
-    t_roof = sum_l max(F_l / P_f32mfma, B_l / P_hbm); frac = t_roof /
-    ms_per_step (the timed headline step).  Per layer the measured time sits
-    beside its roofline time; 'top_gaps' lists the five largest differences
-    (weight gradients run on a side stream concurrently with the data-gradient
-    chain, so measured times overlap and their sum exceeds the step).  The
-    loss, the ProposalLayer (side stream, latency-bound) and the gradient
-    zero-fill are not logged: the roofline is a lower bound."""
+    RPN output heads, the optimizer) with its executed MFMA FLOPs, compulsory
+    HBM bytes and the MFMA form it ran on, bracketed by HIP events on the
+    stream it runs on.  t_roof = sum_l max(F_l / P_l, B_l / P_hbm) with P_l the
+    ceiling of the kernel that ran group l (x3 kernels: bf16 peak / 6 = 419.4
+    TFLOP/s; f32 MFMA kernels: 157.3); frac = t_roof / ms_per_step (the timed
+    headline step); frac_f32_priced prices every group at the f32 MFMA peak
+    (the looser bound of round 3).  The host is put ahead of the GPU first
+    (_host_ahead), so each group's event bracket is GPU time -- its own kernels,
+    slowed by whatever the side streams run beside them -- not enqueue gaps.
+    'top_gaps' lists the five largest measured - roofline differences (weight
+    gradients run on a side stream concurrently with the data-gradient chain,
+    so measured times overlap and their sum exceeds the step).  The loss, the
+    ProposalLayer (side stream, latency-bound) and the gradient zero-fill are
+    not logged: the roofline is a lower bound."""
     from m3d import nn as mnn
+    run_step()                         # an eager, un-logged step first (allocator / caches warm)
+    torch.cuda.synchronize()
     mnn.LAYER_LOG, mnn.LAYER_TIMING = [], True
     try:
+        _host_ahead()
         run_step()
         torch.cuda.synchronize()
         rec = mnn.LAYER_LOG
     finally:
         mnn.LAYER_LOG, mnn.LAYER_TIMING = None, False
-    pf, pb = F32_MFMA_PEAK_TFLOPS * 1e12, HBM_PEAK_GBS * 1e9
+    if not rec:
+        return {"error": "no launch group logged (a graph replay is not instrumented)"}
+    pb = HBM_PEAK_GBS * 1e9
     rows, phases = [], {}
-    for kind, fd, fe, nb, phase, name, e0, e1 in rec:
+    for r_ in rec:
+        kind, fd, fe, nb, phase, name, e0, e1 = r_[:8]
+        eng = r_[8] if len(r_) > 8 else "f32"
+        pf = _peak_flops(eng)
         tr = max(fe / pf, nb / pb)
+        tr32 = _roof_s(r_, f32_only=True)
         tm = e0.elapsed_time(e1) / 1e3 if e0 is not None else None
-        rows.append({"layer": name, "kind": kind, "phase": phase, "flop": fe, "bytes": nb,
+        rows.append({"layer": name, "kind": kind, "phase": phase, "engine": eng, "flop": fe, "bytes": nb,
                      "bound": "mfma" if fe / pf >= nb / pb else "hbm",
-                     "roof_us": round(tr * 1e6, 2), "meas_us": None if tm is None else round(tm * 1e6, 2)})
-        ph = phases.setdefault(phase, {"launch_groups": 0, "roof_ms": 0.0, "meas_ms": 0.0, "tflop": 0.0, "gb": 0.0})
+                     "roof_us": round(tr * 1e6, 2), "roof_f32_us": round(tr32 * 1e6, 2),
+                     "meas_us": None if tm is None else round(tm * 1e6, 2)})
+        ph = phases.setdefault(phase, {"launch_groups": 0, "roof_ms": 0.0, "roof_f32_ms": 0.0, "meas_ms": 0.0,
+                                       "tflop": 0.0, "gb": 0.0})
         ph["launch_groups"] += 1
         ph["roof_ms"] += tr * 1e3
+        ph["roof_f32_ms"] += tr32 * 1e3
         ph["meas_ms"] += (tm or 0.0) * 1e3
         ph["tflop"] += fe / 1e12
         ph["gb"] += nb / 1e9
     for ph in phases.values():
-        for k in ("roof_ms", "meas_ms", "tflop", "gb"):
+        for k in ("roof_ms", "roof_f32_ms", "meas_ms", "tflop", "gb"):
             ph[k] = round(ph[k], 3)
     roof = sum(r["roof_us"] for r in rows) / 1e3
+    roof32 = sum(r["roof_f32_us"] for r in rows) / 1e3
     gaps = sorted((r for r in rows if r["meas_us"] is not None), key=lambda r: r["meas_us"] - r["roof_us"],
                   reverse=True)[:5]
     if table_path:
         with open(table_path, "w") as f:
-            json.dump({"ms_per_step": ms_per_step, "step_roofline_ms": roof, "rows": rows}, f, indent=0)
+            json.dump({"ms_per_step": ms_per_step, "step_roofline_ms": roof, "step_roofline_f32_priced_ms": roof32,
+                       "rows": rows}, f, indent=0)
     return {"step_roofline_ms": round(roof, 3), "ms_per_step": round(ms_per_step, 3),
-            "frac": round(roof / ms_per_step, 4), "launch_groups": len(rows), "phases": phases,
-            "top_gaps": [{k: r[k] for k in ("layer", "kind", "phase", "bound", "roof_us", "meas_us")} for r in gaps],
-            "peaks": {"f32_mfma_tflops": F32_MFMA_PEAK_TFLOPS, "hbm_gbs": HBM_PEAK_GBS},
-            "note": "sum over launch groups of max(executed MFMA FLOPs / f32 MFMA peak, compulsory bytes / HBM "
-                    "peak) / ms_per_step; Winograd layers priced at their executed GEMM FLOPs"}
+            "frac": round(roof / ms_per_step, 4),
+            "step_roofline_f32_priced_ms": round(roof32, 3), "frac_f32_priced": round(roof32 / ms_per_step, 4),
+            "launch_groups": len(rows), "phases": phases,
+            "top_gaps": [{k: r[k] for k in ("layer", "kind", "phase", "engine", "bound", "roof_us", "meas_us")}
+                         for r in gaps],
+            "peaks": {"x3_tflops": X3_PEAK_TFLOPS, "f32_mfma_tflops": F32_MFMA_PEAK_TFLOPS, "hbm_gbs": HBM_PEAK_GBS},
+            "note": "sum over launch groups of max(executed MFMA FLOPs / the ceiling of the kernel that ran them, "
+                    "compulsory bytes / HBM peak) / ms_per_step; Winograd layers priced at their executed GEMM FLOPs; "
+                    "meas_us = HIP events around the group with the host enqueued ahead (GPU time)"}
 
 
 def roi_leg_large(S, dev, n_rois=512):
@@ -776,6 +876,67 @@ def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
                       + f"), oracle SGD update of all weights + ProposalLayer (C NMS) {t_rest:.1f} s"}
 
 
+def cpu_ops_leg(fmaps, S, dev, n_rois=128, pools=(7, 14)):
+    """the reference's native ops are single-threaded CPU
+    OpKernels (CropAndResize3D @0x4370, its GradImage @0x3a80,
+    NonMaxSuppression3D @0xe4e0: no Shard), so each is timed here as the
+    oracle's C restatement (oracle/oracle.c, gcc -O2, ONE thread) beside the
+    HIP kernel on the same inputs: NMS 15000 -> 6000 at IoU 0.7 (the
+    ProposalLayer's training shape) and CropAndResize3D fwd / GradImage of 128
+    ROIs at 7^3 and 14^3 on P2 of the 128^3 forward (C = 256)."""
+    from m3d import ops
+    from oracle import ops_ref as R
+    res = {"threads": 1, "kind": "port"}
+    # NMS at the time_nms shape and seed
+    rng = np.random.default_rng(4)
+    k = 15000
+    c = rng.uniform(0.05, 0.95, (k, 3))
+    ext = np.exp(rng.uniform(np.log(0.02), np.log(0.3), (k, 3))) / 2
+    bnp = np.concatenate([c - ext, c + ext], 1).astype(np.float32)
+    snp = np.sort(rng.uniform(size=k))[::-1].astype(np.float32).copy()
+    t0 = time.perf_counter()
+    keep_c = R.non_max_suppression_3d(bnp, snp, 6000, 0.7)
+    t_c = time.perf_counter() - t0
+    bt, st_ = torch.from_numpy(bnp).to(dev), torch.from_numpy(snp).to(dev)
+    keep_g = ops.non_max_suppression_3d(bt, st_, 6000, 0.7)
+    t_g = _event_time(lambda: ops.non_max_suppression_3d_padded(bt, st_, 6000, 0.7), 5)
+    res["nms_15000_6000"] = {"cpu_ms": round(t_c * 1e3, 2), "gpu_ms": round(t_g * 1e3, 4),
+                             "speedup": round(t_c / t_g, 1),
+                             "identical": bool(np.array_equal(keep_g.cpu().numpy(), keep_c))}
+    p2 = fmaps[0].detach().contiguous()
+    img = p2.cpu().numpy()
+    boxes = roi_boxes(n_rois, S)[0]
+    bi = np.zeros(n_rois, np.int32)
+    bt = torch.from_numpy(boxes).to(dev)
+    bit = torch.from_numpy(bi).to(dev)
+    for p in pools:
+        t0 = time.perf_counter()
+        crop_c = R.crop_and_resize_3d(img, boxes, bi, (p, p, p))
+        t_fc = time.perf_counter() - t0
+        crop_g = ops.crop_and_resize_3d(p2, bt, bit, (p, p, p), validate=False)
+        t_fg = _event_time(lambda: ops.crop_and_resize_3d(p2, bt, bit, (p, p, p), validate=False), 5)
+        g = np.random.default_rng(p).normal(size=crop_c.shape).astype(np.float32)
+        t0 = time.perf_counter()
+        gi_c = R.crop_and_resize_3d_grad_image(g, boxes, bi, img.shape)
+        t_bc = time.perf_counter() - t0
+        gt = torch.from_numpy(g).to(dev)
+        t_ba = _event_time(lambda: ops.crop_and_resize_3d_grad_image(gt, bt, bit, img.shape, deterministic=0), 5)
+        gi_d = ops.crop_and_resize_3d_grad_image(gt, bt, bit, img.shape, deterministic=1)
+        t_bd = _event_time(lambda: ops.crop_and_resize_3d_grad_image(gt, bt, bit, img.shape, deterministic=1), 5)
+        res[f"crop_{p}"] = {"cpu_fwd_ms": round(t_fc * 1e3, 2), "gpu_fwd_ms": round(t_fg * 1e3, 4),
+                            "fwd_speedup": round(t_fc / t_fg, 1),
+                            "fwd_identical": bool(np.array_equal(crop_g.cpu().numpy(), crop_c)),
+                            "cpu_grad_image_ms": round(t_bc * 1e3, 2),
+                            "gpu_grad_image_atomic_ms": round(t_ba * 1e3, 4),
+                            "gpu_grad_image_deterministic_ms": round(t_bd * 1e3, 4),
+                            "grad_speedup_deterministic": round(t_bc / t_bd, 1),
+                            "grad_deterministic_identical": bool(np.array_equal(gi_d.cpu().numpy(), gi_c))}
+        del crop_c, gi_c, gi_d, crop_g
+    res["note"] = (f"single-thread C restatement vs the HIP kernel, same inputs; crops: {n_rois} ROIs on P2 "
+                   f"{list(p2.shape)}")
+    return res
+
+
 # ---------------------------------------------------------------- main
 def deterministic_leg(step, steps, warmup):
     """The same N=1 training step in deterministic mode (m3d.set_deterministic:
@@ -841,6 +1002,9 @@ def main():
         def step():
             return data_parallel_train_step(model, image, targets, world, proposals=props)
 
+    def eager_step():
+        return data_parallel_train_step(model, image, targets, world, proposals=props)
+
     log(f"[bench] rank {rank}/{world} size {S}^3, warmup {args.warmup}")
     for _ in range(args.warmup):
         r = step()
@@ -876,9 +1040,13 @@ def main():
                       "hip_graph": bool(world == 1 and args.graph)}}
     if world == 1 and not args.no_extras:
         try:
-            out["step_roofline"] = step_roofline(model, step, ms, os.environ.get("M3D_STEP_ROOFLINE_TABLE"))
+            out["step_roofline"] = step_roofline(model, eager_step, ms, os.environ.get("M3D_STEP_ROOFLINE_TABLE"))
         except Exception as e:  # report, never hide
             out["step_roofline"] = {"error": repr(e)}
+    if world > 1:
+        v = validate_dp(model, world)
+        out.setdefault("validation", {})["dp"] = v
+        log(f"[bench] dp validation: {json.dumps(v)}")
     if world > 1 and not args.no_extras:
         try:
             ar = time_allreduce(model.store.grad_flat, world)
@@ -886,6 +1054,7 @@ def main():
             ar = {"error": repr(e)}
         if rank == 0:
             out["allreduce"] = ar
+            out["validation"]["dp"]["allreduce_bus_GBps"] = ar.get("bus_GBps")
     if args.slab_size and not args.no_extras:
         del r
         torch.cuda.empty_cache()
@@ -896,6 +1065,8 @@ def main():
                     if world > 1 else contextlib.nullcontext():
                 out["depth_slab"] = depth_slab_leg(args.slab_size, args.steps, args.warmup, rank, world, dev,
                                                    proposals=props)
+                if "validation" in out["depth_slab"]:
+                    out.setdefault("validation", {})["depth_slab"] = out["depth_slab"]["validation"]
         except Exception as e:  # report, never hide
             out["depth_slab"] = {"error": repr(e)}
     if world == 1 and not args.no_extras:
@@ -908,7 +1079,7 @@ def main():
         except Exception as e:  # report, never hide
             out["targets_in_step"] = {"error": repr(e)}
         try:
-            out["deterministic"] = deterministic_leg(step, max(3, args.steps // 2), 2)
+            out["deterministic"] = deterministic_leg(eager_step, max(3, args.steps // 2), 2)
         except Exception as e:  # report, never hide
             out["deterministic"] = {"error": repr(e)}
     if rank == 0 and not args.no_extras:
@@ -956,13 +1127,60 @@ def main():
                 out["mrcnn_inference"] = {"error": repr(e)}
         if world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(model, S, (match, bbox), args.cpu_slab)
+                with torch.no_grad():
+                    fm2 = model.features(image)
+                out["cpu_ops"] = cpu_ops_leg(fm2, S, dev)
+                del fm2
+            except Exception as e:
+                out["cpu_ops"] = {"error": repr(e)}
+            try:
+                # the box's CPU share (OMP_NUM_THREADS) and every CPU of its affinity;
+                # the faster one is the reported baseline, both are kept
+                n_share = torch.get_num_threads()
+                try:
+                    n_aff = min(len(os.sched_getaffinity(0)), 256)
+                except (AttributeError, OSError):
+                    n_aff = n_share
+                runs = [cpu_baseline(model, S, (match, bbox), args.cpu_slab, threads=n_share)]
+                if n_aff > n_share:
+                    runs.append(cpu_baseline(model, S, (match, bbox), args.cpu_slab, threads=n_aff))
+                torch.set_num_threads(n_share)
+                best = dict(max(runs, key=lambda r: r["value"]))
+                best["runs"] = [{"cores": r["cores"], "value": round(r["value"], 4)} for r in runs]
+                out["cpu_baseline"] = best
             except Exception as e:
                 out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
+        out["summary"] = summary(out)     # last key: survives a truncated tail of the line
         print(json.dumps(out), flush=True)
+    failed = [k for k, v in out.get("validation", {}).items() if isinstance(v, dict) and v.get("ok") is False]
     if world > 1:
         dist.destroy_process_group()
+    if failed:
+        log(f"[bench] VALIDATION FAILED: {failed}")
+        sys.exit(4)
+
+
+def summary(out):
+    """Compact trailer of the JSON line: the headline numbers of every config."""
+    def g(*path):
+        d = out
+        for k in path:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+    return {"volumes_per_s_128": out.get("value"), "ms_per_step_128": out.get("ms_per_step"),
+            "depth_slab_ms_per_step_256": g("depth_slab", "ms_per_step"),
+            "depth_slab_volumes_per_s_256": g("depth_slab", "volumes_per_s"),
+            "depth_slab_n_gpus": g("depth_slab", "n_gpus"),
+            "step_roofline_frac_128": g("step_roofline", "frac"),
+            "step_roofline_frac_256": g("depth_slab", "step_roofline", "frac"),
+            "dominant_kernel_frac": g("roofline", "frac"),
+            "roi14_256_frac_hbm": g("roi_align_256", "pool14", "frac_hbm"),
+            "mrcnn_inference_256_ms": g("mrcnn_inference", "ms_per_volume"),
+            "validation_ok": all(v.get("ok", True) for v in out.get("validation", {}).values()
+                                 if isinstance(v, dict))}
 
 
 if __name__ == "__main__":

@@ -114,3 +114,67 @@ def test_overlapped_bucket_allreduce():
         want = torch.arange(n, dtype=torch.float32) * 1.5 + i
         torch.testing.assert_close(torch.from_numpy(g), want)
     assert all(np.array_equal(a, b) for a, b in zip(out[0]["grads"], out[1]["grads"]))
+
+
+def _replicas(rank, world):
+    """m3d.parallel.validate_replicas (bench.py's N > 1 self-check): tensors
+    equal on every rank pass, one flipped bit on one rank fails exactly that
+    tensor; the float loss comparison of the depth-slab check."""
+    from m3d.parallel import rel_close, tensor_digest, validate_replicas
+    g = torch.Generator().manual_seed(7)
+    w = torch.randn(100_000, generator=g)
+    rois = torch.rand((6000, 6), generator=g)
+    bad = w.clone()
+    if rank == world - 1:
+        bad.view(torch.int32)[12345] ^= 1                 # one ulp on one rank
+    ok = validate_replicas({"weights": w, "rpn_rois": rois})
+    nok = validate_replicas({"weights": bad, "rpn_rois": rois})
+    d1, d2 = tensor_digest(w), tensor_digest(bad)
+    return {"ok": ok, "nok": nok, "digest_differs": bool(not torch.equal(d1, d2)),
+            "close": rel_close(1.0, 1.0 + 5e-6, 1e-5), "far": rel_close(1.0, 1.0 + 5e-5, 1e-5)}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_validate_replicas(world):
+    out = run(_replicas, world)
+    for rank, r in out.items():
+        assert r["ok"] == {"ok": True, "identical": {"rpn_rois": True, "weights": True}}
+        assert r["nok"] == {"ok": False, "identical": {"rpn_rois": True, "weights": False}}
+        assert r["digest_differs"] == (rank == world - 1)
+        assert r["close"] and not r["far"]
+
+
+def test_init_from_env_timeout():
+    """A gloo group from init_from_env with a 3 s timeout: rank 1 skips the
+    all-reduce, rank 0's all_reduce raises within the timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res[0][0] == "raised" and res[0][1] < 30, res
+    assert res[1] == ("skipped", 0.0)
+
+
+def _timeout_worker(rank, world, port, q):
+    import time as _t
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "3d-mask-r-cnn_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      M3D_DIST_TIMEOUT="3")
+    from m3d.parallel import init_from_env
+    init_from_env(backend="gloo")
+    if rank == 1:
+        q.put((1, ("skipped", 0.0)))
+        _t.sleep(8)
+        return
+    t0 = _t.time()
+    try:
+        dist.all_reduce(torch.ones(4))
+        q.put((0, ("completed", _t.time() - t0)))
+    except Exception:
+        q.put((0, ("raised", _t.time() - t0)))
