@@ -52,3 +52,123 @@ __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
 
 }  // namespace m3d
+
+// ---- tuning constants -------------------------------------------------------
+// Every kernel-variant choice of the product library is a compile-time constant
+// holding its measured-best value (DESIGN.md 5 lists the A/B runs).  An A/B
+// build overrides one:  make ab AB_DEFS=-DM3D_TUNE_ROI_SLICES=16  (libm3d_ab.so,
+// loaded with M3D_LIB_FILE=libm3d_ab.so).  Variants measured slower are compiled
+// only in such builds (if constexpr on these values).  The one runtime switch
+// left is M3D_OPERAND_LIMIT (conv3d.hip: lowers the 32-bit operand bound so the
+// per-batch-item path runs at test sizes; tests/test_gpu_conv.py).
+#ifndef M3D_TUNE_GEMM_NBUF
+#define M3D_TUNE_GEMM_NBUF 1
+#endif
+#ifndef M3D_TUNE_GEMM_PERSIST
+#define M3D_TUNE_GEMM_PERSIST 1
+#endif
+#ifndef M3D_TUNE_GEMM_X3
+#define M3D_TUNE_GEMM_X3 29
+#endif
+#ifndef M3D_TUNE_GEMM_BK
+#define M3D_TUNE_GEMM_BK 32
+#endif
+#ifndef M3D_TUNE_WGRAD_MINM
+#define M3D_TUNE_WGRAD_MINM 512
+#endif
+#ifndef M3D_TUNE_WGRAD_K64
+#define M3D_TUNE_WGRAD_K64 1
+#endif
+#ifndef M3D_TUNE_X3W_TR
+#define M3D_TUNE_X3W_TR 1
+#endif
+#ifndef M3D_TUNE_X3W_TR_FLOOR
+#define M3D_TUNE_X3W_TR_FLOOR 0
+#endif
+#ifndef M3D_TUNE_X3W_TR_MINM
+#define M3D_TUNE_X3W_TR_MINM 256
+#endif
+#ifndef M3D_TUNE_X3W_DBG
+#define M3D_TUNE_X3W_DBG 0
+#endif
+#ifndef M3D_TUNE_X3W_TR_MIN_M
+#define M3D_TUNE_X3W_TR_MIN_M 0
+#endif
+#ifndef M3D_TUNE_X3W_MINM
+#define M3D_TUNE_X3W_MINM 0
+#endif
+#ifndef M3D_TUNE_X3W_OCC
+#define M3D_TUNE_X3W_OCC 2
+#endif
+#ifndef M3D_TUNE_X3_AF128
+#define M3D_TUNE_X3_AF128 0
+#endif
+#ifndef M3D_TUNE_X3_256
+#define M3D_TUNE_X3_256 1
+#endif
+#ifndef M3D_TUNE_WINO_NZ
+#define M3D_TUNE_WINO_NZ 4
+#endif
+#ifndef M3D_TUNE_WINO_WGRAD_NZ
+#define M3D_TUNE_WINO_WGRAD_NZ 4
+#endif
+#ifndef M3D_TUNE_WINO_DGRAD_NZ
+#define M3D_TUNE_WINO_DGRAD_NZ 0
+#endif
+#ifndef M3D_TUNE_WINO_XCD
+#define M3D_TUNE_WINO_XCD 0
+#endif
+#ifndef M3D_TUNE_STEM_MFMA
+#define M3D_TUNE_STEM_MFMA 1
+#endif
+#ifndef M3D_TUNE_STEM_WGRAD
+#define M3D_TUNE_STEM_WGRAD 1
+#endif
+#ifndef M3D_TUNE_STEM_X3
+#define M3D_TUNE_STEM_X3 0
+#endif
+#ifndef M3D_TUNE_WGRAD1_X3_MIN_N
+#define M3D_TUNE_WGRAD1_X3_MIN_N 65
+#endif
+#ifndef M3D_TUNE_X3_BK
+#define M3D_TUNE_X3_BK 32
+#endif
+#ifndef M3D_TUNE_X3_OCC3
+#define M3D_TUNE_X3_OCC3 1
+#endif
+#ifndef M3D_TUNE_X3_PERSIST
+#define M3D_TUNE_X3_PERSIST 0
+#endif
+#ifndef M3D_TUNE_X3_256_DBG
+#define M3D_TUNE_X3_256_DBG 0
+#endif
+#ifndef M3D_TUNE_WINO_GRAD4
+#define M3D_TUNE_WINO_GRAD4 0
+#endif
+#ifndef M3D_TUNE_BN_BLOCKS
+#define M3D_TUNE_BN_BLOCKS 1024
+#endif
+#ifndef M3D_TUNE_NMS_REDUCE
+#define M3D_TUNE_NMS_REDUCE 1
+#endif
+#ifndef M3D_TUNE_ROI_SLICES
+#define M3D_TUNE_ROI_SLICES 8
+#endif
+#ifndef M3D_TUNE_ROI_REGION
+#define M3D_TUNE_ROI_REGION 0
+#endif
+#ifndef M3D_TUNE_ROI_BWD_GATHER
+#define M3D_TUNE_ROI_BWD_GATHER 1
+#endif
+#ifndef M3D_TUNE_ROI_SORT
+#define M3D_TUNE_ROI_SORT -1
+#endif
+#ifndef M3D_TUNE_ROI_STAGE
+#define M3D_TUNE_ROI_STAGE 0
+#endif
+#ifndef M3D_TUNE_ROI_ZSPLIT
+#define M3D_TUNE_ROI_ZSPLIT 1
+#endif
+#ifndef M3D_TUNE_ROI_PC
+#define M3D_TUNE_ROI_PC 0
+#endif

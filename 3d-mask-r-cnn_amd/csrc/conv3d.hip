@@ -1033,14 +1033,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 // M3D_GEMM_NBUF=1 (default: 3 blocks/CU, measured 3-5 % faster) or 2 (double-
 // buffered LDS, 2 blocks/CU) selects the k-loop (A/B testing)
 static int gemm_nbuf_env() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_NBUF"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_GEMM_NBUF;
     return v;
 }
 
 // M3D_GEMM_PERSIST=0 disables the persistent tile loop of the batched
 // (Winograd) GEMMs (A/B testing; default on).
 static int gemm_persist_env() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_GEMM_PERSIST;
     return v;
 }
 static int num_cus() {
@@ -1067,7 +1067,7 @@ static int num_cus() {
 // x3_gemm_kernel<AF32>) splits it on its way into LDS: a third less HBM
 // traffic for U, 34.2 -> 32.9 ms/step at 128^3 (default on).
 static int x3_mask() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_X3"); return e ? atoi(e) : 29; }();
+    static constexpr int v = M3D_TUNE_GEMM_X3;
     return v;
 }
 static int gemm_x3_env() { return x3_mask() & 1; }
@@ -1119,7 +1119,7 @@ static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch)
 // M3D_GEMM_BK=64 selects 64-deep k-tiles (1 block/CU: measured 25-30% slower
 // than 32-deep at 2 blocks/CU; kept for A/B testing)
 static int gemm_bk_env() {
-    static int v = [] { const char* e = getenv("M3D_GEMM_BK"); return e ? atoi(e) : 32; }();
+    static constexpr int v = M3D_TUNE_GEMM_BK;
     return v;
 }
 
@@ -1152,12 +1152,12 @@ static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatc
 // M3D_WGRAD_MINM: minimum output rows reduced per workgroup (default 512: measured
 // 45.6 ms/step vs 46.4 at 256, 47.0 at 1024, 47.5 at 128)
 static int wgrad_minm_env() {
-    static int v = [] { const char* e = getenv("M3D_WGRAD_MINM"); return e ? atoi(e) : 512; }();
+    static constexpr int v = M3D_TUNE_WGRAD_MINM;
     return v;
 }
 // M3D_WGRAD_K64=0 disables the 64-deep (K <= 64) weight-gradient tiles
 static int wgrad_k64_env() {
-    static int v = [] { const char* e = getenv("M3D_WGRAD_K64"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_WGRAD_K64;
     return v;
 }
 
@@ -1512,7 +1512,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
 // M3D_X3W_TR (default 1): the 256x256 transposed-read weight-gradient kernel
 // for GEMMs with K, N >= 192; 0 keeps the 128x128 x3_wgrad_kernel everywhere.
 static int wgrad_tr_env() {
-    static int v = [] { const char* e = getenv("M3D_X3W_TR"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_X3W_TR;
     return v;
 }
 
@@ -1522,7 +1522,7 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t cus = num_cus();
     // M3D_X3W_TR_FLOOR=1: splits = floor(CUs / tiles) (one wave of workgroups at
     // one per CU) instead of the ceiling (e.g. 96 tiles: 2 x 96 vs 3 x 96 = 288)
-    static const int fl = [] { const char* e = getenv("M3D_X3W_TR_FLOOR"); return e ? atoi(e) : 0; }();
+    static constexpr int fl = M3D_TUNE_X3W_TR_FLOOR;
     int64_t splits = fl ? cus / tiles : (cus + tiles - 1) / tiles;
     // M3D_X3W_TR_MINM: fewest m rows per workgroup.  Every split adds a 256x256
     // fp32 atomic epilogue: the small-m 1x1x1 gradients of res4 / res5 (m = 8192
@@ -1530,7 +1530,7 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     // and their 16.7 M atomics per launch slowed the data-gradient stream beside
     // them.  256: 128^3 step 28.73 -> 27.8 ms (scripts/gpu_wgrad1b.sh, wg1c/d A/B:
     // 256 / 384 / 512 equal within noise, 1024 28.2-28.5 ms); alone 73 -> 64 us.
-    static const int64_t minm = [] { const char* e = getenv("M3D_X3W_TR_MINM"); return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256; }();
+    static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -1539,8 +1539,10 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
-    static const int dbg = [] { const char* e = getenv("M3D_X3W_DBG"); return e ? atoi(e) : 0; }();
-    switch (dbg) {
+    static constexpr int dbg = M3D_TUNE_X3W_DBG;
+    if constexpr (dbg == 0) {
+        hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
+    } else switch (dbg) {
         case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
         case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
         case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
@@ -1559,7 +1561,7 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
     // M3D_X3W_TR_MIN_M: smallest m (per batch) taking the 256x256 kernel (small-m
     // gradients split m finely to fill the chip, one atomic epilogue per split)
-    static const int64_t tr_min_m = [] { const char* e = getenv("M3D_X3W_TR_MIN_M"); return e ? (int64_t)atoll(e) : (int64_t)0; }();
+    static constexpr int64_t tr_min_m = M3D_TUNE_X3W_TR_MIN_M;
     if (wgrad_tr_env() && K >= 192 && N >= 192 && M >= tr_min_m) {
         launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
         return;
@@ -1567,7 +1569,7 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;
     // M3D_X3W_MINM: this kernel's m-split floor (default: M3D_WGRAD_MINM's)
-    static const int x3w_minm = [] { const char* e = getenv("M3D_X3W_MINM"); return e ? atoi(e) : 0; }();
+    static constexpr int x3w_minm = M3D_TUNE_X3W_MINM;
     const int64_t mfloor = x3w_minm > 0 ? x3w_minm : wgrad_minm_env();
     const int64_t minm = mfloor > 32 ? mfloor : 32;
     const int64_t max_splits = (M + minm - 1) / minm;
@@ -1578,8 +1580,8 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     mper = (mper + 31) / 32 * 32;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 127) / 128), (unsigned)((N + 127) / 128), (unsigned)(splits * nbatch));
-    static const int occ = [] { const char* e = getenv("M3D_X3W_OCC"); return e && atoi(e) == 3 ? 3 : 2; }();
-    if (occ == 2)
+    static constexpr int occ = M3D_TUNE_X3W_OCC;
+    if constexpr (occ == 2)
         hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
     else
         hipLaunchKernelGGL((x3_wgrad_kernel<3>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
@@ -2081,6 +2083,7 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
         }
 }
 
+#if M3D_TUNE_WINO_GRAD4
 // The same transform with 4 consecutive channels per thread (N % 4 == 0):
 // 16-B loads and non-temporal 16-B stores (1 KiB per wave-instruction instead
 // of 256 B) for this write-dominated kernel (P*16 outputs per 2x2xNZ inputs).
@@ -2148,6 +2151,7 @@ __global__ __launch_bounds__(256) void wino_grad4_kernel(const float* __restrict
     }
 }
 
+#endif  // M3D_TUNE_WINO_GRAD4
 // dW[t][c][n] += (G^T (x) G^T (x) Gz^T) dWh[.][c][n]
 template <int NZ>
 __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ dWh, int C,
@@ -2698,6 +2702,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         }
 }
 
+#if M3D_TUNE_X3_AF128
 // ---- the same GEMM with 256x128 tiles, 4 waves, two workgroups per CU -------
 // x3_gemm256_af_kernel holds one workgroup per CU (144 KB of LDS), so while it
 // stores its tile (the fp32 C it writes is 2/3 of its HBM traffic) the CU's
@@ -2848,20 +2853,22 @@ __global__ __launch_bounds__(256, 2) void x3_gemm_af128_kernel(X3G g) {
 
 // M3D_X3_AF128=1: the fp32-A point GEMMs on x3_gemm_af128_kernel (A/B)
 static int x3_af128_env() {
-    static int v = [] { const char* e = getenv("M3D_X3_AF128"); return e ? atoi(e) : 0; }();
+    static constexpr int v = M3D_TUNE_X3_AF128;
     return v;
 }
+
+#endif  // M3D_TUNE_X3_AF128
 
 // M3D_X3_256 (default 1): the Winograd point GEMMs with N % 256 == 0 on
 // x3_gemm256_kernel; 0 keeps x3_gemm_kernel everywhere (A/B)
 static int x3_256_env() {
-    static int v = [] { const char* e = getenv("M3D_X3_256"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_X3_256;
     return v;
 }
 
 // M3D_WINO_NZ = 2 selects the F(2x2x2) tiles (A/B testing; default 4: F(2x2x4))
 static int wino_nz() {
-    static int v = [] { const char* e = getenv("M3D_WINO_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
+    static constexpr int v = M3D_TUNE_WINO_NZ;
     return v;
 }
 // The weight gradient runs on the forward's F(2x2x4) tiles (round 3; was
@@ -2874,13 +2881,13 @@ static int wino_nz() {
 // whole-step gradients at 128^3 median 1.2e-6 vs float64; step 30.9 -> 29.7 ms.
 // M3D_WINO_WGRAD_NZ=2 restores F(2x2x2).
 static int wino_wgrad_nz() {
-    static int v = [] { const char* e = getenv("M3D_WINO_WGRAD_NZ"); return e && atoi(e) == 2 ? 2 : 4; }();
+    static constexpr int v = M3D_TUNE_WINO_WGRAD_NZ;
     return v;
 }
 // M3D_WINO_DGRAD_NZ overrides the data-gradient tile (default: the forward's)
 static int wino_dgrad_nz() {
-    static int v = [] { const char* e = getenv("M3D_WINO_DGRAD_NZ"); return e ? (atoi(e) == 2 ? 2 : 4) : wino_nz(); }();
-    return v;
+    static constexpr int v = M3D_TUNE_WINO_DGRAD_NZ;   // 0: the forward's tile
+    return v ? v : wino_nz();
 }
 static int wino_points(int nz) { return 16 * (nz + 2); }
 static int wino_points() { return wino_points(wino_nz()); }
@@ -2895,7 +2902,7 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
     g.tz_mode = 0;
-    static const int xcd = [] { const char* e = getenv("M3D_WINO_XCD"); return e ? atoi(e) : 0; }();
+    static constexpr int xcd = M3D_TUNE_WINO_XCD;
     g.xcd = xcd;
     return g;
 }
@@ -3243,7 +3250,8 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
     }
 }
 
-// ---- the stem forward on the exact bf16 split (default) ----------------------
+#if M3D_TUNE_STEM_X3
+// ---- the stem forward on the exact bf16 split (A/B builds: M3D_TUNE_STEM_X3) ----
 // stem_fwd_kernel above runs the f32 MFMA (1/16 of the bf16 rate), which bounds
 // it near 1.2 ms at 256^3 even at full issue.  Here the product runs as 6
 // v_mfma_f32_32x32x16_bf16 on the 3-way split of both operands (as the
@@ -3611,10 +3619,11 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_x3b_kernel(ConvP p, Epi e, in
         buf ^= 1;
     }
 }
+#endif  // M3D_TUNE_STEM_X3
 
 static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, int sx, int sz, int dly, int dlx,
                     int dlz, int res_mode, int64_t split_n, int64_t ldy) {
-    static const int env = [] { const char* v = getenv("M3D_STEM_MFMA"); return v ? atoi(v) : 1; }();
+    static constexpr int env = M3D_TUNE_STEM_MFMA;
     // the kernel's own epilogue covers bias / z / frozen BN / activation, plain
     // [M, 64] stores (no residual, split or accumulate)
     return env && Cin == 1 && kh == 7 && kw == 7 && kd == 7 && Cout == 64 && sy == 2 && sx == 2 && sz == 1 &&
@@ -3734,7 +3743,7 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(ConvP p, const float* _
 }
 
 static bool stem_wgrad_env() {
-    static const int v = [] { const char* e = getenv("M3D_STEM_WGRAD"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_STEM_WGRAD;
     return v != 0;
 }
 
@@ -3775,19 +3784,21 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     // vs 0.28 ms alone at 128^3); with 4 per CU the others absorb its share
     // M3D_STEM_X3=1 / 2: the bf16-split forms (measured slower than the f32 kernel: 2.65 / 2.24-2.5 vs
     // 2.2 ms at 256^3, DESIGN.md round-3 list); default the f32 MFMA kernel
-    static const int x3 = [] { const char* v = getenv("M3D_STEM_X3"); return v ? atoi(v) : 0; }();
-    if (x3 == 2) {
+#if M3D_TUNE_STEM_X3
+    static constexpr int x3 = M3D_TUNE_STEM_X3;
+    if constexpr (x3 == 2) {
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, 2 * (int64_t)ncu));
         hipLaunchKernelGGL(stem_fwd_x3b_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
         return check_launch("stem_fwd_x3b_kernel");
     }
-    if (x3) {
+    if constexpr (x3 == 1) {
         // one workgroup per CU (131 KB of LDS): pairs of workgroups take the two
         // 32-channel halves of the same tiles, each wave its own tiles
         const unsigned grid = (unsigned)(2 * std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, ncu / 2)));
         hipLaunchKernelGGL(stem_fwd_x3_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
         return check_launch("stem_fwd_x3_kernel");
     }
+#endif
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 7) / 8, 4 * (int64_t)ncu));
     hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, tz_n, ntiles);
     return check_launch("stem_fwd_kernel");
@@ -4062,7 +4073,7 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
     // 1x1x1 stride-1 convs: im2col is x itself, the plain weight-gradient GEMM
     // dW += x^T dz -- on the exact bf16 split like the Winograd ones
     // M3D_WGRAD1_X3_MIN_N: smallest Cout taking this path (A/B: 65 = round 2's Cout > 64)
-    static const int min_n = [] { const char* e = getenv("M3D_WGRAD1_X3_MIN_N"); return e ? atoi(e) : 65; }();
+    static constexpr int min_n = M3D_TUNE_WGRAD1_X3_MIN_N;
     if (vec && ((x3_mask() >> 3) & 1) && kh == 1 && kw == 1 && kd == 1 && sy == 1 && sx == 1 && sz == 1 &&
         py == 0 && px == 0 && pz == 0 && OH == H && OW == W && OD == D && Cout >= min_n) {
         launch_wgrad_x3(x, dz, dw, p.M, (int)Cin, (int)Cout, 1, 0, 0, 0, st(s));
@@ -4248,15 +4259,15 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, in
 
 // M3D_X3_BK (16 | 32) and M3D_X3_PERSIST (0 | 1): x3_gemm_kernel variant (A/B)
 static int x3_bk_env() {
-    static int v = [] { const char* e = getenv("M3D_X3_BK"); return e && atoi(e) == 16 ? 16 : 32; }();
+    static constexpr int v = M3D_TUNE_X3_BK;
     return v;
 }
 static int x3_occ3_env() {
-    static int v = [] { const char* e = getenv("M3D_X3_OCC3"); return e ? atoi(e) : 1; }();
+    static constexpr int v = M3D_TUNE_X3_OCC3;
     return v;
 }
 static int x3_persist_env() {
-    static int v = [] { const char* e = getenv("M3D_X3_PERSIST"); return e ? atoi(e) : 0; }();
+    static constexpr int v = M3D_TUNE_X3_PERSIST;
     return v;
 }
 
@@ -4274,12 +4285,14 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
     q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
     q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
-    if (af32 && x3_256_env() && x3_af128_env() && N % 128 == 0 && T >= 256) {
+#if M3D_TUNE_X3_AF128
+    if (M3D_TUNE_X3_AF128 && af32 && x3_256_env() && N % 128 == 0 && T >= 256) {
         const int64_t t128 = ((T + 255) / 256) * (N / 128) * P;
         const dim3 grid((unsigned)(t128 < 65536 ? t128 : 65536), (unsigned)((t128 + 65535) / 65536));
         hipLaunchKernelGGL(x3_gemm_af128_kernel, grid, dim3(256), 0, s, q);
         return;
     }
+#endif
     if (af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
@@ -4289,8 +4302,10 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     if (!af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
-        static const int dbg = [] { const char* e = getenv("M3D_X3_256_DBG"); return e ? atoi(e) : 0; }();
-        switch (dbg) {
+        static constexpr int dbg = M3D_TUNE_X3_256_DBG;
+        if constexpr (dbg == 0) {
+            hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
+        } else switch (dbg) {
             case 1: hipLaunchKernelGGL(x3_gemm256_kernel<1>, grid, dim3(512), 0, s, q); break;
             case 2: hipLaunchKernelGGL(x3_gemm256_kernel<2>, grid, dim3(512), 0, s, q); break;
             case 3: hipLaunchKernelGGL(x3_gemm256_kernel<3>, grid, dim3(512), 0, s, q); break;
@@ -4694,11 +4709,13 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
     else
         WINO_INPUT(nz, false, dim3(grid_for(g.T * Cin, 256)), st(s), x, g, (int)Cin, ws.U);
     // M3D_WINO_GRAD4=1: the float4 form (measured slower: 278 vs 253 us avg, write-bound)
-    static const int grad4 = [] { const char* v = getenv("M3D_WINO_GRAD4"); return v ? atoi(v) : 0; }();
+#if M3D_TUNE_WINO_GRAD4
+    static constexpr int grad4 = M3D_TUNE_WINO_GRAD4;
     if (grad4 && Cout % 4 == 0)
         WINO_LAUNCH_NZ(nz, wino_grad4_kernel, dim3(grid_for(g.T * (Cout / 4), 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     else
+#endif
         WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     if (wgrad_x3_env() && Cout > 64) {

@@ -743,7 +743,7 @@ extern "C" int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64
 // at 128^3, 512: 32.4 ms; scripts/gpu_step_ab.sh, round 2) and halves the
 // partial rows bn_sums_reduce_kernel folds.
 static int bn_blocks_env() {
-    static int v = [] { const char* e = getenv("M3D_BN_BLOCKS"); return e ? atoi(e) : 1024; }();
+    static constexpr int v = M3D_TUNE_BN_BLOCKS;
     return v > 0 ? v : 1024;
 }
 static void bn_grid(int64_t M, int64_t C, int& T, int& groups, int64_t& gx) {

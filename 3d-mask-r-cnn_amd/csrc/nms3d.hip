@@ -517,7 +517,7 @@ extern "C" int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int
     rc = check_launch("nms_mask_kernel");
     if (rc) return rc;
     // M3D_NMS_REDUCE=0: the general kernel at every size (A/B)
-    static const int pf = [] { const char* e = getenv("M3D_NMS_REDUCE"); return e ? atoi(e) : 1; }();
+    static constexpr int pf = M3D_TUNE_NMS_REDUCE;
     if (pf && cb <= 256) {
         hipLaunchKernelGGL(nms_reduce_pf_kernel, dim3(1), dim3(1024), 0, st(s), w.mask, w.keys, N, cb, max_out,
                            keep, num_keep);

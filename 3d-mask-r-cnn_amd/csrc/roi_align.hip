@@ -411,6 +411,7 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     }
 }
 
+#if M3D_TUNE_ROI_PC
 // Producer / consumer form of line_fwd_sl_kernel<8> (M3D_ROI_PC=1): a
 // workgroup of 8 waves -- waves 0-3 gather and interpolate (loads only), waves
 // 4-7 store what their partner produced one z step earlier (stores only),
@@ -507,6 +508,7 @@ __global__ __launch_bounds__(512) void line_fwd_pc_kernel(LineArgs a, Pyr P, con
         __syncthreads();
     }
 }
+#endif  // M3D_TUNE_ROI_PC
 
 // Spatial order of the lines (m3d_pyramid_roi_align3d_fwd_ws): a counting sort
 // by the owner (y, x) column of each line -- bucket = level base + (b, ty, lx)
@@ -625,7 +627,7 @@ __global__ void roi_perm_kernel(const int32_t* __restrict__ inv, int64_t lines, 
 }
 
 static int roi_slices() {
-    static const int env = [] { const char* e = getenv("M3D_ROI_SLICES"); return e ? atoi(e) : 8; }();
+    static constexpr int env = M3D_TUNE_ROI_SLICES;
     return env;
 }
 
@@ -758,7 +760,7 @@ __global__ __launch_bounds__(256) void region_fwd_kernel(LineArgs a, Pyr P, Regi
 // default -- measured 3x slower at 256^3), 1 (2x2x8), 2 (4x4x4),
 // 3 (2x2x16), 4 (4x4x8)
 static int roi_region_mode() {
-    static const int env = [] { const char* e = getenv("M3D_ROI_REGION"); return e ? atoi(e) : 0; }();
+    static constexpr int env = M3D_TUNE_ROI_REGION;
     return env;
 }
 
@@ -891,7 +893,7 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(GatherArgs a, Pyr P) {
 // the gather-form backward for C in {64, 128, 256, 512} and crops <= 32 per
 // axis (M3D_ROI_BWD_GATHER=0: the per-sample atomic scatter everywhere)
 static bool gather_bwd_ok(int64_t C, int ch, int cw, int cd) {
-    static const int env = [] { const char* e = getenv("M3D_ROI_BWD_GATHER"); return e ? atoi(e) : 1; }();
+    static constexpr int env = M3D_TUNE_ROI_BWD_GATHER;
     return env && (C == 64 || C == 128 || C == 256 || C == 512) && ch <= 32 && cw <= 32 && cd <= 32;
 }
 
@@ -1533,9 +1535,9 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             // 14^3 mask pool -- PMC fabric reads at 256^3 / 512 ROIs 3.41 -> 1.89 GB,
             // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for the 7^3 pool
             // (its lines are short and the sort does not pay); M3D_ROI_SORT overrides
-            static const int sort_env0 = [] { const char* e = getenv("M3D_ROI_SORT"); return e ? atoi(e) : -1; }();
+            static constexpr int sort_env0 = M3D_TUNE_ROI_SORT;
             // register-staged z parts (M3D_ROI_STAGE = PD, 0: off): zs = ceil(pd / PD) parts per line
-            static const int stage_env = [] { const char* e = getenv("M3D_ROI_STAGE"); return e ? atoi(e) : 0; }();
+            static constexpr int stage_env = M3D_TUNE_ROI_STAGE;
             const int spd = (stage_env == 4 || stage_env == 7 || stage_env == 14) && sl == 8 ? stage_env : 0;
             int sort_env = sort_env0 >= 0 ? sort_env0 : (pd >= 14 ? 3 : 0);
             if (sort_env == 3 && spd && spd < pd) sort_env = 0;   // the wave order sorts whole lines
@@ -1590,28 +1592,37 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 if (rc) return rc;
                 perm = pm;
             }
-            static const int zs_env = [] { const char* e = getenv("M3D_ROI_ZSPLIT"); return e ? atoi(e) : 1; }();
+            static constexpr int zs_env = M3D_TUNE_ROI_ZSPLIT;
             const int zs = spd ? (int)((pd + spd - 1) / spd)
                                : (wperm ? 1 : std::max(1, std::min(zs_env, (int)pd)));
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
-            static const int pc_env = [] { const char* e = getenv("M3D_ROI_PC"); return e ? atoi(e) : 0; }();
+#if M3D_TUNE_ROI_PC
+            static constexpr int pc_env = M3D_TUNE_ROI_PC;
             if (pc_env && sl == 8 && zs == 1 && !spd && !perm) {
                 hipLaunchKernelGGL(line_fwd_pc_kernel, dim3(grid), dim3(512), 0, s, a, P, wperm);
                 return check_launch("line_fwd_pc_kernel");
             }
+#endif
+#if M3D_TUNE_ROI_STAGE
             if (spd) {
                 if (spd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 else if (spd == 7) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
                 return check_launch("line_fwd_sl_kernel<staged>");
             }
-            if (sl == 2) hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-            else if (sl == 4) hipLaunchKernelGGL(line_fwd_sl_kernel<4>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-            else if (sl == 16) hipLaunchKernelGGL(line_fwd_sl_kernel<16>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-            else hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+#endif
+            if constexpr (M3D_TUNE_ROI_SLICES == 2)
+                hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else if constexpr (M3D_TUNE_ROI_SLICES == 4)
+                hipLaunchKernelGGL(line_fwd_sl_kernel<4>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else if constexpr (M3D_TUNE_ROI_SLICES == 16)
+                hipLaunchKernelGGL(line_fwd_sl_kernel<16>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
+            else
+                hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
             return check_launch("line_fwd_sl_kernel");
         }
+#if M3D_TUNE_ROI_REGION
         const int mode = roi_region_mode();
         if (mode && ph <= 64 && pw <= 64 && pd <= 64) {
             switch (mode) {
@@ -1622,6 +1633,7 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             }
             return check_launch("region_fwd_kernel");
         }
+#endif
         hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, s, a, P);
         return check_launch("line_fwd_kernel");
     }

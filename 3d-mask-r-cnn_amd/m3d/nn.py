@@ -312,36 +312,17 @@ def _shared_wino_release(wshare):
         wshare.pop("pending_bwd", None)
 
 
-# One Winograd workspace arena per (device, stream), grown to the largest conv
-# and reused by every later one: the convs of a stream run in its order, so a
-# workspace is never live twice.  Per-call allocations of 4-20 GB workspaces
-# (at 256^3) of changing sizes fragmented the caching allocator -- 263 GB
-# reserved for 115 GB allocated, segments freed and re-allocated inside the
-# step, the 256^3 step at 290-890 ms instead of ~190 (r03p).  M3D_WINO_ARENA=0:
-# per-call workspaces.
-WINO_ARENA = os.environ.get("M3D_WINO_ARENA", "0") != "0"
-_ARENA = {}
-
-
 def _wino_ws(B, H, W, D, OD, cin, cout, dev, dedicated=False):
-    """(workspace, bytes) of one Winograd conv call; from the stream's arena
-    unless ``dedicated`` (a workspace the caller keeps across calls)."""
+    """(workspace, bytes) of one Winograd conv call, from the caching allocator.
+    (A per-stream arena grown to the largest conv measured no better at 256^3 --
+    216-940 ms before the side-stream throttle, DESIGN.md 5 -- and was removed.)"""
     n = int(_L().m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, cin, cout))
-    if dedicated or not WINO_ARENA:
-        return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
-    key = (dev.index if dev.index is not None else torch.cuda.current_device(),
-           torch.cuda.current_stream(dev).cuda_stream)
-    buf = _ARENA.get(key)
-    if buf is None or buf.numel() * 4 < n + 4:
-        _ARENA.pop(key, None)          # the old one returns to the allocator, stream-ordered
-        buf = torch.empty(n // 4 + 1, device=dev, dtype=torch.float32)
-        _ARENA[key] = buf
-    return buf, n
+    return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
 
 
 def release_wino_arena():
-    """Drop the Winograd workspace arenas (e.g. before torch.cuda.empty_cache())."""
-    _ARENA.clear()
+    """Kept for callers of the removed arena (bench.py): nothing is held."""
+    return None
 
 
 def same_out_pad(n, k, s):

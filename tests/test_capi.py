@@ -103,3 +103,20 @@ def test_tf_op_defs_match_the_wheel():
         j = src.index(".SetShapeFn", i)
         got = re.findall(r'\.(?:Input|Output|Attr)\("([^"]*)"\)', src[i:j])
         assert got == d["specs"], (op, got, d["specs"])
+
+
+def test_runtime_switches_are_few_and_tested():
+    """The product library reads its environment only where a test drives the
+    switch: every other kernel-variant choice is a
+    compile-time M3D_TUNE_* constant (csrc/common.h; A/B builds via make ab)."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = set()
+    for f in glob.glob(os.path.join(root, "3d-mask-r-cnn_amd", "csrc", "*")):
+        names |= set(re.findall(r'getenv\("(M3D_\w+)"\)', open(f).read()))
+    assert len(names) < 10, names
+    tests_text = "".join(open(f).read() for f in glob.glob(os.path.join(root, "tests", "*.py"))
+                         if not f.endswith("test_capi.py"))
+    for n in names:
+        assert n in tests_text, f"{n} is read by libm3d but no test drives it"
