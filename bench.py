@@ -816,6 +816,31 @@ def _host_cpus():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
 
 
+def _usable_cpus(default):
+    """CPUs this process can actually run on: its affinity set, capped by the
+    cgroup CPU quota (cpu.max) when one is set -- threads beyond the quota only
+    time-slice against each other."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return default
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(per))))
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            n = min(n, max(1, q // per))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 256))
+
+
 def cpu_baseline(model, S, targets_np, depth_slab=0, threads=None):
     """The oracle restatement timed on the host for the SAME step as the GPU
     leg: oracle/model_ref.py forward (torch-CPU fp32) -> the RPN losses of
@@ -1056,6 +1081,7 @@ def main():
             out["allreduce"] = ar
             out["validation"]["dp"]["allreduce_bus_GBps"] = ar.get("bus_GBps")
     if args.slab_size and not args.no_extras:
+        log(f"[bench] leg depth_slab {args.slab_size}^3 ({time.strftime('%H:%M:%S')})")
         del r
         torch.cuda.empty_cache()
         try:
@@ -1071,14 +1097,17 @@ def main():
             out["depth_slab"] = {"error": repr(e)}
     if world == 1 and not args.no_extras:
         try:
+            log(f"[bench] leg configs0 ({time.strftime('%H:%M:%S')})")
             out["configs0"] = configs0_leg(dev, max(3, args.steps // 2), 2)
         except Exception as e:  # report, never hide
             out["configs0"] = {"error": repr(e)}
         try:
+            log(f"[bench] leg targets_in_step ({time.strftime('%H:%M:%S')})")
             out["targets_in_step"] = targets_in_step_leg(model, image, max(3, args.steps // 2), 2, dev)
         except Exception as e:  # report, never hide
             out["targets_in_step"] = {"error": repr(e)}
         try:
+            log(f"[bench] leg deterministic ({time.strftime('%H:%M:%S')})")
             out["deterministic"] = deterministic_leg(eager_step, max(3, args.steps // 2), 2)
         except Exception as e:  # report, never hide
             out["deterministic"] = {"error": repr(e)}
@@ -1089,6 +1118,7 @@ def main():
             # dominant kernel of the step: x3_gemm256_af_kernel (17.7 % of the step's
             # kernel time: the Winograd point GEMMs plus the big-K 1x1x1 convs,
             # profiles/r02i_bench_kernels_128.txt), then x3_wgrad_tr_kernel (15.7 %)
+            log(f"[bench] leg roofline ({time.strftime('%H:%M:%S')})")
             out["roofline"] = time_wino_gemm(S)
             out["roofline"]["wgrad_gemm"] = time_wgrad_gemm(S)
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
@@ -1096,31 +1126,37 @@ def main():
         except Exception as e:  # report, never hide
             out["roofline"] = {"error": repr(e)}
         try:
+            log(f"[bench] leg roi_align ({time.strftime('%H:%M:%S')})")
             out["roi_align"] = time_roi_align(fmaps, S)
         except Exception as e:
             out["roi_align"] = {"error": repr(e)}
         try:
+            log(f"[bench] leg roi_align_bwd ({time.strftime('%H:%M:%S')})")
             out["roi_align_bwd"] = time_roi_align_bwd(fmaps, S)
         except Exception as e:
             out["roi_align_bwd"] = {"error": repr(e)}
         del fmaps
         try:
+            log(f"[bench] leg nms ({time.strftime('%H:%M:%S')})")
             out["nms"] = time_nms(dev)
         except Exception as e:
             out["nms"] = {"error": repr(e)}
         try:
+            log(f"[bench] leg fwd_roofline ({time.strftime('%H:%M:%S')})")
             out["fwd_roofline"] = fwd_roofline(model, image)
         except Exception as e:
             out["fwd_roofline"] = {"error": repr(e)}
         torch.cuda.empty_cache()
         if args.roi_size:
             try:
+                log(f"[bench] leg roi_align_256 ({time.strftime('%H:%M:%S')})")
                 out["roi_align_256"] = roi_leg_large(args.roi_size, dev)
             except Exception as e:
                 out["roi_align_256"] = {"error": repr(e)}
             torch.cuda.empty_cache()
         if args.infer_size:
             try:
+                log(f"[bench] leg mrcnn_inference ({time.strftime('%H:%M:%S')})")
                 out["mrcnn_inference"] = mrcnn_inference_leg(args.infer_size, max(3, args.steps // 2),
                                                              1, dev)
             except Exception as e:
@@ -1129,6 +1165,7 @@ def main():
             try:
                 with torch.no_grad():
                     fm2 = model.features(image)
+                log(f"[bench] leg cpu_ops ({time.strftime('%H:%M:%S')})")
                 out["cpu_ops"] = cpu_ops_leg(fm2, S, dev)
                 del fm2
             except Exception as e:
@@ -1137,10 +1174,8 @@ def main():
                 # the box's CPU share (OMP_NUM_THREADS) and every CPU of its affinity;
                 # the faster one is the reported baseline, both are kept
                 n_share = torch.get_num_threads()
-                try:
-                    n_aff = min(len(os.sched_getaffinity(0)), 256)
-                except (AttributeError, OSError):
-                    n_aff = n_share
+                n_aff = _usable_cpus(n_share)
+                log(f"[bench] leg cpu_baseline: {n_share} and {n_aff} threads")
                 runs = [cpu_baseline(model, S, (match, bbox), args.cpu_slab, threads=n_share)]
                 if n_aff > n_share:
                     runs.append(cpu_baseline(model, S, (match, bbox), args.cpu_slab, threads=n_aff))

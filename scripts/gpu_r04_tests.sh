@@ -1,0 +1,12 @@
+#!/bin/bash
+# All -m gpu tests + smoke on one box.  Usage: gpurun --timeout 1100 -- bash scripts/gpu_r04_tests.sh TAG
+set -o pipefail
+TAG=${1:-r04}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 950 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -n 2 $OUT/pytest_gpu.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
+tail -n 1 $OUT/smoke.log
+echo DONE
