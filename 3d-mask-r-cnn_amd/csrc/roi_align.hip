@@ -1016,6 +1016,9 @@ __global__ __launch_bounds__(256) void crop_bwd_det_kernel(
     const int CV = C / VEC;
     const int lane = threadIdx.x & 63;
     const int64_t ncols = (int64_t)B * H * W;
+    // Z values per wave when every wave holds whole Z rows of channel vectors
+    // (CV a multiple or a divisor of 64); 0: per-thread z sample loop
+    const int zpw = CV % 64 == 0 ? 1 : (64 % CV == 0 ? 64 / CV : 0);
     auto rdl = [](float v, int l) {
         return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
     };
@@ -1079,18 +1082,38 @@ __global__ __launch_bounds__(256) void crop_bwd_det_kernel(
                 // must run with every lane active, or a value the compiler sinks into
                 // a divergent block is missing in the lanes that skipped it)
                 if (!(myt | myb) || !(mxl | mxr)) continue;
-                // this thread's z samples / corner sides (per thread: Z varies across lanes)
+                // this thread's z samples / corner sides
                 const float zsc = axis_scale(z1, z2, D, cd);
                 uint64_t mzf = 0, mzk = 0;
-                for (int i = 0; i < cd && active; ++i) {
-                    const float in_z = axis_coord(z1, z2, D, cd, i, zsc);
-                    if (in_z < 0 || in_z > (float)(D - 1)) continue;
-                    if (method == 1) {
-                        if ((int)roundf(in_z) == Z) mzf |= 1ull << i;
-                        continue;
+                if (zpw > 0) {
+                    // the wave holds zpw consecutive Z values: lane i computes z sample i
+                    // once, one ballot per (Z, side) gives every thread its masks (instead
+                    // of cd coordinate evaluations per thread and box)
+                    const float in_zl = axis_coord(z1, z2, D, cd, lane, zsc);
+                    const bool vz = lane < cd && !(in_zl < 0 || in_zl > (float)(D - 1));
+                    const int fzl = method == 1 ? (int)roundf(in_zl) : (int)floorf(in_zl);
+                    const int kzl = (int)ceilf(in_zl);
+                    for (int g = 0; g < zpw; ++g) {
+                        const int Zg = zw0 + g;
+                        const uint64_t f = __ballot(vz && fzl == Zg);
+                        const uint64_t k = method == 1 ? 0ull : __ballot(vz && kzl == Zg);
+                        if (active && Z == Zg) {
+                            mzf = f;
+                            mzk = k;
+                        }
                     }
-                    if ((int)floorf(in_z) == Z) mzf |= 1ull << i;
-                    if ((int)ceilf(in_z) == Z) mzk |= 1ull << i;
+                    if (__ballot((mzf | mzk) != 0) == 0) continue;      // wave-uniform skip
+                } else {
+                    for (int i = 0; i < cd && active; ++i) {
+                        const float in_z = axis_coord(z1, z2, D, cd, i, zsc);
+                        if (in_z < 0 || in_z > (float)(D - 1)) continue;
+                        if (method == 1) {
+                            if ((int)roundf(in_z) == Z) mzf |= 1ull << i;
+                            continue;
+                        }
+                        if ((int)floorf(in_z) == Z) mzf |= 1ull << i;
+                        if ((int)ceilf(in_z) == Z) mzk |= 1ull << i;
+                    }
                 }
                 const float* gn = grads + (size_t)n * ch * cw * cd * C + (size_t)cv * VEC;
                 if (method == 1) {                          // nearest: img[ny,nx,nz] += g
@@ -1147,6 +1170,256 @@ __global__ __launch_bounds__(256) void crop_bwd_det_kernel(
                 dst[0] = acc[0];
         }
     }
+}
+
+// Sample hit masks of one axis for one box (crop_bwd_det_col_kernel's list
+// build): bit i of lo / hi set when sample i lies in the image and its floor /
+// ceil voxel (nearest: its rounded voxel, in lo) is V.  The sample coordinate
+// a + i*sc is monotone in i, so only indices within two of the range where it
+// can lie in (V - 1, V + 1) are tested -- each with axis_coord, the kernels'
+// own arithmetic; at spacings below 1e-3 voxel every sample is tested.
+__device__ __forceinline__ void det_axis_hits(float b1, float b2, int S, int n, int V, int method, uint64_t& lo,
+                                              uint64_t& hi) {
+    lo = hi = 0;
+    const float sc = axis_scale(b1, b2, S, n);
+    int i0 = 0, i1 = n - 1;
+    if (n > 1 && fabsf(sc) >= 1e-3f) {
+        const float a = b1 * (float)(S - 1);
+        float r0 = ((float)(V - 1) - a) / sc, r1 = ((float)(V + 1) - a) / sc;
+        if (r0 > r1) { const float t = r0; r0 = r1; r1 = t; }
+        if (!(r1 >= -2.0f) || !(r0 <= (float)(n + 1))) return;       // (NaN boxes: no sample)
+        i0 = max(0, (int)floorf(r0) - 2);
+        i1 = min(n - 1, (int)ceilf(r1) + 2);
+    }
+    for (int i = i0; i <= i1; ++i) {
+        const float c = axis_coord(b1, b2, S, n, i, sc);
+        if (c < 0 || c > (float)(S - 1)) continue;
+        if (method == 1) {
+            if ((int)roundf(c) == V) lo |= 1ull << i;
+            continue;
+        }
+        if ((int)floorf(c) == V) lo |= 1ull << i;
+        if ((int)ceilf(c) == V) hi |= 1ull << i;
+    }
+}
+
+// Deterministic grad_image, column form (the default of mode 1 when the boxes
+// fit the list): a workgroup owns one voxel column (b, Y, X) and a range of its
+// (Z, channel-vector) chunks.  Wave 0 first scans the boxes once, in ascending
+// order, and keeps in LDS only those whose y and x samples really hit the
+// column (exact per-axis ballots, lane = sample index), with their hit masks;
+// every chunk then walks that short list -- instead of re-testing all boxes,
+// and re-deriving the y / x hits, for every 256 destinations of the column.
+// Per destination the terms, their order (box -> y -> x -> z -> corner) and
+// the arithmetic are crop_bwd_det_kernel's: bit-identical.
+constexpr int DET_CAP = 512;        // boxes per column list (host falls back above N = DET_CAP)
+constexpr int DET_CHUNKS = 8;       // 256-destination chunks per workgroup
+
+template <int VEC>
+__global__ __launch_bounds__(256) void crop_bwd_det_col_kernel(
+    const float* __restrict__ grads, const float* __restrict__ boxes,
+    const int32_t* __restrict__ box_ind, int64_t N, int ch, int cw, int cd, int B, int H, int W,
+    int D, int C, int method, int64_t blocks_per_col, float* __restrict__ gimg) {
+    __shared__ int32_t ln[DET_CAP];
+    __shared__ uint64_t lm[DET_CAP][4];          // y top / bottom, x left / right hit masks
+    __shared__ float lb[DET_CAP][8];             // the box, its z scale and first-sample z (broadcast reads)
+    __shared__ int lcount;
+    const int CV = C / VEC;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int zpw = CV % 64 == 0 ? 1 : (64 % CV == 0 ? 64 / CV : 0);
+    const int64_t col = blockIdx.x / blocks_per_col;
+    const int64_t part = blockIdx.x - col * blocks_per_col;
+    const int X = (int)(col % W);
+    const int Y = (int)((col / W) % H);
+    const int b = (int)(col / ((int64_t)H * W));
+    const int64_t nchunks = ((int64_t)D * CV + 255) / 256;
+    const int64_t c0 = part * DET_CHUNKS;
+    const int64_t c1 = c0 + DET_CHUNKS < nchunks ? c0 + DET_CHUNKS : nchunks;
+    if (c0 >= c1) return;                        // (uniform per block)
+    // this block's Z range, for the conservative z part of the box test
+    const int zb0 = (int)min<int64_t>(c0 * 256 / CV, D - 1);
+    const int zb1 = (int)min<int64_t>((c1 * 256 - 1) / CV, D - 1);
+    // lane = box: per-axis hit masks of sample indices (exact: every sample in a
+    // conservative index range is tested with the kernel's coordinate maths).
+    // Wave w takes the 64-box groups w and w + 4 (DET_CAP = 8 groups), counts
+    // its hits per group, and after a prefix over the groups writes them in
+    // ascending box order.
+    static_assert(DET_CAP == 8 * 64, "two 64-box groups per wave");
+    __shared__ int gcnt[8];
+    uint64_t hm[2], my[2][4];
+    bool hit[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int64_t nl = (int64_t)(wave + 4 * r) * 64 + lane;
+        hit[r] = false;
+        my[r][0] = my[r][1] = my[r][2] = my[r][3] = 0;
+        if (nl < N && box_ind[nl] == b) {
+            const float* bx = boxes + nl * 6;
+            const float z1 = bx[2], z2 = bx[5];
+            const float zsc = axis_scale(z1, z2, D, cd);
+            const float ze0 = axis_coord(z1, z2, D, cd, 0, zsc), ze1 = axis_coord(z1, z2, D, cd, cd - 1, zsc);
+            if (!((float)zb1 < floorf(fminf(ze0, ze1)) || (float)zb0 > ceilf(fmaxf(ze0, ze1)))) {
+                det_axis_hits(bx[0], bx[3], H, ch, Y, method, my[r][0], my[r][1]);
+                if (my[r][0] | my[r][1]) det_axis_hits(bx[1], bx[4], W, cw, X, method, my[r][2], my[r][3]);
+                hit[r] = (my[r][0] | my[r][1]) && (my[r][2] | my[r][3]);
+            }
+        }
+        hm[r] = __ballot(hit[r]);
+        if (lane == 0) gcnt[wave + 4 * r] = __builtin_popcountll(hm[r]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int g = wave + 4 * r;
+        int base = 0;
+        for (int q = 0; q < g; ++q) base += gcnt[q];
+        if (hit[r]) {
+            const int64_t nl = (int64_t)g * 64 + lane;
+            const int slot = base + __builtin_popcountll(hm[r] & ((1ull << lane) - 1));
+            ln[slot] = (int32_t)nl;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) lm[slot][q] = my[r][q];
+            const float* bx = boxes + nl * 6;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lb[slot][q] = bx[q];
+            lb[slot][6] = axis_scale(bx[2], bx[5], D, cd);
+        }
+    }
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int q = 0; q < 8; ++q) t += gcnt[q];
+        lcount = t;
+    }
+    __syncthreads();
+    const int nlist = lcount;
+    for (int64_t c = c0; c < c1; ++c) {
+        const int64_t idx = c * 256 + threadIdx.x;
+        const bool active = idx < (int64_t)D * CV;
+        const int Z = active ? (int)(idx / CV) : 0;
+        const int cv = active ? (int)(idx - (int64_t)Z * CV) : 0;
+        const int zw0 = (int)min<int64_t>((c * 256 + wave * 64) / CV, D - 1);
+        float acc[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
+        for (int e = 0; e < nlist; ++e) {
+            const int64_t n = ln[e];
+            const uint64_t myt = lm[e][0], myb = lm[e][1], mxl = lm[e][2], mxr = lm[e][3];
+            const float y1 = lb[e][0], x1 = lb[e][1], z1 = lb[e][2], y2 = lb[e][3], x2 = lb[e][4], z2 = lb[e][5];
+            const float zsc = lb[e][6];
+            uint64_t mzf = 0, mzk = 0;
+            if (zpw > 0) {
+                const float in_zl = axis_coord(z1, z2, D, cd, lane, zsc);
+                const bool vz = lane < cd && !(in_zl < 0 || in_zl > (float)(D - 1));
+                const int fzl = method == 1 ? (int)roundf(in_zl) : (int)floorf(in_zl);
+                const int kzl = (int)ceilf(in_zl);
+                for (int g = 0; g < zpw; ++g) {
+                    const int Zg = zw0 + g;
+                    const uint64_t f = __ballot(vz && fzl == Zg);
+                    const uint64_t k = method == 1 ? 0ull : __ballot(vz && kzl == Zg);
+                    if (active && Z == Zg) {
+                        mzf = f;
+                        mzk = k;
+                    }
+                }
+                if (__ballot((mzf | mzk) != 0) == 0) continue;      // wave-uniform skip
+            } else {
+                for (int i = 0; i < cd && active; ++i) {
+                    const float in_z = axis_coord(z1, z2, D, cd, i, zsc);
+                    if (in_z < 0 || in_z > (float)(D - 1)) continue;
+                    if (method == 1) {
+                        if ((int)roundf(in_z) == Z) mzf |= 1ull << i;
+                        continue;
+                    }
+                    if ((int)floorf(in_z) == Z) mzf |= 1ull << i;
+                    if ((int)ceilf(in_z) == Z) mzk |= 1ull << i;
+                }
+            }
+            const float* gn = grads + (size_t)n * ch * cw * cd * C + (size_t)cv * VEC;
+            if (method == 1) {                          // nearest: img[ny,nx,nz] += g
+                for (uint64_t m1 = myt; m1; m1 &= m1 - 1)
+                    for (uint64_t m2 = mxl; m2; m2 &= m2 - 1) {
+                        const float* gyx = gn + ((size_t)__builtin_ctzll(m1) * cw + __builtin_ctzll(m2)) * cd * C;
+                        for (uint64_t m3 = mzf; m3; m3 &= m3 - 1) {
+                            const float* gr = gyx + (size_t)__builtin_ctzll(m3) * C;
+#pragma unroll
+                            for (int q = 0; q < VEC; ++q) acc[q] += gr[q];
+                        }
+                    }
+                continue;
+            }
+            const float ysc = axis_scale(y1, y2, H, ch), xsc = axis_scale(x1, x2, W, cw);
+            for (uint64_t m1 = myt | myb; m1; m1 &= m1 - 1) {
+                const int iy = __builtin_ctzll(m1);
+                const float in_y = axis_coord(y1, y2, H, ch, iy, ysc);
+                const float yli = in_y - floorf(in_y);
+                for (int a = 0; a < 2; ++a) {
+                    if (!(((a ? myb : myt) >> iy) & 1)) continue;
+                    const float wy = a ? yli : 1.0f - yli;
+                    for (uint64_t m2 = mxl | mxr; m2; m2 &= m2 - 1) {
+                        const int ix = __builtin_ctzll(m2);
+                        const float in_x = axis_coord(x1, x2, W, cw, ix, xsc);
+                        const float xli = in_x - floorf(in_x);
+                        for (int bb = 0; bb < 2; ++bb) {
+                            if (!(((bb ? mxr : mxl) >> ix) & 1)) continue;
+                            const float wyx = wy * (bb ? xli : 1.0f - xli);
+                            const float* gyx = gn + ((size_t)iy * cw + ix) * cd * C;
+                            for (uint64_t m3 = mzf | mzk; m3; m3 &= m3 - 1) {
+                                const int iz = __builtin_ctzll(m3);
+                                const float in_z = axis_coord(z1, z2, D, cd, iz, zsc);
+                                const float zli = in_z - floorf(in_z);
+                                const float* gr = gyx + (size_t)iz * C;
+                                float gv[VEC];
+#pragma unroll
+                                for (int q = 0; q < VEC; ++q) gv[q] = gr[q];
+                                for (int cc = 0; cc < 2; ++cc) {
+                                    if (!(((cc ? mzk : mzf) >> iz) & 1)) continue;
+                                    const float w = wyx * (cc ? zli : 1.0f - zli);
+#pragma unroll
+                                    for (int q = 0; q < VEC; ++q) acc[q] += gv[q] * w;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (active) {
+            float* dst = gimg + ((((size_t)b * H + Y) * W + X) * D + Z) * C + (size_t)cv * VEC;
+            if constexpr (VEC == 4)
+                *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            else
+                dst[0] = acc[0];
+        }
+    }
+}
+
+// launch of the deterministic grad_image into one image set: the column-list
+// kernel when the boxes fit its list, else crop_bwd_det_kernel
+static void launch_det_bwd(const float* grads, const float* boxes, const int32_t* box_ind, int64_t N, int ch,
+                           int cw, int cd, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C, int method,
+                           float* gimg, hipStream_t s) {
+    const bool v4 = (C & 3) == 0;
+    const int64_t cvn = v4 ? C / 4 : C;
+    const int64_t nchunks = (D * cvn + 255) / 256;
+    if (N <= DET_CAP) {
+        const int64_t bpc = (nchunks + DET_CHUNKS - 1) / DET_CHUNKS;
+        const int64_t nblk = B * H * W * bpc;
+        if (v4)
+            hipLaunchKernelGGL(crop_bwd_det_col_kernel<4>, dim3((unsigned)nblk), dim3(256), 0, s, grads, boxes,
+                               box_ind, N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, gimg);
+        else
+            hipLaunchKernelGGL(crop_bwd_det_col_kernel<1>, dim3((unsigned)nblk), dim3(256), 0, s, grads, boxes,
+                               box_ind, N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, gimg);
+        return;
+    }
+    const int64_t nblk = B * H * W * nchunks;
+    const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);
+    if (v4)
+        hipLaunchKernelGGL(crop_bwd_det_kernel<4>, dim3(grid), dim3(256), 0, s, grads, boxes, box_ind, N, ch, cw,
+                           cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, nchunks, gimg);
+    else
+        hipLaunchKernelGGL(crop_bwd_det_kernel<1>, dim3(grid), dim3(256), 0, s, grads, boxes, box_ind, N, ch, cw,
+                           cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, nchunks, gimg);
 }
 
 // CropAndResize3DGradBoxes with the wheel's compiled formulas (DESIGN.md A.4,
@@ -1429,17 +1702,7 @@ extern "C" int m3d_crop_and_resize3d_bwd_image(const float* grads, const float* 
     const int64_t total = N * ch * cw * cd;
     if (deterministic == 1 && B > 0 && ch <= 64 && cw <= 64 && cd <= 64) {
         // destination-owned sums in the replay order: writes every voxel (no zero fill)
-        const bool v4 = (C & 3) == 0;
-        const int64_t cvn = v4 ? C / 4 : C;
-        const int64_t bpc = (D * cvn + 255) / 256;
-        const int64_t nblk = B * H * W * bpc;
-        const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);
-        if (v4)
-            hipLaunchKernelGGL(crop_bwd_det_kernel<4>, dim3(grid), dim3(256), 0, st(s), grads, boxes, box_ind,
-                               N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, grad_image);
-        else
-            hipLaunchKernelGGL(crop_bwd_det_kernel<1>, dim3(grid), dim3(256), 0, st(s), grads, boxes, box_ind,
-                               N, ch, cw, cd, (int)B, (int)H, (int)W, (int)D, (int)C, method, bpc, grad_image);
+        launch_det_bwd(grads, boxes, box_ind, N, ch, cw, cd, B, H, W, D, C, method, grad_image, st(s));
         return check_launch("crop_bwd_det_kernel");
     }
     if (hipMemsetAsync(grad_image, 0, sizeof(float) * (size_t)(B * H * W * D * C), st(s)) !=
@@ -1725,18 +1988,8 @@ extern "C" int m3d_pyramid_roi_align3d_bwd_det(const float* grad_out, const floa
                 return check_launch("memset gmaps");
             continue;
         }
-        const bool v4 = (C & 3) == 0;
-        const int64_t cvn = v4 ? C / 4 : C;
-        const int64_t bpc = (D * cvn + 255) / 256;
-        const unsigned grid = (unsigned)std::min<int64_t>(B * H * W * bpc, 1 << 20);
-        if (v4)
-            hipLaunchKernelGGL(crop_bwd_det_kernel<4>, dim3(grid), dim3(256), 0, st(s), grad_out, boxes_adj,
-                               box_ind_ws + l * BN, BN, ph, pw, pd, (int)B, (int)H, (int)W, (int)D, (int)C, 0, bpc,
-                               gmaps[l]);
-        else
-            hipLaunchKernelGGL(crop_bwd_det_kernel<1>, dim3(grid), dim3(256), 0, st(s), grad_out, boxes_adj,
-                               box_ind_ws + l * BN, BN, ph, pw, pd, (int)B, (int)H, (int)W, (int)D, (int)C, 0, bpc,
-                               gmaps[l]);
+        launch_det_bwd(grad_out, boxes_adj, box_ind_ws + l * BN, BN, ph, pw, pd, B, H, W, D, C, 0, gmaps[l],
+                       st(s));
     }
     return check_launch("crop_bwd_det_kernel<pyr>");
 }
