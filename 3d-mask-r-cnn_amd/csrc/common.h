@@ -172,3 +172,6 @@ __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a
 #ifndef M3D_TUNE_ROI_PC
 #define M3D_TUNE_ROI_PC 0
 #endif
+#ifndef M3D_TUNE_X3AF
+#define M3D_TUNE_X3AF 0
+#endif

@@ -2566,10 +2566,25 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
 // alias and inserts no vmcnt(0) drain of the prefetch.  Same split, same MFMA
 // order: bit-identical to x3_gemm256_kernel.
 template <int N_> struct IC { static constexpr int v = N_; };
+// M3D_TUNE_X3AF (A/B bits): 1 static s_setprio 1 for waves 4-7, 2 s_setprio
+// around each step's MFMA cluster, 8 all six stages in ONE __shared__ array
 __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
+#if M3D_TUNE_X3AF & 8
+    __shared__ __attribute__((aligned(16))) char sAll[18 * G2_PL];
+    char* const sA0 = sAll;
+    char* const sA1 = sAll + 3 * G2_PL;
+    char* const sA2 = sAll + 6 * G2_PL;
+    char* const sB0 = sAll + 9 * G2_PL;
+    char* const sB1 = sAll + 12 * G2_PL;
+    char* const sB2 = sAll + 15 * G2_PL;
+#else
     __shared__ __attribute__((aligned(16))) char sA0[3 * G2_PL], sA1[3 * G2_PL], sA2[3 * G2_PL];
     __shared__ __attribute__((aligned(16))) char sB0[3 * G2_PL], sB1[3 * G2_PL], sB2[3 * G2_PL];
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if M3D_TUNE_X3AF & 1
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
     const int wm = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
     const int64_t nbx = (g.M + 255) / 256, nby = g.N / 256;
     const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
@@ -2657,6 +2672,9 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
             for (int pl = 0; pl < 3; ++pl)
                 bfr[j][pl] = *reinterpret_cast<const bf16x8*>(SB + pl * G2_PL + off);
         }
+#if M3D_TUNE_X3AF & 2
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int off = x3_off16(wm * 128 + i * 32 + l32, h);
@@ -2674,6 +2692,9 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
             }
         }
+#if M3D_TUNE_X3AF & 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
     };
     // stage kt % 3 and register set kt % 2 static: six steps per trip
     for (int kt = 0;;) {
