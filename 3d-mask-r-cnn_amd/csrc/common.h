@@ -51,6 +51,12 @@ inline unsigned grid_for(int64_t n, int per_block, int64_t cap = 1 << 30) {
 __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
 
+// elementwise.hip: fold [3][rows][C] channel partials into s0 / s1 / s2 (+=)
+int bn_sums_reduce(const float* part, int64_t rows, int64_t C, float* s0, float* s1, float* s2, hipStream_t s);
+int64_t bn_act_bwd_rows(int64_t M, int64_t C);
+int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, const m3d_bn_bwd_t* bn,
+                      float* dx, int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
+
 }  // namespace m3d
 
 // ---- tuning constants -------------------------------------------------------
@@ -174,4 +180,7 @@ __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a
 #endif
 #ifndef M3D_TUNE_X3AF
 #define M3D_TUNE_X3AF 0
+#endif
+#ifndef M3D_TUNE_X3_256_MIN_TILES
+#define M3D_TUNE_X3_256_MIN_TILES 256
 #endif

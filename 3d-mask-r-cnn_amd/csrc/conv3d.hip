@@ -81,7 +81,24 @@ struct Epi {
     float* yh;
     int hlo, dl;
     int deconv = 0;   // > 0: 2x2x2 stride-2 transposed conv, n = tap * deconv + o
+    // fused BN-ReLU backward of the unit that produced this data gradient's
+    // input (m3d_conv3d_bwd_data_bn): the stored value t (after accumulate) is
+    // the unit's output gradient; written instead are dz = act'(t) * scale
+    // (into y), dpre = act'(t) (into fdres, if set), and per-tile channel sums
+    // of dpre, dpre * xhat, dz (rows of fpart, [3][rows][N]) -- the maths of
+    // bn_act_bwd_kernel
+    int fbn = 0, frelu = 0;
+    const float* fy = nullptr;
+    const float* fz = nullptr;
+    const float* fscale = nullptr;
+    const float* fmean = nullptr;
+    const float* frstd = nullptr;
+    float* fdres = nullptr;
+    float* fpart = nullptr;
+    int64_t fprows = 0;           // partial rows (stride of the three sum planes)
 };
+
+
 
 // activation codes (Epi::relu): 0 none, 1 ReLU, 2 sigmoid (mrcnn_mask)
 __device__ __forceinline__ float act(int code, float v) {
@@ -235,6 +252,39 @@ __device__ __forceinline__ void epi_store(const ConvP& p, const Epi& e, int64_t 
 // element-wise): 16-byte loads / stores when the row strides allow it.
 __device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast<const float4*>(q); }
 __device__ __forceinline__ void st4(float* q, const float4& v) { *reinterpret_cast<float4*>(q) = v; }
+
+// The fused BN-act backward of four channels n..n+3 of row m (simple rows):
+// bn_act_bwd_kernel's per-element maths, sums accumulated in s[3][4].
+__device__ __forceinline__ void epi_bnbwd4(const Epi& e, int64_t m, int n, float4 t, float (&s)[3][4]) {
+    const int64_t off = m * e.ldy + n;
+    float g[4] = {t.x, t.y, t.z, t.w};
+    if (e.frelu) {
+        const float4 y4 = ld4(e.fy + off);
+        if (!(y4.x > 0.f)) g[0] = 0.f;
+        if (!(y4.y > 0.f)) g[1] = 0.f;
+        if (!(y4.z > 0.f)) g[2] = 0.f;
+        if (!(y4.w > 0.f)) g[3] = 0.f;
+    }
+    float sc[4] = {1.f, 1.f, 1.f, 1.f}, mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {1.f, 1.f, 1.f, 1.f};
+    float zz[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e.fscale) { const float4 v = ld4(e.fscale + n); sc[0] = v.x; sc[1] = v.y; sc[2] = v.z; sc[3] = v.w; }
+    if (e.fz) {
+        const float4 v = ld4(e.fz + off), a = ld4(e.fmean + n), b = ld4(e.frstd + n);
+        zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w;
+        mu[0] = a.x; mu[1] = a.y; mu[2] = a.z; mu[3] = a.w;
+        rs[0] = b.x; rs[1] = b.y; rs[2] = b.z; rs[3] = b.w;
+    }
+    float d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        d[q] = g[q] * sc[q];
+        s[0][q] += g[q];
+        s[1][q] += g[q] * ((zz[q] - mu[q]) * rs[q]);
+        s[2][q] += d[q];
+    }
+    st4(e.y + off, make_float4(d[0], d[1], d[2], d[3]));
+    if (e.fdres) st4(e.fdres + off, make_float4(g[0], g[1], g[2], g[3]));
+}
 
 __device__ __forceinline__ void epi_store4(const ConvP& p, const Epi& e, int64_t m, int n, float4 v) {
     if (e.split > 0 || (e.ldy & 3)) {
@@ -701,6 +751,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     // residual / accumulated-destination rows loaded before the staging (block-uniform)
     const bool pf = !PERSIST && M3D_EPI_PREFETCH && e.simple && e.split <= 0 && !(e.ldy & 3) &&
                     ((e.res_mode == 1 && !e.accumulate) || (e.res_mode == 0 && e.accumulate));
+    float fs[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // fused BN sums
     for (int hf = 0; hf < HALVES; ++hf) {
         if (hf) __syncthreads();                 // previous half fully read
         if ((wm * TM * 32) / HR == hf) {
@@ -750,16 +801,51 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                 const int n = n0c + c4 * 4;
                 if ((HR * C4T % 256 == 0 || idx < HR * C4T) && m < p.M && n < p.N) {
                     const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
-                    if (PERSIST)   // plain C store (host-checked: simple epilogue, nothing fused)
+                    if (PERSIST) {  // plain C store (host-checked: simple epilogue, nothing fused)
                         st4(e.y + m * e.ldy + n, v);
-                    else if (pf)
+                    } else if (e.fbn) {   // (host-checked: simple rows, no bias / BN / residual / act)
+                        float4 t = v;
+                        if (e.accumulate) {
+                            const float4 o = pf ? pre[u] : ld4(e.y + m * e.ldy + n);
+                            t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
+                        }
+                        epi_bnbwd4(e, m, n, t, fs);
+                    } else if (pf) {
                         epi_store4_pre(p, e, m, n, v, pre[u]);
-                    else
+                    } else {
                         epi_store4(p, e, m, n, v);
+                    }
                 }
             }
         }
         e.y = y_next;
+    }
+    if constexpr (!PERSIST) {
+        if (e.fbn && e.fpart) {
+            // channel sums of the tile: threads t, t + C4T, ... hold channel quad t % C4T
+            __syncthreads();                     // staged tile fully read: Ts reused
+            float* red = Ts;                     // [256][12]
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) red[tid * 12 + a * 4 + q] = fs[a][q];
+            __syncthreads();
+            if (tid < C4T) {
+                float r[12];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) r[k] = red[tid * 12 + k];
+                for (int o = tid + C4T; o < 256; o += C4T)
+#pragma unroll
+                    for (int k = 0; k < 12; ++k) r[k] += red[o * 12 + k];
+                const int n = n0c + tid * 4;
+                const int64_t row = m0c / BM;
+                if (n < p.N)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        st4(e.fpart + ((int64_t)a * e.fprows + row) * p.N + n,
+                            make_float4(r[a * 4], r[a * 4 + 1], r[a * 4 + 2], r[a * 4 + 3]));
+            }
+        }
     }
     if (!more) break;
     L = Ln;
@@ -1080,7 +1166,7 @@ static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch)
         const int64_t tiles = (int64_t)grid.x * grid.y * nbatch;
         const int64_t resident = (int64_t)num_cus() * (gemm_nbuf_env() == 1 ? 3 : 2);
         const bool plain = e.simple && !e.bias && !e.scale && !e.res_mode && !e.relu && !e.z && !e.split &&
-                           !e.accumulate && !e.deconv && (e.ldy & 3) == 0;
+                           !e.accumulate && !e.deconv && !e.fbn && (e.ldy & 3) == 0;
         if constexpr (BT || BN >= 64) {
             if (conv_x3_env() && gemm_nbuf_env() == 1) {
                 if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
@@ -2029,6 +2115,107 @@ __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, c
                 *dst = v;
             }
         }
+    }
+}
+
+// The data-gradient output transform with the fused BN-ReLU backward of the
+// unit whose output dx is (m3d_conv3d_bwd_data_wino_bn): per element of dx
+// (after accumulate) bn_act_bwd_kernel's maths -- dz into dx, dpre into fdres
+// -- and per-block channel sums, one partial row per 256 (tile, channel)
+// pairs: N < 256 (256 % N == 0): the block's 256 / N tiles, row = block;
+// N % 256 == 0: one tile's 256 channels, row = tile.
+template <int NZ>
+__global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __restrict__ Mt, WinoGeom g, int N,
+                                                             Epi e) {
+    constexpr int P = ZT<NZ>::P;
+    const int tid = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+    const bool valid = i < g.T * N;
+    const int n = (int)(i % N);
+    const int64_t t = i / N;
+    float sp = 0.f, sx = 0.f, sz = 0.f;
+    if (valid) {
+        int b, ty, tx, tz;
+        tile_coords(t, g, b, ty, tx, tz);
+        const int64_t stride = g.T * N;
+        const float* src = Mt + t * N + n;
+        float m[4][4][P];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
+        float r1[4][4][NZ];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
+        float r2[4][2][NZ];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int k = 0; k < NZ; ++k)
+                at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
+        float o[2][2][NZ];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int k = 0; k < NZ; ++k)
+                at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
+        const float sc = e.fscale ? e.fscale[n] : 1.0f;
+        const float mu = e.fz ? e.fmean[n] : 0.0f, rs = e.fz ? e.frstd[n] : 1.0f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int y = 2 * ty + a;
+            if (y >= g.H) continue;
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                const int xx = 2 * tx + bb;
+                if (xx >= g.W) continue;
+#pragma unroll
+                for (int k = 0; k < NZ; ++k) {
+                    const int z = NZ * tz + k;
+                    if (z >= g.D) continue;
+                    const int64_t off = ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * e.ldy + n;
+                    float gv = o[a][bb][k];
+                    if (e.accumulate) gv += e.y[off];
+                    if (e.frelu && !(e.fy[off] > 0.f)) gv = 0.f;
+                    const float d = gv * sc;
+                    sp += gv;
+                    sx += gv * (((e.fz ? e.fz[off] : 0.0f) - mu) * rs);
+                    sz += d;
+                    e.y[off] = d;
+                    if (e.fdres) e.fdres[off] = gv;
+                }
+            }
+        }
+    }
+    if (!e.fpart) return;                        // (block-uniform)
+    if (N % 256 == 0) {
+        if (valid) {
+            e.fpart[(0 * e.fprows + t) * N + n] = sp;
+            e.fpart[(1 * e.fprows + t) * N + n] = sx;
+            e.fpart[(2 * e.fprows + t) * N + n] = sz;
+        }
+        return;
+    }
+    __shared__ float red[3][256];
+    red[0][tid] = sp;
+    red[1][tid] = sx;
+    red[2][tid] = sz;
+    __syncthreads();
+    if (tid < N) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+        for (int q = tid; q < 256; q += N) {
+            a0 += red[0][q];
+            a1 += red[1][q];
+            a2 += red[2][q];
+        }
+        const int64_t row = blockIdx.x;
+        e.fpart[(0 * e.fprows + row) * N + tid] = a0;
+        e.fpart[(1 * e.fprows + row) * N + tid] = a1;
+        e.fpart[(2 * e.fprows + row) * N + tid] = a2;
     }
 }
 
@@ -3881,11 +4068,32 @@ extern "C" int m3d_conv3d_fwd(const float* x, int64_t B, int64_t H, int64_t W, i
                               y, ldy, y2, ldy2, split_n, s);
 }
 
+static int bwd_data_direct(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                           int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
+                           int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dx,
+                           int32_t accumulate, hipStream_t s, const Epi* fb, int64_t* fb_rows);
+
 extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, int64_t H,
                                    int64_t W, int64_t D, int64_t Cin, int32_t kh, int32_t kw,
                                    int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
                                    int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px,
                                    int32_t pz, float* dx, int32_t accumulate, m3d_stream_t s) {
+    return bwd_data_direct(dz, w, B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px, pz, dx,
+                           accumulate, st(s), nullptr, nullptr);
+}
+
+// the output-tile height dispatch_gemm picks for a GEMM of N columns (rows of
+// the fused BN backward's channel partials: one per tile row)
+static int dispatch_bm(const ConvP& p, int nbatch = 1) {
+    if (p.N <= 64) return 128;
+    const int64_t blocks128 = ((p.M + 127) / 128) * ((p.N + 127) / 128) * nbatch;
+    return blocks128 < 512 ? 64 : 128;
+}
+
+static int bwd_data_direct(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                           int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
+                           int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dx,
+                           int32_t accumulate, hipStream_t hs, const Epi* fb, int64_t* fb_rows) {
     int rc = conv_check(B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
     if (rc) return rc;
     if (Cout % 32) return einval("conv3d bwd-data: Cout must be a multiple of 32");
@@ -3894,15 +4102,17 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
     if (!unit && (sy != 1 || sx != 1 || sz != 1))
         return einval("conv3d bwd-data: strided convs supported for 1x1x1 kernels only");
     if (per_item(B, H * W * D, Cin, OH * OW * OD, Cout)) {
+        if (fb) return einval("conv3d bwd-data (fused BN backward): batch past the 32-bit operand bound");
         for (int64_t b = 0; b < B; ++b) {
-            rc = m3d_conv3d_bwd_data(dz + b * OH * OW * OD * Cout, w, 1, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
-                                     sy, sx, sz, py, px, pz, dx + b * H * W * D * Cin, accumulate, s);
+            rc = bwd_data_direct(dz + b * OH * OW * OD * Cout, w, 1, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
+                                 sy, sx, sz, py, px, pz, dx + b * H * W * D * Cin, accumulate, hs, nullptr, nullptr);
             if (rc) return rc;
         }
         return M3D_OK;
     }
     ConvP p{};
     Epi e{};
+    if (fb) e = *fb;
     e.y = dx;
     e.ldy = Cin;
     e.accumulate = accumulate;
@@ -3935,8 +4145,63 @@ extern "C" int m3d_conv3d_bwd_data(const float* dz, const float* w, int64_t B, i
         e.simple = 1;
     }
     p.M = (int64_t)p.B * p.OH * p.OW * p.OD;
-    dispatch_gemm<true, true>(p, e, st(s));
+    if (fb) {
+        if (!e.simple) return einval("conv3d bwd-data (fused BN backward): strided convs unsupported");
+        e.fprows = (p.M + dispatch_bm(p) - 1) / dispatch_bm(p);
+        if (fb_rows) *fb_rows = e.fprows;
+    }
+    dispatch_gemm<true, true>(p, e, hs);
     return check_launch("conv_gemm_kernel(bwd-data)");
+}
+
+// ---- data gradients with the fused BN-ReLU backward of the producing unit -----
+static int bn_fuse_epi(const m3d_bn_bwd_t* bn, int64_t C, void* ws, size_t ws_bytes, int64_t rows, Epi& e) {
+    if (!bn) return einval("bwd-data (fused BN backward): null descriptor");
+    if (bn->relu && !bn->y) return einval("bwd-data (fused BN backward): relu needs y");
+    if (bn->sum_dpre_xhat && !(bn->z && bn->mean && bn->rstd))
+        return einval("bwd-data (fused BN backward): xhat sums need z, mean and rstd");
+    if (C % 4) return einval("bwd-data (fused BN backward): C must be a multiple of 4");
+    const bool sums = bn->sum_dpre || bn->sum_dpre_xhat || bn->sum_dz;
+    if (sums && ws_bytes < sizeof(float) * 3 * (size_t)rows * (size_t)C)
+        return einval("bwd-data (fused BN backward): workspace too small");
+    e.fbn = 1;
+    e.frelu = bn->relu ? 1 : 0;
+    e.fy = bn->y;
+    e.fz = bn->sum_dpre_xhat ? bn->z : nullptr;
+    e.fscale = bn->scale;
+    e.fmean = bn->mean;
+    e.frstd = bn->rstd;
+    e.fdres = bn->dres;
+    e.fpart = sums ? (float*)ws : nullptr;
+    e.fprows = rows;
+    return M3D_OK;
+}
+
+// rows of channel partials either fused form writes for an input grid of M voxels (upper bound)
+static int64_t bn_fuse_rows(int64_t B, int64_t H, int64_t W, int64_t D, int64_t C) {
+    const int64_t M = B * H * W * D;
+    const int64_t t2 = B * ((H + 1) / 2) * ((W + 1) / 2) * ((D + 1) / 2);   // Winograd tiles, NZ >= 2
+    return std::max<int64_t>(std::max<int64_t>((M + 63) / 64, t2), bn_act_bwd_rows(M, C));
+}
+
+extern "C" size_t m3d_bn_bwd_fused_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t C) {
+    if (C <= 0) C = 4;
+    return sizeof(float) * 3 * (size_t)bn_fuse_rows(B, H, W, D, C) * (size_t)C;
+}
+
+extern "C" int m3d_conv3d_bwd_data_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                      int64_t Cin, int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH,
+                                      int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz, int32_t py,
+                                      int32_t px, int32_t pz, float* dx, int32_t accumulate, const m3d_bn_bwd_t* bn,
+                                      void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    Epi e{};
+    int rc = bn_fuse_epi(bn, Cin, workspace, ws_bytes, bn_fuse_rows(B, H, W, D, Cin), e);
+    if (rc) return rc;
+    int64_t rows = 0;
+    rc = bwd_data_direct(dz, w, B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px, pz, dx, accumulate,
+                         st(s), &e, &rows);
+    if (rc) return rc;
+    return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, st(s));
 }
 
 // ---- split-K form of the 1x1x1 direct convs whose tiles do not fill the chip --
@@ -4068,6 +4333,45 @@ extern "C" int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64
     e.simple = (sy == 1 && sx == 1 && sz == 1 && H == OH && W == OW && D == OD);
     hipLaunchKernelGGL(splitk_epi_kernel, dim3(grid_for(M * Cin / 4, 256)), dim3(256), 0, st(s), part, sp, p, e);
     return check_launch("splitk_epi_kernel(bwd-data)");
+}
+
+// the split-K form with the fused BN-ReLU backward of the unit whose output dx
+// is: the K-slice reduce is bn_act_bwd_kernel summing the slices (stride 1 only)
+extern "C" int m3d_conv3d_bwd_data_splitk_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                             int64_t D, int64_t Cin, int64_t Cout, float* dx, int32_t accumulate,
+                                             int32_t splits, void* workspace, size_t ws_bytes,
+                                             const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes,
+                                             m3d_stream_t s) {
+    Epi chk{};
+    int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, bn_fuse_rows(B, H, W, D, Cin), chk);
+    if (rc) return rc;
+    const int64_t M = B * H * W * D;
+    if (splits <= 1) return m3d_conv3d_bwd_data_bn(dz, w, B, H, W, D, Cin, 1, 1, 1, Cout, H, W, D, 1, 1, 1, 0, 0,
+                                                   0, dx, accumulate, bn, bn_ws, bn_ws_bytes, s);
+    if (per_item(B, H * W * D, Cin, H * W * D, Cout))
+        return einval("conv3d bwd-data split-K (fused BN backward): batch past the 32-bit operand bound");
+    rc = conv_check(B, H, W, D, Cin, 1, 1, 1, Cout, H, W, D, 1, 1, 1);
+    if (rc) return rc;
+    if (Cout % 32) return einval("conv3d bwd-data: Cout must be a multiple of 32");
+    if (splits > 64 || Cout % (32 * splits)) return einval("conv3d split-K: Cout must be a multiple of 32 * splits");
+    if (!workspace || ws_bytes < sizeof(float) * (size_t)splits * (size_t)M * (size_t)Cin)
+        return einval("conv3d split-K: workspace smaller than splits * M * Cin floats");
+    const int64_t slice = Cout / splits;
+    ConvP q{};
+    q.a = dz; q.B = (int)B; q.H = (int)H; q.W = (int)W; q.D = (int)D; q.C = (int)Cout;
+    q.OH = (int)H; q.OW = (int)W; q.OD = (int)D;
+    q.kh = q.kw = q.kd = 1; q.sy = q.sx = q.sz = 1;
+    q.M = M; q.K = (int)slice; q.w = w; q.N = (int)Cin; q.flip = 1;
+    q.bsa = slice; q.bsw = slice; q.bsy = M * Cin;
+    Epi pe{};
+    pe.y = static_cast<float*>(workspace); pe.ldy = Cin; pe.simple = 1;
+    pe.YH = (int)H; pe.YW = (int)W; pe.YD = (int)D;
+    pe.ysy = pe.ysx = pe.ysz = 1;
+    dispatch_gemm<true, true>(q, pe, st(s), splits);
+    rc = check_launch("conv_gemm_kernel(bwd-data split-K, fused BN)");
+    if (rc) return rc;
+    return bn_act_bwd_splitk(static_cast<const float*>(workspace), splits, M, Cin, bn, dx, accumulate, bn_ws,
+                             bn_ws_bytes, st(s));
 }
 
 extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,
@@ -4314,7 +4618,10 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
         return;
     }
 #endif
-    if (af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
+    // M3D_TUNE_X3_256_MIN_TILES: fewest 256x256 tiles (all batches) for the
+    // 256-kernel; below it the 128x128 x3_gemm_kernel fills the chip better
+    const int64_t t256n = ((T + 255) / 256) * (N / 256) * P;
+    if (af32 && x3_256_env() && N % 256 == 0 && T >= 256 && t256n >= M3D_TUNE_X3_256_MIN_TILES) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
         hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
@@ -4607,7 +4914,7 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t s, float* dx_halo = nullptr,
-                         int hlo = 0, bool v_ready = false);
+                         int hlo = 0, bool v_ready = false, const Epi* fb = nullptr);
 
 // The same two entry points for convs that share one kernel across calls (the
 // RPN head's rpn_conv_shared1 on P2..P6, core/models.py:512-557): with
@@ -4637,13 +4944,39 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s));
 }
 
+extern "C" int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                           int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
+                                           int32_t accumulate, void* workspace, size_t ws_bytes, int32_t v_ready,
+                                           const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes,
+                                           m3d_stream_t s) {
+    if (Cin % 256 != 0 && 256 % Cin != 0)
+        return einval("conv3d winograd bwd-data (fused BN backward): Cin must divide 256 or be a multiple of it");
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout))
+        return einval("conv3d winograd bwd-data (fused BN backward): batch past the 32-bit operand bound");
+    const int nz = wino_dgrad_nz();
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
+    const int64_t rows = Cin % 256 == 0 ? g.T : (g.T * Cin + 255) / 256;
+    Epi e{};
+    int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
+    if (rc) return rc;
+    rc = bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s), nullptr, 0,
+                       v_ready != 0, &e);
+    if (rc) return rc;
+    return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, st(s));
+}
+
 // the data-gradient output transform: dx over the (halo-extended) grid, or,
 // for a depth slab with dx_halo, interior planes into dx (depth dl) and the
 // neighbours' planes into dx_halo [B][H][W][2][C]
 static void wino_dgrad_out(const float* Mt, const WinoGeom& g, int C, float* dx, int accumulate,
-                           float* dx_halo, int hlo, int dl, int nz, hipStream_t hs) {
+                           float* dx_halo, int hlo, int dl, int nz, hipStream_t hs, const Epi* fb = nullptr) {
     Epi o{};
+    if (fb) o = *fb;                 // the fused BN backward's fields
     o.y = dx; o.ldy = C; o.accumulate = accumulate;
+    if (fb) {
+        WINO_LAUNCH_NZ(nz, wino_output_bn_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+        return;
+    }
     if (dx_halo) {
         o.yh = dx_halo; o.hlo = hlo; o.dl = dl;
         WINO_LAUNCH_NZ(nz, wino_output_halo_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
@@ -4654,7 +4987,8 @@ static void wino_dgrad_out(const float* Mt, const WinoGeom& g, int C, float* dx,
 
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
-                         void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo, bool v_ready) {
+                         void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo, bool v_ready,
+                         const Epi* fb) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -4685,7 +5019,7 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
             WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
                               (int)Cout, ws.U);
         wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), hs, af32);
-        wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs);
+        wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs, fb);
         return check_launch("conv3d winograd bwd-data (x3)");
     }
     WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
@@ -4697,7 +5031,7 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
     e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
     e.ysy = e.ysx = e.ysz = 1;
     dispatch_gemm<false, true>(p, e, hs, wino_points(nz));
-    wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs);
+    wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs, fb);
     return check_launch("conv3d winograd bwd-data");
 }
 

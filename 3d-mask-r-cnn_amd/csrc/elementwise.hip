@@ -262,11 +262,17 @@ __global__ void subsample221_kernel(const float4* __restrict__ src, int B, int H
 // block pass; gridDim.y channel groups of 4*T channels.  Each block writes its
 // per-channel partial sums to part[3][gridDim.x][C] (no contended atomics);
 // bn_sums_reduce_kernel then folds them in a fixed order (deterministic).
+// splits > 1: dy is the K-slice partials of a split-K data gradient (slice k
+// at dy + k * plane), summed in slice order as splitk_epi_kernel does; acc_dz:
+// dz holds the data gradient's earlier contribution, added after the slices
+// (the accumulated store's order) and overwritten in place by dz -- the fused
+// split-K form of m3d_conv3d_bwd_data_splitk + this kernel.
 __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ z,
     int64_t M, int C, int T, int relu, const float* __restrict__ scale,
-    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dz,
-    float* __restrict__ dres, int accumulate_res, int want_xhat, float* __restrict__ part) {
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* dz,
+    float* __restrict__ dres, int accumulate_res, int want_xhat, float* __restrict__ part,
+    int splits = 1, int64_t plane = 0, int acc_dz = 0) {
     const int R = 256 / T;
     const int tx = threadIdx.x % T, ty = threadIdx.x / T;
     const int c = (blockIdx.y * T + tx) * 4;
@@ -286,6 +292,14 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
                 const bool in = r < M;
                 const int64_t off = (in ? r : r0) * C + c;
                 g4[u] = *(const float4*)(dy + off);
+                for (int k = 1; k < splits; ++k) {
+                    const float4 t = *(const float4*)(dy + k * plane + off);
+                    g4[u].x += t.x; g4[u].y += t.y; g4[u].z += t.z; g4[u].w += t.w;
+                }
+                if (acc_dz) {
+                    const float4 t = *(const float4*)(dz + off);
+                    g4[u].x += t.x; g4[u].y += t.y; g4[u].z += t.z; g4[u].w += t.w;
+                }
                 y4[u] = relu ? *(const float4*)(y + off) : make_float4(1.f, 1.f, 1.f, 1.f);
                 z4[u] = want_xhat ? *(const float4*)(z + off) : make_float4(0.f, 0.f, 0.f, 0.f);
                 a4[u] = (dres && accumulate_res) ? *(const float4*)(dres + off) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -784,6 +798,43 @@ extern "C" int m3d_bn_affine(const float* gamma, const float* beta, const float*
                        mean, var, eps, (int)C, scale, shift, rstd);
     return check_launch("bn_affine_kernel");
 }
+
+namespace m3d {
+// bn_act_bwd_kernel's partial rows for M rows of C channels
+int64_t bn_act_bwd_rows(int64_t M, int64_t C) {
+    int T, groups;
+    int64_t gx;
+    bn_grid(M, C, T, groups, gx);
+    return gx;
+}
+
+// The split-K data gradient's reduce with the fused BN-ReLU backward: dx =
+// sum of the K-slice partials (+ dx when accumulating), then bn_act_bwd_kernel's
+// maths -- dz into dx, dpre into bn->dres, the channel sums via the workspace.
+int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, const m3d_bn_bwd_t* bn,
+                      float* dx, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+    int T, groups;
+    int64_t gx;
+    bn_grid(M, C, T, groups, gx);
+    const bool sums = bn->sum_dpre || bn->sum_dpre_xhat || bn->sum_dz;
+    if (sums && ws_bytes < sizeof(float) * 3 * (size_t)gx * (size_t)C)
+        return einval("bwd-data split-K (fused BN backward): workspace too small");
+    hipLaunchKernelGGL(bn_act_bwd_kernel, dim3((unsigned)gx, (unsigned)groups), dim3(256), 0, s, slices, bn->y,
+                       bn->z, M, (int)C, T, bn->relu ? 1 : 0, bn->scale, bn->mean, bn->rstd, dx, bn->dres, 0,
+                       bn->sum_dpre_xhat ? 1 : 0, sums ? (float*)ws : nullptr, splits, M * C, accumulate ? 1 : 0);
+    int rc = check_launch("bn_act_bwd_kernel(split-K)");
+    if (rc || !sums) return rc;
+    return bn_sums_reduce((const float*)ws, gx, C, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, s);
+}
+
+// fold [3][rows][C] channel partials into s0 / s1 / s2 (+=, fixed order; NULL: skipped)
+int bn_sums_reduce(const float* part, int64_t rows, int64_t C, float* s0, float* s1, float* s2, hipStream_t s) {
+    if (!(s0 || s1 || s2) || rows <= 0) return M3D_OK;
+    hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 15) / 16), 3), dim3(256), 0, s, part,
+                       (int)rows, (int)C, s0, s1, s2);
+    return check_launch("bn_sums_reduce_kernel(fused)");
+}
+}  // namespace m3d
 
 extern "C" size_t m3d_bn_act_bwd_workspace_bytes(int64_t M, int64_t C) {
     int T, groups;

@@ -24,6 +24,15 @@ c_f = ctypes.c_float
 c_p = ctypes.c_void_p
 c_sz = ctypes.c_size_t
 
+
+class BnBwd(ctypes.Structure):
+    """m3d_bn_bwd_t (include/m3d.h): the producing unit's BN-ReLU backward fused
+    into a data-gradient epilogue."""
+    _fields_ = [("y", ctypes.c_void_p), ("z", ctypes.c_void_p), ("scale", ctypes.c_void_p),
+                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("relu", ctypes.c_int32),
+                ("dres", ctypes.c_void_p), ("sum_dpre", ctypes.c_void_p), ("sum_dpre_xhat", ctypes.c_void_p),
+                ("sum_dz", ctypes.c_void_p)]
+
 # name -> argtypes (all return int unless listed in _RESTYPES)
 _SIGS = {
     "m3d_last_error": [],
@@ -67,6 +76,14 @@ _SIGS = {
                               c_i32, c_p, c_p, c_p, c_sz, c_i32, c_p],
     "m3d_conv3d_bwd_data_wino_v": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p,
                                    c_sz, c_i32, c_p],
+    "m3d_bn_bwd_fused_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
+    "m3d_conv3d_bwd_data_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
+                               c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                               c_p, c_i32, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_wino_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32,
+                                    c_p, c_sz, c_i32, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_splitk_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32,
+                                      c_p, c_sz, c_p, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_data": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
                             c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                             c_p, c_i32, c_p],
@@ -158,7 +175,7 @@ _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_s
              "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_rpn_loss_workspace_bytes": c_sz,
-             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
+             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
              "m3d_get_deterministic": c_i32}
 

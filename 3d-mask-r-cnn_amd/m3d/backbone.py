@@ -13,7 +13,7 @@ import os
 
 import torch
 
-from .nn import GradLink, _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
+from .nn import BNFuse, GradLink, _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
 from .params import BNLayer, ConvLayer
 
 # the RPN head's shared conv transforms its weights once per pass for all
@@ -29,11 +29,11 @@ class _Unit:
         self.bn = BNLayer(store, bn_name, cout)
         self.stride, self.padding = tuple(stride), padding
 
-    def __call__(self, x, relu, residual=None, need_dx=True, link=None):
+    def __call__(self, x, relu, residual=None, need_dx=True, link=None, fuse=None, fuse_in=None):
         geo = conv_geom(tuple(x.shape[1:4]), self.conv.k, self.stride, self.padding)
         return conv_bn_act(x, self.conv, geo, relu, residual=residual,
                            res_mode=1 if residual is not None else 0, bn=self.bn, need_dx=need_dx,
-                           link=link)
+                           link=link, fuse=fuse, fuse_in=fuse_in)
 
 
 class _Block:
@@ -47,22 +47,29 @@ class _Block:
         self.c = _Unit(store, c + "2c", b + "2c", (1, 1, 1), f2, f3, (1, 1, 1), "valid")
         self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
 
-    def __call__(self, x, links=None):
+    def __call__(self, x, links=None, fuse_in=None, fuse_out=None):
+        """``fuse_in``: the BNFuse of the unit that made x, when this block is
+        x's only consumer (an identity block inside a stage: its 2a data
+        gradient, after the GradLink summed 2c's residual gradient, is x's whole
+        gradient); ``fuse_out``: this block's output unit's BNFuse for the next."""
         # the two gradients of x are summed by the bwd-data kernel (GradLink)
         # instead of an autograd add: identity block 2c's residual gradient
         # into 2a's data gradient; conv block shortcut's and 2a's data gradients
         x = x.contiguous()
         train = torch.is_grad_enabled() and x.requires_grad
+        # 2a -> 2b -> 2c: each unit's output has one consumer, whose data
+        # gradient applies its BN-ReLU backward (nn.BNFuse)
+        fa, fb = (BNFuse(), BNFuse()) if train else (None, None)
         if self.sc is None:
             link = GradLink("res", x, links) if train else None
-            y = self.a(x, relu=True, link=link)
-            y = self.b(y, relu=True)
-            return self.c(y, relu=True, residual=x, link=link)
+            y = self.a(x, relu=True, link=link, fuse=fa, fuse_in=fuse_in)
+            y = self.b(y, relu=True, fuse=fb, fuse_in=fa)
+            return self.c(y, relu=True, residual=x, link=link, fuse=fuse_out, fuse_in=fb)
         link = GradLink("dx2", x, links) if train else None
-        short = self.sc(x, relu=False, link=link)
-        y = self.a(x, relu=True, link=link)
-        y = self.b(y, relu=True)
-        return self.c(y, relu=True, residual=short)
+        short = self.sc(x, relu=False, link=link, fuse_in=fuse_in)
+        y = self.a(x, relu=True, link=link, fuse=fa, fuse_in=fuse_in)
+        y = self.b(y, relu=True, fuse=fb, fuse_in=fa)
+        return self.c(y, relu=True, residual=short, fuse=fuse_out, fuse_in=fb)
 
 
 class ResNet3D:
@@ -94,9 +101,15 @@ class ResNet3D:
         x = self.stem(image, relu=True, need_dx=False)
         c1 = x = max_pool3d(x, (3, 3, 3), (2, 2, 1), "same")
         outs = [c1]
+        train = torch.is_grad_enabled() and x.requires_grad
         for blocks in self.stages:
-            for blk in blocks:
-                x = blk(x, self.links)
+            # a block output feeding the next block of its stage has that block
+            # as its only consumer; a stage's last output also feeds the FPN
+            fuse = None
+            for i, blk in enumerate(blocks):
+                nxt = BNFuse() if train and i + 1 < len(blocks) else None
+                x = blk(x, self.links, fuse_in=fuse, fuse_out=nxt)
+                fuse = nxt
             outs.append(x)
         if not self.stage5:
             outs.append(None)
@@ -161,9 +174,10 @@ class RPNHead:
         wshare = {} if SHARE_WINO_WEIGHTS else None
         for p in feature_maps:
             g1 = conv_geom(tuple(p.shape[1:4]), (3, 3, 3), (1, 1, 1), "same")
-            s = conv_bn_act(p, self.shared1, g1, relu=True, wshare=wshare)
+            f1 = BNFuse() if torch.is_grad_enabled() else None     # shared1 -> shared2 only
+            s = conv_bn_act(p, self.shared1, g1, relu=True, wshare=wshare, fuse=f1)
             g2 = conv_geom(tuple(s.shape[1:4]), (1, 1, 1), (1, 1, 1), "valid")
-            shared.append(conv_bn_act(s, self.shared2, g2, relu=True))
+            shared.append(conv_bn_act(s, self.shared2, g2, relu=True, fuse_in=f1))
         if wshare is not None:
             wshare.pop("fwd", None)        # the forward's workspace is not needed past the loop
         apl = self.apl

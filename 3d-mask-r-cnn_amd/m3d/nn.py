@@ -8,6 +8,7 @@ gradients.  Layout is channels-last [B,H,W,D,C] throughout, as the reference.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 from dataclasses import dataclass
 
@@ -422,6 +423,83 @@ def _link_park(link, dx, acc):
     return dx
 
 
+# Fused BN-ReLU backward (m3d_conv3d_bwd_data_bn / _wino_bn): the data
+# gradient of a unit's sole consumer applies the unit's frozen-BN + ReLU backward
+# in its epilogue (dz and dres stored, the beta / gamma / bias sums reduced from
+# per-tile partials), so the unit's own backward skips bn_act_bwd -- one
+# read-modify-write pass over the activation gradient less per fused unit.
+# M3D_BN_FUSE=0 runs bn_act_bwd everywhere (A/B).
+BN_FUSE = os.environ.get("M3D_BN_FUSE", "1") != "0"
+
+
+class BNFuse:
+    """Hand-off of one unit's BN-ReLU backward to its consumer's data gradient.
+
+    The model wires it where the graph guarantees the consumer's data gradient
+    is the last contribution to the unit's output gradient: a block's 2a -> 2b
+    and 2b -> 2c, an identity block's input conv (whose GradLink already holds
+    the residual gradient), the RPN head's shared1 -> shared2.  The producer
+    arms it in forward; the consumer fuses when its data-gradient kernel has the
+    fused form and its result is final, and marks it ``done``; the producer's
+    backward then takes the incoming gradient as its dz (checked to be the
+    consumer's buffer: any other contribution raises instead of being lost)."""
+    __slots__ = ("armed", "done", "y", "z", "bn", "relu", "need_res", "grads", "buf", "dres", "name")
+
+    def __init__(self):
+        self.armed = self.done = False
+        self.y = self.z = self.bn = self.grads = self.buf = self.dres = None
+        self.relu = self.need_res = False
+        self.name = ""
+
+    def arm(self, y, z, bn, relu, need_res, grads, name):
+        self.armed, self.done = True, False
+        self.y, self.z, self.bn, self.relu, self.need_res, self.grads, self.name = \
+            y, z, bn, relu, need_res, grads, name
+        self.buf = self.dres = None
+
+    def clear(self):
+        self.armed = self.done = False
+        self.y = self.z = self.bn = self.grads = self.buf = self.dres = None
+
+    def descriptor(self, dres):
+        """The m3d_bn_bwd_t of the fused entry points (the tensors stay held by
+        this record and the caller's dres)."""
+        g = self.grads or {}
+        mean = rstd = scale = None
+        if self.bn is not None:
+            mean, rstd, scale = self.bn
+        d = _lib.BnBwd(ptr(self.y), ptr(self.z), ptr(scale), ptr(mean), ptr(rstd), 1 if self.relu else 0,
+                       ptr(dres), ptr(g.get("beta")), ptr(g.get("gamma") if self.z is not None else None),
+                       ptr(g.get("bias")))
+        return d
+
+
+def _per_item(B, vin, cin, vout, cout):
+    """csrc/conv3d.hip per_item(): batches whose operands pass the 32-bit bound
+    run one item at a time (the fused forms refuse those)."""
+    lim = int(os.environ.get("M3D_OPERAND_LIMIT", "0") or 0)
+    lim = (lim if 0 < lim < 0xFFFFFFF0 else 0xFFFFFFF0) // 4
+    return B > 1 and (B * vin * cin >= lim or B * vout * cout >= lim or B * vin > 0x7FFFFFFF
+                      or B * vout > 0x7FFFFFFF)
+
+
+def _fuse_final(link, x, acc):
+    """Is this data gradient the last contribution to x's gradient?  A linked x
+    (GradLink keyed by x) is final once the parked partner gradient was taken
+    (acc = 1); an unlinked one is final on its own (the model wires BNFuse only
+    to sole consumers)."""
+    linked = link is not None and link.key == (x.data_ptr(), tuple(x.shape))
+    return acc == 1 if linked else acc == 0
+
+
+def _bn_fuse_ws(rec, B, H, W, D, C, dev):
+    g = rec.grads or {}
+    if g.get("beta") is None and g.get("bias") is None and (g.get("gamma") is None or rec.z is None):
+        return None, 0
+    n = int(_L().m3d_bn_bwd_fused_workspace_bytes(B, H, W, D, C))
+    return torch.empty(n // 4 + 1, device=dev, dtype=torch.float32), n
+
+
 class _ConvBNAct(torch.autograd.Function):
     """y = act(BN_frozen(conv(x, w) + b) [+ residual]).
 
@@ -430,7 +508,7 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, w, b, bn, geo, relu, res_mode, grads, need_dx, link=None, halo=None,
-                wshare=None, name=""):
+                wshare=None, name="", fuse=None, fuse_in=None):
         t0 = _span()
         ctx.name = name
         B, H, W, D, Cin = x.shape
@@ -544,6 +622,18 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
+        # this unit's BN-ReLU backward handed to its consumer (BNFuse)
+        ctx.fuse = None
+        if (fuse is not None and BN_FUSE and grads is not None and (bn is not None or relu)
+                and Cout % 4 == 0):
+            fuse.arm(y, z, ctx.bn, relu, res_mode == 1, grads, name)
+            ctx.fuse = fuse
+        # ... and the producer's, applied in this unit's data gradient
+        ctx.fuse_in = None
+        if (fuse_in is not None and fuse_in.armed and need_dx and halo is None and wshare is None
+                and fuse_in.y is not None and fuse_in.y.data_ptr() == x.data_ptr()
+                and fuse_in.y.shape == x.shape):
+            ctx.fuse_in = fuse_in
         return y
 
     @staticmethod
@@ -562,13 +652,30 @@ class _ConvBNAct(torch.autograd.Function):
         logging = LAYER_LOG is not None
         direct = 2.0 * M * kh * kw * kd * Cin * Cout
         t0 = _span()
-        if trivial:
+        rec = ctx.fuse
+        ctx.fuse = None
+        fused_bn = rec is not None and rec.done
+        if fused_bn:
+            # the consumer's data gradient already applied this unit's BN-ReLU
+            # backward: dy is its dz buffer, dres and the BN / bias sums are written
+            if rec.buf is None or dy.data_ptr() != rec.buf.data_ptr() or dy.shape != rec.buf.shape:
+                raise RuntimeError(f"{ctx.name}: fused BN-ReLU backward was applied by its consumer, but the "
+                                   "output gradient has another contribution (the unit is not the consumer's "
+                                   "sole producer-consumer pair; see nn.BNFuse)")
+            dz = dy
+            dres = rec.dres
+            rec.clear()
+        elif trivial:
+            if rec is not None:
+                rec.clear()
             dz = dy
             dres = dy if need_res else None
             if grads.get("bias") is not None:
                 bn_act_bwd(dy, None, None, M, Cout, False, None, None, None, None, None, None, None,
                            grads["bias"])
         else:
+            if rec is not None:
+                rec.clear()
             dz = torch.empty_like(dy)
             dres = torch.empty_like(dy) if need_res else None
             mean = rstd = scale = None
@@ -576,7 +683,7 @@ class _ConvBNAct(torch.autograd.Function):
                 mean, rstd, scale = ctx.bn
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
-        if logging:
+        if logging and not fused_bn:
             nel = dy.numel() * (1 + (0 if trivial else 1 + (ctx.relu or ctx.bn is not None) +
                                      (z is not None) + (dres is not None and not trivial)))
             _log("bn_act_bwd", 0, 0, 4.0 * nel, "bwd_bn", ctx.name, t0)
@@ -630,6 +737,7 @@ class _ConvBNAct(torch.autograd.Function):
             td = _span()
             ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             dx = None
+            fused_nel = 0
             if ctx.need_dx:
                 dx, acc = _link_take(ctx.link, x)
                 if dx is None:
@@ -644,18 +752,33 @@ class _ConvBNAct(torch.autograd.Function):
                     if ctx.wshare is not None:      # may be held across calls: not the arena
                         ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
                     ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout))
-                    check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
-                                                       geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, stream()),
-                          "conv3d_bwd_data_wino")
+                    rec = ctx.fuse_in
+                    if (rec is not None and rec.armed and (Cin % 256 == 0 or 256 % Cin == 0)
+                            and not _per_item(B, H * W * max(D, OD), max(Cin, Cout), 0, 0)
+                            and _fuse_final(ctx.link, x, acc)):
+                        dres_f = torch.empty_like(x) if rec.need_res else None
+                        bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
+                        d = rec.descriptor(dres_f)
+                        check(L.m3d_conv3d_bwd_data_wino_bn(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD, geo.pad[2],
+                                                            ptr(dx), acc, ptr(ws), wsb, v_ready, ctypes.addressof(d),
+                                                            ptr(bws), bwsb, stream()), "conv3d_bwd_data_wino_bn")
+                        rec.buf, rec.dres, rec.done = dx, dres_f, True
+                        fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
+                    else:
+                        check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                           geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready,
+                                                           stream()), "conv3d_bwd_data_wino")
                     _shared_wino_release(ctx.wshare)
                 if logging:
                     _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_tile_z())),
-                         4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)), "bwd_data", ctx.name, td, "x3")
+                         4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel), "bwd_data", ctx.name,
+                         td, "x3")
                 dx = _link_park(ctx.link, dx, acc)
             _grad_done(grads, side)
             ctx.halo = None
+            ctx.fuse_in = None
             return (dx, (dres if need_res else None), None, None, None, None, None, None, None, None, None, None,
-                    None, None)
+                    None, None, None, None)
         if halo is not None and ctx.need_dx:
             raise ValueError("the stem's halo form has no data gradient (its input is the volume)")
         if grads.get("kernel") is not None:
@@ -678,6 +801,8 @@ class _ConvBNAct(torch.autograd.Function):
         link = ctx.link
         acc = 0
         td = _span()
+        rec = ctx.fuse_in
+        fused_nel = 0
         if ctx.need_dx:
             strided = any(s != 1 for s in geo.stride)
             dx, acc = _link_take(link, x)                     # dx = parked gradient + conv^T dz
@@ -696,17 +821,39 @@ class _ConvBNAct(torch.autograd.Function):
                 planes = _x3_planes(w, Cin, Cout, False)
                 check(L.m3d_conv3d_bwd_data_x3(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), stream()),
                       "conv3d_bwd_data_x3")
+            elif (nsk > 1 and rec is not None and rec.armed and not strided and (OH, OW, OD) == (H, W, D)
+                  and not _per_item(B, H * W * D, Cin, OH * OW * OD, cpad) and _fuse_final(link, x, acc)):
+                wsk = torch.empty((nsk, M * Cin), device=x.device, dtype=torch.float32)
+                dres_f = torch.empty_like(x) if rec.need_res else None
+                bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
+                d = rec.descriptor(dres_f)
+                check(L.m3d_conv3d_bwd_data_splitk_bn(ptr(dzd), ptr(wd), B, H, W, D, Cin, cpad, ptr(dx), acc, nsk,
+                                                      ptr(wsk), wsk.numel() * 4, ctypes.addressof(d), ptr(bws),
+                                                      bwsb, stream()), "conv3d_bwd_data_splitk_bn")
+                rec.buf, rec.dres, rec.done = dx, dres_f, True
+                fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
             elif nsk > 1:
                 wsk = torch.empty((nsk, M * Cin), device=x.device, dtype=torch.float32)
                 check(L.m3d_conv3d_bwd_data_splitk(ptr(dzd), ptr(wd), B, H, W, D, Cin, cpad, OH, OW, OD,
                                                    *geo.stride, ptr(dx), acc, nsk, ptr(wsk), wsk.numel() * 4,
                                                    stream()), "conv3d_bwd_data_splitk")
+            elif (rec is not None and rec.armed and not strided and (OH, OW, OD) == (H, W, D)
+                  and not _per_item(B, H * W * D, Cin, OH * OW * OD, cpad) and _fuse_final(link, x, acc)):
+                dres_f = torch.empty_like(x) if rec.need_res else None
+                bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
+                d = rec.descriptor(dres_f)
+                check(L.m3d_conv3d_bwd_data_bn(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW, OD,
+                                               *geo.stride, *geo.pad, ptr(dx), acc, ctypes.addressof(d), ptr(bws),
+                                               bwsb, stream()), "conv3d_bwd_data_bn")
+                rec.buf, rec.dres, rec.done = dx, dres_f, True
+                fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
             else:
                 check(L.m3d_conv3d_bwd_data(ptr(dzd), ptr(wd), B, H, W, D, Cin, kh, kw, kd, cpad, OH, OW,
                                             OD, *geo.stride, *geo.pad, ptr(dx), acc, stream()),
                       "conv3d_bwd_data")
             if logging:
-                _log(f"conv{kh}_dgrad", direct, direct, 4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc)),
+                _log(f"conv{kh}_dgrad", direct, direct,
+                     4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel),
                      "bwd_data", ctx.name, td, "x3" if dx_x3 else "f32")
             dx = _link_park(link, dx, acc)
         _grad_done(grads, side)
@@ -723,7 +870,8 @@ class _ConvBNAct(torch.autograd.Function):
                 check(L.m3d_upsample221_bwd(ptr(dres), rb, rh, rw, rd, rc, ptr(dr), 0, stream()),
                       "upsample221_bwd")
                 _log("upsample_bwd", 0, 0, 4.0 * (dres.numel() + dr.numel()), "bwd_data", ctx.name, tu)
-        return dx, dr, None, None, None, None, None, None, None, None, None, None, None, None
+        ctx.fuse_in = None
+        return dx, dr, None, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _stem_halo(geo, cin, cout, res_mode):
@@ -746,11 +894,13 @@ def _slab_extend(x, geo):
 
 
 def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None,
-                wshare=None):
+                wshare=None, fuse=None, fuse_in=None):
     """Functional entry: ``layer`` is a Conv3D parameter group from params.py.
     ``link``: a GradLink shared by the residual conv and the input conv of an
     identity block (see GradLink).  ``wshare``: a dict shared by the calls of
-    one kernel within a pass (see _shared_wino_ws)."""
+    one kernel within a pass (see _shared_wino_ws).  ``fuse`` / ``fuse_in``:
+    this unit's / its producer's BNFuse record (the caller guarantees this unit
+    is the producer's sole consumer; see BNFuse)."""
     w = layer.kernel.data
     b = layer.bias.data if layer.bias is not None else None
     grads = layer.grad_dict(bn) if torch.is_grad_enabled() else None   # inference: no z / grads
@@ -777,7 +927,7 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         x, geo = _slab_extend(x, geo)
     # the function must see at least one tensor requiring grad to be recorded
     y = _ConvBNAct.apply(x.contiguous(), residual, w, b, bnt, geo, relu, res_mode, grads,
-                         need_dx and x.requires_grad, link, halo, wshare, getattr(layer, "name", ""))
+                         need_dx and x.requires_grad, link, halo, wshare, getattr(layer, "name", ""), fuse, fuse_in)
     if RELU_CAPTURE is not None and relu:
         RELU_CAPTURE.setdefault(getattr(layer, "name", ""), []).append((y.detach() > 0).cpu())
     return y

@@ -373,6 +373,50 @@ int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_halo, int32_t
                                     const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
                                     int64_t Cout, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
 
+/* Data gradients with the producing unit's BN-ReLU backward fused into their
+ * epilogue (the bn_act_bwd pass of core/models.py:102-114 / 157-232 folded
+ * into the kernel that computes the unit's output gradient): the data
+ * gradient t = conv^T(dz) (+ dx when accumulate) of this conv's input x is the
+ * output gradient of the unit U that produced x = act(BN(z) [+ res]); instead
+ * of t, dx receives U's dz = act'(t) * scale, bn->dres (optional) receives
+ * dpre = act'(t) (U's residual gradient), and the channel sums of U's
+ * backward are added (+=, fixed order) into sum_dpre (beta), sum_dpre_xhat
+ * (gamma; needs z, mean, rstd) and sum_dz (bias) -- m3d_bn_act_bwd's results,
+ * without the round trip of t through HBM.  relu: y = U's output (mask y > 0);
+ * scale = NULL: no BN.  workspace: m3d_bn_bwd_fused_workspace_bytes(B, H, W,
+ * D, Cin) bytes of device scratch for the channel partials.
+ * m3d_conv3d_bwd_data_bn: stride-1 convs of m3d_conv3d_bwd_data (the direct
+ * implicit GEMM).  m3d_conv3d_bwd_data_wino_bn: m3d_conv3d_bwd_data_wino_v
+ * with Cin dividing 256 or a multiple of it.  m3d_conv3d_bwd_data_splitk_bn:
+ * m3d_conv3d_bwd_data_splitk of a stride-1 1x1x1 conv (OH,OW,OD = H,W,D), the
+ * K-slice reduce doing the BN-ReLU backward (splits <= 1: the one-pass form). */
+typedef struct m3d_bn_bwd {
+    const float* y;
+    const float* z;
+    const float* scale;
+    const float* mean;
+    const float* rstd;
+    int32_t relu;
+    float* dres;
+    float* sum_dpre;
+    float* sum_dpre_xhat;
+    float* sum_dz;
+} m3d_bn_bwd_t;
+size_t m3d_bn_bwd_fused_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t C);
+int m3d_conv3d_bwd_data_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                           int64_t Cin, int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH,
+                           int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz, int32_t py,
+                           int32_t px, int32_t pz, float* dx, int32_t accumulate, const m3d_bn_bwd_t* bn,
+                           void* workspace, size_t ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                                void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn,
+                                void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s);
+int m3d_conv3d_bwd_data_splitk_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                  int64_t Cin, int64_t Cout, float* dx, int32_t accumulate, int32_t splits,
+                                  void* workspace, size_t ws_bytes, const m3d_bn_bwd_t* bn, void* bn_ws,
+                                  size_t bn_ws_bytes, m3d_stream_t s);
+
 /* Plain batched fp32 GEMM on the same MFMA kernel: for b < batch,
  * C[b] = act(A[b] B[b] + bias) (+ C[b] if accumulate); A [M][K], B [K][N],
  * C [M][N] row-major, batches contiguous; N multiple of 4.  The Winograd

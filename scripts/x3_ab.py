@@ -25,10 +25,11 @@ for n in names:
     libs.append(L)
 dev = torch.device("cuda:0")
 res = {}
-for S in (128, 256):
-    nb, K, N = 96, 256, 512
-    q = S // 4
-    T = ((q + 1) // 2) ** 2 * ((S + 3) // 4)
+SHAPES = [("P2_128", 8192, 256, 512), ("P2_256", 65536, 256, 512), ("res2_128", 8192, 64, 64),
+          ("res3_128", 2048, 128, 128), ("res4_128", 512, 256, 256), ("res5_128", 128, 512, 512),
+          ("res4_256", 4096, 256, 256)]
+for S, T, K, N in SHAPES:
+    nb = 96
     g = torch.Generator(device=dev).manual_seed(5)
     A = torch.randn((nb, T, K), device=dev, generator=g)
     Bt = torch.randn((nb, N, K), device=dev, generator=g) * 0.05
