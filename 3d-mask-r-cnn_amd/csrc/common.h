@@ -178,6 +178,11 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_ROI_PC
 #define M3D_TUNE_ROI_PC 0
 #endif
+// PyramidROIAlign forward in the separable row form (row_fwd_kernel) for pools
+// of depth >= this (0: off)
+#ifndef M3D_TUNE_ROI_ROW
+#define M3D_TUNE_ROI_ROW 0
+#endif
 #ifndef M3D_TUNE_X3AF
 #define M3D_TUNE_X3AF 0
 #endif

@@ -254,26 +254,22 @@ __device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast
 __device__ __forceinline__ void st4(float* q, const float4& v) { *reinterpret_cast<float4*>(q) = v; }
 
 // The fused BN-act backward of four channels n..n+3 of row m (simple rows):
-// bn_act_bwd_kernel's per-element maths, sums accumulated in s[3][4].
-__device__ __forceinline__ void epi_bnbwd4(const Epi& e, int64_t m, int n, float4 t, float (&s)[3][4]) {
+// bn_act_bwd_kernel's per-element maths, sums accumulated in s[3][4].  The
+// caller loads y4 / z4 (and the channel's scale / mean / rstd in bn[3]) ahead
+// of the batch's stores: a load issued after a store to a possibly aliasing
+// address waits for it.
+__device__ __forceinline__ void epi_bnbwd4(const Epi& e, int64_t m, int n, float4 t, float4 y4, float4 z4,
+                                           const float4 (&bn)[3], float (&s)[3][4]) {
     const int64_t off = m * e.ldy + n;
     float g[4] = {t.x, t.y, t.z, t.w};
     if (e.frelu) {
-        const float4 y4 = ld4(e.fy + off);
         if (!(y4.x > 0.f)) g[0] = 0.f;
         if (!(y4.y > 0.f)) g[1] = 0.f;
         if (!(y4.z > 0.f)) g[2] = 0.f;
         if (!(y4.w > 0.f)) g[3] = 0.f;
     }
-    float sc[4] = {1.f, 1.f, 1.f, 1.f}, mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {1.f, 1.f, 1.f, 1.f};
-    float zz[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e.fscale) { const float4 v = ld4(e.fscale + n); sc[0] = v.x; sc[1] = v.y; sc[2] = v.z; sc[3] = v.w; }
-    if (e.fz) {
-        const float4 v = ld4(e.fz + off), a = ld4(e.fmean + n), b = ld4(e.frstd + n);
-        zz[0] = v.x; zz[1] = v.y; zz[2] = v.z; zz[3] = v.w;
-        mu[0] = a.x; mu[1] = a.y; mu[2] = a.z; mu[3] = a.w;
-        rs[0] = b.x; rs[1] = b.y; rs[2] = b.z; rs[3] = b.w;
-    }
+    const float sc[4] = {bn[0].x, bn[0].y, bn[0].z, bn[0].w}, mu[4] = {bn[1].x, bn[1].y, bn[1].z, bn[1].w};
+    const float rs[4] = {bn[2].x, bn[2].y, bn[2].z, bn[2].w}, zz[4] = {z4.x, z4.y, z4.z, z4.w};
     float d[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -752,6 +748,17 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     const bool pf = !PERSIST && M3D_EPI_PREFETCH && e.simple && e.split <= 0 && !(e.ldy & 3) &&
                     ((e.res_mode == 1 && !e.accumulate) || (e.res_mode == 0 && e.accumulate));
     float fs[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // fused BN sums
+    // fused BN: a thread's channel quad is the same in every batch (256 % C4T == 0)
+    static_assert(256 % C4T == 0, "fixed channel quad per thread");
+    float4 fbn4[3] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f),
+                      make_float4(1.f, 1.f, 1.f, 1.f)};
+    if (!PERSIST && e.fbn) {
+        const int n = n0c + (tid % C4T) * 4;
+        if (n < p.N) {
+            if (e.fscale) fbn4[0] = ld4(e.fscale + n);
+            if (e.fz) { fbn4[1] = ld4(e.fmean + n); fbn4[2] = ld4(e.frstd + n); }
+        }
+    }
     for (int hf = 0; hf < HALVES; ++hf) {
         if (hf) __syncthreads();                 // previous half fully read
         if ((wm * TM * 32) / HR == hf) {
@@ -781,6 +788,19 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
 #pragma unroll
         for (int q0 = 0; q0 < QN; q0 += PB) {
             float4 pre[PB];
+            float4 fy4[PB], fz4[PB];
+            if (!PERSIST && e.fbn) {             // the batch's y / z rows before its first store
+#pragma unroll
+                for (int u = 0; u < PB; ++u) {
+                    const int idx = tid + 256 * (q0 + u);
+                    const int row = idx / C4T, c4 = idx % C4T;
+                    const int64_t m = m0c + hf * HR + row;
+                    const int n = n0c + c4 * 4;
+                    const bool in = idx < HR * C4T && m < p.M && n < p.N;
+                    fy4[u] = in && e.frelu ? ld4(e.fy + m * e.ldy + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+                    fz4[u] = in && e.fz ? ld4(e.fz + m * e.ldy + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
             if (pf) {
                 const float* src = e.res_mode == 1 ? e.res : e.y;
 #pragma unroll
@@ -809,7 +829,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                             const float4 o = pf ? pre[u] : ld4(e.y + m * e.ldy + n);
                             t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
                         }
-                        epi_bnbwd4(e, m, n, t, fs);
+                        epi_bnbwd4(e, m, n, t, fy4[u], fz4[u], fbn4, fs);
                     } else if (pf) {
                         epi_store4_pre(p, e, m, n, v, pre[u]);
                     } else {
@@ -2165,31 +2185,42 @@ __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __rest
                 at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
         const float sc = e.fscale ? e.fscale[n] : 1.0f;
         const float mu = e.fz ? e.fmean[n] : 0.0f, rs = e.fz ? e.frstd[n] : 1.0f;
+        // every load of the tile's outputs (old dx, y, z) before the first store:
+        // a load issued after a store to a possibly aliasing address waits for it
+        float ov[2][2][NZ], yv[2][2][NZ], zv[2][2][NZ];
+        int64_t offs[2][2][NZ];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            const int y = 2 * ty + a;
-            if (y >= g.H) continue;
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int bb = 0; bb < 2; ++bb) {
-                const int xx = 2 * tx + bb;
-                if (xx >= g.W) continue;
+            for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) {
-                    const int z = NZ * tz + k;
-                    if (z >= g.D) continue;
-                    const int64_t off = ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * e.ldy + n;
+                    const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
+                    const bool in = y < g.H && xx < g.W && z < g.D;
+                    const int64_t off = in ? ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * e.ldy + n : -1;
+                    offs[a][bb][k] = off;
+                    ov[a][bb][k] = in && e.accumulate ? e.y[off] : 0.0f;
+                    yv[a][bb][k] = in && e.frelu ? e.fy[off] : 1.0f;
+                    zv[a][bb][k] = in && e.fz ? e.fz[off] : 0.0f;
+                }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                for (int k = 0; k < NZ; ++k) {
+                    const int64_t off = offs[a][bb][k];
+                    if (off < 0) continue;
                     float gv = o[a][bb][k];
-                    if (e.accumulate) gv += e.y[off];
-                    if (e.frelu && !(e.fy[off] > 0.f)) gv = 0.f;
+                    if (e.accumulate) gv += ov[a][bb][k];
+                    if (e.frelu && !(yv[a][bb][k] > 0.f)) gv = 0.f;
                     const float d = gv * sc;
                     sp += gv;
-                    sx += gv * (((e.fz ? e.fz[off] : 0.0f) - mu) * rs);
+                    sx += gv * ((zv[a][bb][k] - mu) * rs);
                     sz += d;
                     e.y[off] = d;
                     if (e.fdres) e.fdres[off] = gv;
                 }
-            }
-        }
     }
     if (!e.fpart) return;                        // (block-uniform)
     if (N % 256 == 0) {

@@ -168,16 +168,18 @@ class RPNHead:
         self.backbone = backbone        # its GradLinks are checked in finish_backward
 
     def __call__(self, feature_maps):
-        shared = []
+        shared, fuses = [], []
         # rpn_conv_shared1 is one kernel on every level: its Winograd weight
         # transform is done once per pass (forward and data gradient) and reused
         wshare = {} if SHARE_WINO_WEIGHTS else None
         for p in feature_maps:
             g1 = conv_geom(tuple(p.shape[1:4]), (3, 3, 3), (1, 1, 1), "same")
-            f1 = BNFuse() if torch.is_grad_enabled() else None     # shared1 -> shared2 only
+            # shared1 -> shared2 -> the class / bbox heads: sole consumers (nn.BNFuse)
+            f1, f2 = (BNFuse(), BNFuse()) if torch.is_grad_enabled() else (None, None)
             s = conv_bn_act(p, self.shared1, g1, relu=True, wshare=wshare, fuse=f1)
             g2 = conv_geom(tuple(s.shape[1:4]), (1, 1, 1), (1, 1, 1), "valid")
-            shared.append(conv_bn_act(s, self.shared2, g2, relu=True, fuse_in=f1))
+            shared.append(conv_bn_act(s, self.shared2, g2, relu=True, fuse=f2, fuse_in=f1))
+            fuses.append(f2)
         if wshare is not None:
             wshare.pop("fwd", None)        # the forward's workspace is not needed past the loop
         apl = self.apl
@@ -192,7 +194,7 @@ class RPNHead:
             self.w_grad = torch.zeros((cin, npad), device=w24.device, dtype=torch.float32)
             self.b_grad = torch.zeros((npad,), device=w24.device, dtype=torch.float32)
             grads = {"kernel": self.w_grad, "bias": self.b_grad}
-        logits, bbox = _RPNOut.apply(w24, b24, grads, apl, *shared)
+        logits, bbox = _RPNOut.apply(w24, b24, grads, apl, tuple(fuses), *shared)
         probs = torch.softmax(logits, dim=-1)
         return logits, probs, bbox
 

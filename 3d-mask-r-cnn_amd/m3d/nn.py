@@ -461,15 +461,20 @@ class BNFuse:
         self.armed = self.done = False
         self.y = self.z = self.bn = self.grads = self.buf = self.dres = None
 
-    def descriptor(self, dres):
+    def descriptor(self, dres, item=None):
         """The m3d_bn_bwd_t of the fused entry points (the tensors stay held by
-        this record and the caller's dres)."""
+        this record and the caller's dres); ``item``: batch item b's rows only."""
         g = self.grads or {}
         mean = rstd = scale = None
         if self.bn is not None:
             mean, rstd, scale = self.bn
-        d = _lib.BnBwd(ptr(self.y), ptr(self.z), ptr(scale), ptr(mean), ptr(rstd), 1 if self.relu else 0,
-                       ptr(dres), ptr(g.get("beta")), ptr(g.get("gamma") if self.z is not None else None),
+        y, z = self.y, self.z
+        if item is not None:
+            y = y[item:item + 1]
+            z = z[item:item + 1] if z is not None else None
+            dres = dres[item:item + 1] if dres is not None else None
+        d = _lib.BnBwd(ptr(y), ptr(z), ptr(scale), ptr(mean), ptr(rstd), 1 if self.relu else 0,
+                       ptr(dres), ptr(g.get("beta")), ptr(g.get("gamma") if z is not None else None),
                        ptr(g.get("bias")))
         return d
 
@@ -1046,7 +1051,9 @@ class _RPNOut(torch.autograd.Function):
     rpn_class_logits [B,A,2] / rpn_bbox [B,A,6] (core/models.py:3250-3263)."""
 
     @staticmethod
-    def forward(ctx, w24, b24, grads, apl, *shared):
+    def forward(ctx, w24, b24, grads, apl, fuses, *shared):
+        """``fuses``: per level, the BNFuse of the rpn_conv_shared2 unit that
+        made ``shared[level]`` (this head is its only consumer) or None."""
         t0 = _span()
         dev = shared[0].device
         B = shared[0].shape[0]
@@ -1073,6 +1080,9 @@ class _RPNOut(torch.autograd.Function):
                  "fwd", "rpn_class_raw+rpn_bbox_pred", t0)
         ctx.save_for_backward(w24, *shared)
         ctx.grads, ctx.rows, ctx.apl = grads, rows, apl
+        ctx.fuses = [f if (f is not None and f.armed and f.y is not None and f.y.data_ptr() == s.data_ptr()
+                           and f.y.shape == s.shape) else None
+                     for f, s in zip(fuses or [None] * len(shared), shared)]
         return logits, bbox
 
     @staticmethod
@@ -1093,6 +1103,14 @@ class _RPNOut(torch.autograd.Function):
         dshared = [torch.empty_like(s) for s in shared]
         L = _L()
         R = sum(rows)
+        fuses = ctx.fuses
+        ctx.fuses = None
+        fws = [None] * len(shared)
+        for li, rec in enumerate(fuses):
+            if rec is not None and not _per_item(1, rows[li], Cin, rows[li], npad):
+                _, H, W, D, _ = shared[li].shape
+                fws[li] = (torch.empty_like(shared[li]) if rec.need_res else None,
+                           *_bn_fuse_ws(rec, 1, H, W, D, Cin, dev))
         for b in range(B):
             # all levels' output gradients as one [R, npad] matrix (row = voxel,
             # level-concatenated like the outputs): one cat + one pad instead of
@@ -1112,13 +1130,24 @@ class _RPNOut(torch.autograd.Function):
                     check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
                                                   W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
                                                   stream()), "rpn_out_wgrad")
-                check(L.m3d_conv3d_bwd_data(ptr(dz), ptr(w_pad), 1, H, W, D, Cin, 1, 1, 1, npad, H,
-                                            W, D, 1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(),
-                                            0, stream()), "rpn_out_dgrad")
+                if fws[li] is not None:
+                    # rpn_conv_shared2's ReLU backward (and bias sums) in this data gradient's epilogue
+                    dres_f, bws, bwsb = fws[li]
+                    d = fuses[li].descriptor(dres_f, b)
+                    check(L.m3d_conv3d_bwd_data_bn(ptr(dz), ptr(w_pad), 1, H, W, D, Cin, 1, 1, 1, npad, H, W, D,
+                                                   1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(), 0,
+                                                   ctypes.addressof(d), ptr(bws), bwsb, stream()), "rpn_out_dgrad_bn")
+                else:
+                    check(L.m3d_conv3d_bwd_data(ptr(dz), ptr(w_pad), 1, H, W, D, Cin, 1, 1, 1, npad, H,
+                                                W, D, 1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(),
+                                                0, stream()), "rpn_out_dgrad")
                 off += r
+        for li, rec in enumerate(fuses):
+            if fws[li] is not None:
+                rec.buf, rec.dres, rec.done = dshared[li], fws[li][0], True
         if LAYER_LOG is not None:
             f = 2.0 * B * R * Cin * n_out
             nx = sum(s.numel() for s in shared)
             _log("conv1_bwd", 2 * f, 2 * f, 4.0 * (2 * nx + 2 * B * R * npad + 2 * w24.numel()), "bwd_data",
                  "rpn_class_raw+rpn_bbox_pred (wgrad+dgrad)", t0)
-        return (None, None, None, None) + tuple(dshared)
+        return (None, None, None, None, None) + tuple(dshared)

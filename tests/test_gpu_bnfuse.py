@@ -203,11 +203,11 @@ def test_model_fused_vs_unfused(cuda, monkeypatch):
     n_on = sum(1 for r in log_on if r[0] == "bn_act_bwd")
     n_off = sum(1 for r in log_off if r[0] == "bn_act_bwd")
     # 16 blocks x (2a -> 2b, 2b -> 2c) + 12 block -> block inside the stages + the
-    # RPN head's shared1 -> shared2 on 5 levels (fewer where shared2's data
-    # gradient runs the x3 GEMM, which has no fused form)
+    # RPN head's shared1 -> shared2 and shared2 -> class/bbox heads on 5 levels
+    # (fewer where shared2's data gradient runs the x3 GEMM, which has no fused form)
     left = [r[5] for r in log_on if r[0] == "bn_act_bwd"]
     print("bn_act_bwd left with the fusion on:", n_on, "of", n_off, left)
-    assert n_off - n_on >= 44, (n_on, n_off, left)
+    assert n_off - n_on >= 49, (n_on, n_off, left)
     assert torch.equal(l_on, l_on2)
     assert torch.equal(flat_on, flat_on2)
     assert abs(float(l_on) - float(l_off)) <= 1e-6 * abs(float(l_off))
