@@ -179,9 +179,14 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #define M3D_TUNE_ROI_PC 0
 #endif
 // PyramidROIAlign forward in the separable row form (row_fwd_kernel) for pools
-// of depth >= this (0: off)
+// of depth >= this (0: off; A/B builds only -- bit-identical, but 1.03 ms vs the
+// line kernel's 0.88 ms at 256^3 14^3 and 0.24 vs 0.14 ms at 128^3, r04r)
 #ifndef M3D_TUNE_ROI_ROW
 #define M3D_TUNE_ROI_ROW 0
+#endif
+// ... its workgroups per output row (channel groups of 256 / CG channels)
+#ifndef M3D_TUNE_ROI_ROW_CG
+#define M3D_TUNE_ROI_ROW_CG 1
 #endif
 #ifndef M3D_TUNE_X3AF
 #define M3D_TUNE_X3AF 0

@@ -411,42 +411,59 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     }
 }
 
+#if M3D_TUNE_ROI_ROW
 // ---- PyramidROIAlign forward, separable row form ----------------------------------
-// One workgroup per output row (n, y) over all C channels.  tri() lerps z first
-// (per corner column), then x, then y, so the z-lerped value of a (source row,
-// x column) at sample z is shared by every output x whose corners use that
+// One workgroup per output row (n, y) over all C = 256 channels.  tri() lerps z
+// first (per corner column), then x, then y, so the z-lerped value of a (source
+// row, x column) at sample z is shared by every output x whose corners use that
 // column: per z sample the workgroup loads the rows ty / by of each distinct x
 // column once (the line kernel loads 8 corner rows per output), z-lerps them
-// into LDS, and every (x, channel quad) finishes x- and y-lerps from LDS with
-// tri()'s operations (bit-identical).  The distinct columns are the union of
-// the samples' floor / ceil indices (XS <= 2 cw slots); a column's plane
-// pair is kept in registers across z samples when the next floor plane is the
-// previous ceil plane.  Outputs are stored as full C-channel rows.
-template <int CW_MAX>
-__global__ __launch_bounds__(256) void row_fwd_kernel(LineArgs a, Pyr P) {
+// into LDS, and every (x, channel quad) finishes the x- and y-lerps from LDS
+// with tri()'s operations (bit-identical).  The distinct columns are the union
+// of the samples' floor / ceil indices (<= 2 cw slots).  The next sample's
+// corner rows are loaded while the current one's outputs are written (one
+// register stage); a floor plane equal to the previous ceil plane is reused.
+// tri()'s x- then y-lerp of the four z-lerped corners (same operations), scrubbed
+__device__ __forceinline__ float row_xy(float tl, float tr, float bl, float br, float xl, float yl) {
+    const float top = tl + (tr - tl) * xl;
+    const float bot = bl + (br - bl) * xl;
+    return scrub(top + (bot - top) * yl);
+}
+
+// sample z's planes (fz = -1: outside the map, extrapolate)
+__device__ __forceinline__ void row_zplanes(float z1, float z2, int D, int cd, int z, float zsc, int& fz, int& kz,
+                                            float& zl) {
+    const float in_z = axis_coord(z1, z2, D, cd, z, zsc);
+    if (in_z < 0 || in_z > (float)(D - 1)) { fz = -1; kz = -1; zl = 0.0f; return; }
+    fz = (int)floorf(in_z); kz = (int)ceilf(in_z); zl = in_z - (float)fz;
+}
+
+template <int CW_MAX, int NT, int CG>
+__global__ __launch_bounds__(NT) void row_fwd_kernel(LineArgs a, Pyr P) {
     constexpr int XS = 2 * CW_MAX;
-    constexpr int IPT = (2 * XS * 64 + 255) / 256;        // (row, slot, quad) items per thread
-    __shared__ float4 T[2][XS][64];
+    constexpr int C4 = 64 / CG;                           // channel quads of this group (C = 256)
+    constexpr int IPT = (2 * XS * C4 + NT - 1) / NT;        // (row, slot, quad) items per thread
+    __shared__ float4 T[2 * XS][C4];
     __shared__ int s_l[CW_MAX], s_r[CW_MAX], s_oob[CW_MAX], s_col[XS], s_ns;
     __shared__ float s_xl[CW_MAX];
     const int tid = threadIdx.x;
-    const int64_t row = xcd_block();
+    const int64_t rb = xcd_block();                       // (row, channel group), groups adjacent
+    const int64_t row = rb / CG;
+    const int cg = (int)(rb - row * CG);
     if (row >= a.lines) return;                           // (block-uniform)
     const int y = (int)(row % a.ch);
     const int64_t n = row / a.ch;
     const int l = a.levels[n] - 2;
     const int H = P.H[l], W = P.W[l], D = P.D[l];
-    const int C4 = a.C >> 2;
-    const float4* img = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)(n / a.N) * H * W * D * a.C);
+    const float4* img = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)(n / a.N) * H * W * D * a.C) + cg * C4;
     const float* box = a.boxes + n * 6;
     const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
     const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
     const float zsc = axis_scale(z1, z2, D, a.cd);
-    float4* o = reinterpret_cast<float4*>(a.out) + (row * a.cw) * (int64_t)a.cd * C4;
+    float4* o = reinterpret_cast<float4*>(a.out) + (row * a.cw) * (int64_t)a.cd * 64 + cg * C4;
     const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
-    const int nout = a.cw * a.cd * C4;
     if (in_y < 0 || in_y > (float)(H - 1)) {
-        for (int i = tid; i < nout; i += 256) st_nt(o + i, ex);
+        for (int i = tid; i < a.cw * a.cd * C4; i += NT) st_nt(o + (int64_t)(i / C4) * 64 + i % C4, ex);
         return;
     }
     const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
@@ -478,7 +495,6 @@ __global__ __launch_bounds__(256) void row_fwd_kernel(LineArgs a, Pyr P) {
     }
     __syncthreads();
     const int ns = s_ns;
-    // slot of each sample's floor / ceil column (threads < cw), then back to LDS
     int my_sl = 0, my_sr = 0;
     if (tid < a.cw && !s_oob[tid]) {
         for (int k = 0; k < ns; ++k) {
@@ -486,65 +502,99 @@ __global__ __launch_bounds__(256) void row_fwd_kernel(LineArgs a, Pyr P) {
             if (s_col[k] == s_r[tid]) my_sr = k;
         }
     }
+    const int nr = ty == by ? 1 : 2;
+    const int bot = (nr - 1) * ns;                        // T row offset of the bottom source row
+    const size_t rowD = (size_t)D * 64, rowW = (size_t)W * rowD;
+    // this thread's items: T row j = r * ns + slot, channel quad q (fixed over z)
+    const float4* cp[IPT];
+    int tj[IPT];
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+        const int i = tid + NT * u;
+        const int j = i / C4, q = i & (C4 - 1);
+        const int r = j >= ns ? 1 : 0;
+        tj[u] = j < nr * ns ? j : -1;
+        cp[u] = img + (r ? by : ty) * rowW + s_col[tj[u] < 0 ? 0 : j - r * ns] * rowD + q;
+    }
     __syncthreads();
     if (tid < a.cw) { s_l[tid] = my_sl; s_r[tid] = my_sr; }
-    const int nr = ty == by ? 1 : 2;
-    const int items = nr * ns * C4;
-    const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
-    int pk = -1;
-    float4 kv[IPT];
-    for (int z = 0; z < a.cd; ++z) {
-        const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
-        __syncthreads();                                  // the previous sample's T fully read
-        if (in_z < 0 || in_z > (float)(D - 1)) {
-            for (int i = tid; i < a.cw * C4; i += 256) st_nt(o + ((int64_t)(i / C4) * a.cd + z) * C4 + i % C4, ex);
-            continue;
-        }
-        const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
-        const float zl = in_z - (float)fz;
-        const bool reuse = fz == pk;
+    // loads of the first in-range sample (z planes uniform: row_zplanes)
+    float4 f[IPT], k[IPT];
+    int fz, kz, pk = -1;
+    float zl;
+    row_zplanes(z1, z2, D, a.cd, 0, zsc, fz, kz, zl);
+    if (fz >= 0) {
 #pragma unroll
         for (int u = 0; u < IPT; ++u) {
-            const int i = tid + 256 * u;
-            if (i < items) {
-                const int q = i % C4, sl = (i / C4) % ns, r = i / (C4 * ns);
-                const float4* col = img + (r ? by : ty) * rowW + s_col[sl] * rowD + q;
-                const float4 f = reuse ? kv[u] : col[(size_t)fz * C4];
-                const float4 k = kz != fz ? col[(size_t)kz * C4] : f;
-                kv[u] = k;
-                float4 t;
-                t.x = f.x + (k.x - f.x) * zl;
-                t.y = f.y + (k.y - f.y) * zl;
-                t.z = f.z + (k.z - f.z) * zl;
-                t.w = f.w + (k.w - f.w) * zl;
-                T[r][sl][q] = t;
+            if (tj[u] >= 0) {
+                f[u] = cp[u][(size_t)fz * 64];
+                k[u] = cp[u][(size_t)kz * 64];            // (kz == fz: the same row)
             }
         }
         pk = kz;
+    }
+    for (int z = 0; z < a.cd; ++z) {
+        const bool in = fz >= 0;
+        if (in) {
+#pragma unroll
+            for (int u = 0; u < IPT; ++u) {
+                if (tj[u] >= 0) {
+                    float4 t;
+                    t.x = f[u].x + (k[u].x - f[u].x) * zl;
+                    t.y = f[u].y + (k[u].y - f[u].y) * zl;
+                    t.z = f[u].z + (k[u].z - f[u].z) * zl;
+                    t.w = f[u].w + (k[u].w - f[u].w) * zl;
+                    T[tj[u]][tid & (C4 - 1)] = t;
+                }
+            }
+        }
+        // the next sample's corner rows in flight across the barrier and the stores
+        if (z + 1 < a.cd) {
+            row_zplanes(z1, z2, D, a.cd, z + 1, zsc, fz, kz, zl);
+            if (fz >= 0) {
+                // uniform branches, no per-item selects: a select between a register
+                // array element and a load becomes a select of addresses, and the
+                // array is then kept in scratch
+                if (fz == pk) {
+#pragma unroll
+                    for (int u = 0; u < IPT; ++u)
+                        if (tj[u] >= 0) f[u] = k[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < IPT; ++u)
+                        if (tj[u] >= 0) f[u] = cp[u][(size_t)fz * 64];
+                }
+                if (kz != fz) {
+#pragma unroll
+                    for (int u = 0; u < IPT; ++u)
+                        if (tj[u] >= 0) k[u] = cp[u][(size_t)kz * 64];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < IPT; ++u)
+                        if (tj[u] >= 0) k[u] = f[u];
+                }
+                pk = kz;
+            }
+        }
         __syncthreads();
-        for (int i = tid; i < a.cw * C4; i += 256) {
-            const int x = i / C4, q = i % C4;
+        for (int i = tid; i < a.cw * C4; i += NT) {
+            const int x = i / C4, q = i & (C4 - 1);
             float4 res = ex;
-            if (!s_oob[x]) {
+            if (in && !s_oob[x]) {
                 const int a0 = s_l[x], a1 = s_r[x];
                 const float xl = s_xl[x];
-                const float4 tl = T[0][a0][q], tr = T[0][a1][q];
-                const float4 bl = T[nr - 1][a0][q], br = T[nr - 1][a1][q];
-                float v[4];
-                const float tlv[4] = {tl.x, tl.y, tl.z, tl.w}, trv[4] = {tr.x, tr.y, tr.z, tr.w};
-                const float blv[4] = {bl.x, bl.y, bl.z, bl.w}, brv[4] = {br.x, br.y, br.z, br.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float top = tlv[c] + (trv[c] - tlv[c]) * xl;
-                    const float bot = blv[c] + (brv[c] - blv[c]) * xl;
-                    v[c] = scrub(top + (bot - top) * yl);
-                }
-                res = make_float4(v[0], v[1], v[2], v[3]);
+                const float4 tl = T[a0][q], tr = T[a1][q];
+                const float4 bl = T[bot + a0][q], br = T[bot + a1][q];
+                res = make_float4(row_xy(tl.x, tr.x, bl.x, br.x, xl, yl), row_xy(tl.y, tr.y, bl.y, br.y, xl, yl),
+                                  row_xy(tl.z, tr.z, bl.z, br.z, xl, yl), row_xy(tl.w, tr.w, bl.w, br.w, xl, yl));
             }
-            st_nt(o + ((int64_t)x * a.cd + z) * C4 + q, res);
+            st_nt(o + ((int64_t)x * a.cd + z) * 64 + q, res);
         }
+        __syncthreads();                                  // T read before the next sample writes it
     }
 }
+
+#endif  // M3D_TUNE_ROI_ROW
 
 #if M3D_TUNE_ROI_PC
 // Producer / consumer form of line_fwd_sl_kernel<8> (M3D_ROI_PC=1): a
@@ -1923,14 +1973,23 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
     if ((C & 3) == 0) {
         LineArgs a{nullptr, nullptr, boxes_adj, levels, N, B * N * ph * pw, 0, 0, 0, (int)C, ph, pw, pd,
                    0.0f, out};
-        if constexpr (M3D_TUNE_ROI_ROW > 0) {
-            if (C <= 256 && pw <= 14 && pd >= M3D_TUNE_ROI_ROW) {
+#if M3D_TUNE_ROI_ROW
+        {
+            if (C == 256 && pw <= 14 && pd >= M3D_TUNE_ROI_ROW) {
                 LineArgs ra = a;
                 ra.lines = B * N * ph;
-                hipLaunchKernelGGL(row_fwd_kernel<14>, dim3((unsigned)ra.lines), dim3(256), 0, s, ra, P);
+                if constexpr (M3D_TUNE_ROI_ROW_CG == 2)
+                    hipLaunchKernelGGL((row_fwd_kernel<14, 256, 2>), dim3((unsigned)(2 * ra.lines)), dim3(256), 0, s,
+                                       ra, P);
+                else if constexpr (M3D_TUNE_ROI_ROW_CG == 4)
+                    hipLaunchKernelGGL((row_fwd_kernel<14, 256, 4>), dim3((unsigned)(4 * ra.lines)), dim3(256), 0, s,
+                                       ra, P);
+                else
+                    hipLaunchKernelGGL((row_fwd_kernel<14, 512, 1>), dim3((unsigned)ra.lines), dim3(512), 0, s, ra, P);
                 return check_launch("row_fwd_kernel");
             }
         }
+#endif
         const int sl = roi_slices();
         if (C == 256 && (sl == 2 || sl == 4 || sl == 8 || sl == 16)) {
             const int32_t* perm = nullptr;
