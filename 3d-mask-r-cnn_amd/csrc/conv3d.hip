@@ -360,12 +360,17 @@ __device__ __forceinline__ void epi_store4_pre(const ConvP& p, const Epi& e, int
 // -------------------------------------------------------------------------
 // fwd / bwd-data implicit GEMM
 // -------------------------------------------------------------------------
+// FBN: the data gradient with the fused BN-ReLU backward of the unit it feeds
+// (its own instantiation at 2 blocks/CU: the epilogue's extra rows and sums
+// spill at 3, and must not touch the register budget of the other forms)
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false,
-          bool X3 = false>
-__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_gemm_kernel(ConvP p, Epi e) {
+          bool X3 = false, bool FBN = false>
+__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) void conv_gemm_kernel(ConvP p,
+                                                                                                  Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
     static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
+    static_assert(!FBN || (!PERSIST && !X3), "fused BN backward: one tile per block, f32 MFMA");
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     static_assert(WM * WN == 4, "4 waves");
     static_assert(TM >= 1 && TN >= 1, "tile");
@@ -752,7 +757,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
     static_assert(256 % C4T == 0, "fixed channel quad per thread");
     float4 fbn4[3] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f),
                       make_float4(1.f, 1.f, 1.f, 1.f)};
-    if (!PERSIST && e.fbn) {
+    if (FBN) {
         const int n = n0c + (tid % C4T) * 4;
         if (n < p.N) {
             if (e.fscale) fbn4[0] = ld4(e.fscale + n);
@@ -789,7 +794,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
         for (int q0 = 0; q0 < QN; q0 += PB) {
             float4 pre[PB];
             float4 fy4[PB], fz4[PB];
-            if (!PERSIST && e.fbn) {             // the batch's y / z rows before its first store
+            if (FBN) {                           // the batch's y / z rows before its first store
 #pragma unroll
                 for (int u = 0; u < PB; ++u) {
                     const int idx = tid + 256 * (q0 + u);
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
                     const float4 v = *reinterpret_cast<const float4*>(Ts + row * LDT + c4 * 4);
                     if (PERSIST) {  // plain C store (host-checked: simple epilogue, nothing fused)
                         st4(e.y + m * e.ldy + n, v);
-                    } else if (e.fbn) {   // (host-checked: simple rows, no bias / BN / residual / act)
+                    } else if (FBN) {     // (host-checked: simple rows, no bias / BN / residual / act)
                         float4 t = v;
                         if (e.accumulate) {
                             const float4 o = pf ? pre[u] : ld4(e.y + m * e.ldy + n);
@@ -840,8 +845,8 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 ? 3 : 2)) void conv_
         }
         e.y = y_next;
     }
-    if constexpr (!PERSIST) {
-        if (e.fbn && e.fpart) {
+    if constexpr (FBN) {
+        if (e.fpart) {
             // channel sums of the tile: threads t, t + C4T, ... hold channel quad t % C4T
             __syncthreads();                     // staged tile fully read: Ts reused
             float* red = Ts;                     // [256][12]
@@ -1182,6 +1187,13 @@ static int conv_x3_env() { return (x3_mask() >> 1) & 1; }
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK>
 static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
     dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
+    if constexpr (BT && BK == 32) {
+        if (e.fbn) {                       // the fused BN-ReLU backward's own instantiation
+            hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, false, false, true>), grid,
+                               dim3(256), 0, s, p, e);
+            return;
+        }
+    }
     if constexpr (BK == 32 && AVEC) {      // (the scalar-A loader spills at 3 blocks/CU)
         const int64_t tiles = (int64_t)grid.x * grid.y * nbatch;
         const int64_t resident = (int64_t)num_cus() * (gemm_nbuf_env() == 1 ? 3 : 2);
@@ -1243,7 +1255,7 @@ static void launch_gemm_bk(bool bk64, const ConvP& p, const Epi& e, hipStream_t 
 template <bool BT, bool AVEC>
 static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch = 1) {
     // 64-deep k-tiles when a k-tile stays inside one tap (C % 64 == 0)
-    const bool bk64 = AVEC && p.C % 64 == 0 && gemm_bk_env() == 64;
+    const bool bk64 = AVEC && p.C % 64 == 0 && gemm_bk_env() == 64 && !e.fbn;
     if (p.N <= 32) {
         launch_gemm<128, 32, 4, 1, BT, AVEC, 32>(p, e, s, nbatch);
     } else if (p.N <= 64) {
@@ -2185,42 +2197,42 @@ __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __rest
                 at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
         const float sc = e.fscale ? e.fscale[n] : 1.0f;
         const float mu = e.fz ? e.fmean[n] : 0.0f, rs = e.fz ? e.frstd[n] : 1.0f;
-        // every load of the tile's outputs (old dx, y, z) before the first store:
-        // a load issued after a store to a possibly aliasing address waits for it
-        float ov[2][2][NZ], yv[2][2][NZ], zv[2][2][NZ];
-        int64_t offs[2][2][NZ];
+        // per output row pair a: its loads (old dx, y, z) before its stores -- a load
+        // issued after a store to a possibly aliasing address waits for it -- in two
+        // halves, so only 2 x 2 x NZ x 3 loaded values are live beside o
+        const int64_t ostr = (int64_t)g.D * e.ldy;             // output x step
+        const int64_t obase = ((((int64_t)b * g.H + 2 * ty) * g.W + 2 * tx) * g.D + NZ * tz) * e.ldy + n;
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 2; ++a) {
+            float ov[2][NZ], yv[2][NZ], zv[2][NZ];
+            bool in[2][NZ];
 #pragma unroll
             for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) {
-                    const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
-                    const bool in = y < g.H && xx < g.W && z < g.D;
-                    const int64_t off = in ? ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * e.ldy + n : -1;
-                    offs[a][bb][k] = off;
-                    ov[a][bb][k] = in && e.accumulate ? e.y[off] : 0.0f;
-                    yv[a][bb][k] = in && e.frelu ? e.fy[off] : 1.0f;
-                    zv[a][bb][k] = in && e.fz ? e.fz[off] : 0.0f;
+                    in[bb][k] = 2 * ty + a < g.H && 2 * tx + bb < g.W && NZ * tz + k < g.D;
+                    const int64_t off = obase + (a * (int64_t)g.W + bb) * ostr + k * e.ldy;
+                    ov[bb][k] = in[bb][k] && e.accumulate ? e.y[off] : 0.0f;
+                    yv[bb][k] = in[bb][k] && e.frelu ? e.fy[off] : 1.0f;
+                    zv[bb][k] = in[bb][k] && e.fz ? e.fz[off] : 0.0f;
                 }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
             for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) {
-                    const int64_t off = offs[a][bb][k];
-                    if (off < 0) continue;
+                    if (!in[bb][k]) continue;
+                    const int64_t off = obase + (a * (int64_t)g.W + bb) * ostr + k * e.ldy;
                     float gv = o[a][bb][k];
-                    if (e.accumulate) gv += ov[a][bb][k];
-                    if (e.frelu && !(yv[a][bb][k] > 0.f)) gv = 0.f;
+                    if (e.accumulate) gv += ov[bb][k];
+                    if (e.frelu && !(yv[bb][k] > 0.f)) gv = 0.f;
                     const float d = gv * sc;
                     sp += gv;
-                    sx += gv * ((zv[a][bb][k] - mu) * rs);
+                    sx += gv * ((zv[bb][k] - mu) * rs);
                     sz += d;
                     e.y[off] = d;
                     if (e.fdres) e.fdres[off] = gv;
                 }
+        }
     }
     if (!e.fpart) return;                        // (block-uniform)
     if (N % 256 == 0) {
