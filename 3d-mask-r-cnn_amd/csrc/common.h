@@ -73,8 +73,11 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_GEMM_PERSIST
 #define M3D_TUNE_GEMM_PERSIST 1
 #endif
+// GEMM forms on the exact bf16 split (bit mask, conv3d.hip x3_mask); 31 = all,
+// the implicit-GEMM convs included since round 4 (same-box step A/B with the
+// fused BN backward: 27.33 -> 27.08 ms, profiles/r04v_cx3_step_ab.txt)
 #ifndef M3D_TUNE_GEMM_X3
-#define M3D_TUNE_GEMM_X3 29
+#define M3D_TUNE_GEMM_X3 31
 #endif
 #ifndef M3D_TUNE_GEMM_BK
 #define M3D_TUNE_GEMM_BK 32

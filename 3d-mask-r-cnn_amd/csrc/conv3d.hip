@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) vo
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
     static_assert(AVEC || BK == 32, "scalar A loader is BK=32");
-    static_assert(!FBN || (!PERSIST && !X3), "fused BN backward: one tile per block, f32 MFMA");
+    static_assert(!FBN || !PERSIST, "fused BN backward: one tile per block");
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     static_assert(WM * WN == 4, "4 waves");
     static_assert(TM >= 1 && TN >= 1, "tile");
@@ -1165,12 +1165,13 @@ static int num_cus() {
     return v;
 }
 
-// M3D_GEMM_X3 (bit mask, default 29): fp32 GEMMs on the exact 3-way bf16 split
+// M3D_GEMM_X3 (bit mask, default 31): fp32 GEMMs on the exact 3-way bf16 split
 // (6 bf16 MFMAs per product, see split3) instead of v_mfma_f32_32x32x2_f32.
 // bit 0: Winograd fwd / bwd-data point GEMMs on operands pre-split by the
 // transforms (x3_gemm_kernel; measured 39.9 -> 37.9 ms/step at 128^3, GEMM
 // error vs fp64 below the f32 MFMA's: scripts/x3_accuracy.py); bit 1:
-// implicit-GEMM convs splitting in the LDS store (slower: off); bit 2: the
+// implicit-GEMM convs splitting in the LDS store (neutral to -0.3 ms/step
+// through round 3, on since round 4: -0.25 ms with the fused BN backward); bit 2: the
 // Winograd weight-gradient GEMMs (x3_wgrad_kernel; 38.2 -> 37.0 ms/step);
 // bit 3: the weight gradients of 1x1x1 stride-1 convs on the same kernel;
 // bit 4: the Winograd input transform writes U as fp32 (4 B per point
@@ -1189,6 +1190,13 @@ static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch)
     dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)nbatch);
     if constexpr (BT && BK == 32) {
         if (e.fbn) {                       // the fused BN-ReLU backward's own instantiation
+            if constexpr (AVEC) {
+                if (conv_x3_env()) {       // the same GEMM form as the unfused data gradient
+                    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, false, true, true>), grid,
+                                       dim3(256), 0, s, p, e);
+                    return;
+                }
+            }
             hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, false, false, true>), grid,
                                dim3(256), 0, s, p, e);
             return;
