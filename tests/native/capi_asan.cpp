@@ -73,6 +73,26 @@ int main() {
     EXPECT_EINVAL(m3d_conv3d_fwd(nf, 1, 8, 8, 8, 4, nf, 3, 3, 3, 8, 8, 8, 8, 0, 1, 1, 1, 1, 1, nf, nf, nf, nf,
                                  0, 0, of, of, 0, of, 0, 0, s));
     EXPECT_EINVAL(m3d_conv3d_bwd_data(nf, nf, 1, 8, 8, 8, 4, 3, 3, 3, 8, 8, 8, 8, 1, 1, 0, 1, 1, 1, of, 0, s));
+    // data gradients with the fused BN-ReLU backward: descriptor checks come first
+    {
+        float buf[4] = {0, 0, 0, 0};
+        m3d_bn_bwd_t bn{};
+        EXPECT_EINVAL(m3d_conv3d_bwd_data_bn(nf, nf, 1, 8, 8, 8, 64, 1, 1, 1, 32, 8, 8, 8, 1, 1, 1, 0, 0, 0, of, 0,
+                                             nullptr, nullptr, 0, s));                    // no descriptor
+        bn.relu = 1;                                                                    // relu without y
+        EXPECT_EINVAL(m3d_conv3d_bwd_data_bn(nf, nf, 1, 8, 8, 8, 64, 1, 1, 1, 32, 8, 8, 8, 1, 1, 1, 0, 0, 0, of, 0,
+                                             &bn, nullptr, 0, s));
+        bn.relu = 0;
+        bn.sum_dpre_xhat = buf;                                                         // xhat sums without z
+        EXPECT_EINVAL(m3d_conv3d_bwd_data_bn(nf, nf, 1, 8, 8, 8, 64, 1, 1, 1, 32, 8, 8, 8, 1, 1, 1, 0, 0, 0, of, 0,
+                                             &bn, nullptr, 0, s));
+        bn.sum_dpre_xhat = nullptr;
+        bn.sum_dz = buf;                                                                // sums, no workspace
+        EXPECT_EINVAL(m3d_conv3d_bwd_data_splitk_bn(nf, nf, 1, 4, 4, 8, 1024, 256, of, 0, 2, nullptr, 0, &bn,
+                                                    nullptr, 0, s));
+        EXPECT_EINVAL(m3d_conv3d_bwd_data_wino_bn(nf, nf, 1, 8, 8, 8, 96, 64, 8, 1, of, 0, nullptr, 0, 0, &bn,
+                                                  nullptr, 0, s));                      // Cin 96: no fused form
+    }
     EXPECT_EINVAL(m3d_conv3d_bwd_weight(nf, nf, 1, 8, 8, -8, 4, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, of, s));
     EXPECT_EINVAL(m3d_conv3d_fwd_dil(nf, 1, 8, 8, 8, 4, nf, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, 0, 1, 1, nf,
                                      nf, nf, nf, 0, 0, of, of, 0, of, 0, 0, s));
