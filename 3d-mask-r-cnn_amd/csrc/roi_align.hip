@@ -1998,13 +1998,15 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
             const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
             // default order: waves sorted by their feature-map column (mode 3) for the
             // 14^3 mask pool -- PMC fabric reads at 256^3 / 512 ROIs 3.41 -> 1.89 GB,
-            // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for the 7^3 pool
-            // (its lines are short and the sort does not pay); M3D_ROI_SORT overrides
+            // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for small 7^3
+            // launches (their lines are short and the sort does not pay); M3D_ROI_SORT overrides
             static constexpr int sort_env0 = M3D_TUNE_ROI_SORT;
             // register-staged z parts (M3D_ROI_STAGE = PD, 0: off): zs = ceil(pd / PD) parts per line
             static constexpr int stage_env = M3D_TUNE_ROI_STAGE;
             const int spd = (stage_env == 4 || stage_env == 7 || stage_env == 14) && sl == 8 ? stage_env : 0;
-            int sort_env = sort_env0 >= 0 ? sort_env0 : (pd >= 14 ? 3 : 0);
+            // ... and for the 7^3 pool once the launch is large (512 ROIs at 256^3: PMC
+            // traffic 1.34 -> 1.09 GB at the same time; at 128^3 the sort costs 4 us of 58)
+            int sort_env = sort_env0 >= 0 ? sort_env0 : ((pd >= 14 || a.lines >= 16384) ? 3 : 0);
             if (sort_env == 3 && spd && spd < pd) sort_env = 0;   // the wave order sorts whole lines
             if (sort_env == 2 && workspace && ws_bytes >= need && nl < INT32_MAX && B * N <= nb) {
                 // ROI order: keys [B*N] (uint64, 8-B aligned at the start), inv [B*N], perm [lines]
