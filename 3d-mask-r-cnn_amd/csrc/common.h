@@ -194,6 +194,8 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_X3AF
 #define M3D_TUNE_X3AF 0
 #endif
+// the 256x256 Winograd point GEMM only where it has at least this many tiles
+// (step A/B r04t1: 0 27.26 ms, 256 27.39, 512 27.36; isolated launches favoured 256)
 #ifndef M3D_TUNE_X3_256_MIN_TILES
-#define M3D_TUNE_X3_256_MIN_TILES 256
+#define M3D_TUNE_X3_256_MIN_TILES 0
 #endif
