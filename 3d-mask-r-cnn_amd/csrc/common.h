@@ -115,6 +115,10 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_X3_256
 #define M3D_TUNE_X3_256 1
 #endif
+// Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z
+#ifndef M3D_TUNE_WINO_NY
+#define M3D_TUNE_WINO_NY 2
+#endif
 #ifndef M3D_TUNE_WINO_NZ
 #define M3D_TUNE_WINO_NZ 4
 #endif

@@ -1867,6 +1867,13 @@ template <> struct ZT<4> {
     }
 };
 
+// y-axis transforms: F(WNY,3) -- 2: F(2,3) as on x; 4: F(4,3) as on z (a 4x2xNZ
+// output tile: 4.5 instead of 6 points per output for NZ = 4, at a larger
+// rounding amplification; M3D_TUNE_WINO_NY)
+constexpr int WNY = M3D_TUNE_WINO_NY;
+using YT = ZT<WNY>;
+constexpr int PY = YT::P;
+
 __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b, int& ty, int& tx,
                                             int& tz) {
     tz = (int)(t % g.TZ);
@@ -1895,7 +1902,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
         const bool edge = tz == 0 || tz == g.TZ - 1;
         if ((g.tz_mode == 1) == edge) return;
     }
-    float d[4][4][P];
+    float d[PY][4][P];
     // branch-free window loads: raw buffer loads whose out-of-range offset
     // returns 0 (the zero padding), so all 16*P loads issue back to back
     // (conditional global loads compiled to a branch + wait per element)
@@ -1903,8 +1910,8 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     __amdgpu_buffer_rsrc_t rh;
     if constexpr (HALO) rh = make_rsrc(g.halo, (uint64_t)g.B * g.H * g.W * 2 * C * 4);
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int y = 2 * ty - 1 + a;
+    for (int a = 0; a < PY; ++a) {
+        const int y = WNY * ty - 1 + a;
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int xx = 2 * tx - 1 + bb;
@@ -1931,23 +1938,30 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
         }
     }
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) ZT<NZ>::bt(d[a][bb]);
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int k = 0; k < P; ++k) bt4(d[a][0][k], d[a][1][k], d[a][2][k], d[a][3][k]);
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-        for (int k = 0; k < P; ++k) bt4(d[0][bb][k], d[1][bb][k], d[2][bb][k], d[3][bb][k]);
+        for (int k = 0; k < P; ++k) {
+            float col[PY];
+#pragma unroll
+            for (int a = 0; a < PY; ++a) col[a] = d[a][bb][k];
+            YT::bt(col);
+#pragma unroll
+            for (int a = 0; a < PY; ++a) d[a][bb][k] = col[a];
+        }
     const int64_t stride = g.T * C;
     if constexpr (X3O) {
         unsigned short* o = reinterpret_cast<unsigned short*>(U) + t * C + c;
-        const int64_t pstride = (int64_t)16 * P * stride;
+        const int64_t pstride = (int64_t)PY * 4 * P * stride;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < PY; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
@@ -1963,7 +1977,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     }
     float* o = U + t * C + c;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
@@ -2034,15 +2048,16 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
         }
     if constexpr (X3O) {
         unsigned short* out = reinterpret_cast<unsigned short*>(V) + (int64_t)np_ * (KN / Np) + kp;
-        const int64_t pstride = (int64_t)16 * P * KN;
+        const int64_t pstride = (int64_t)PY * 4 * P * KN;
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                float o[4];
-                g3(t2[0][b][k], t2[1][b][k], t2[2][b][k], o);
+                float o[PY];
+                const float gy[3] = {t2[0][b][k], t2[1][b][k], t2[2][b][k]};
+                YT::g(gy, o);
 #pragma unroll
-                for (int a = 0; a < 4; ++a) {
+                for (int a = 0; a < PY; ++a) {
                     uint32_t hh, mm, ll;
                     split3(o[a], hh, mm, ll);
                     unsigned short* q = out + (int64_t)((a * 4 + b) * P + k) * KN;
@@ -2058,10 +2073,11 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            float o[4];
-            g3(t2[0][b][k], t2[1][b][k], t2[2][b][k], o);
+            float o[PY];
+            const float gy[3] = {t2[0][b][k], t2[1][b][k], t2[2][b][k]};
+            YT::g(gy, o);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) out[(int64_t)((a * 4 + b) * P + k) * KN] = o[a];
+            for (int a = 0; a < PY; ++a) out[(int64_t)((a * 4 + b) * P + k) * KN] = o[a];
         }
 }
 
@@ -2093,35 +2109,41 @@ __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, c
     tile_coords(t, g, b, ty, tx, tz);
     const int64_t stride = g.T * N;
     const float* src = Mt + t * N + n;
-    float m[4][4][P];
+    float m[PY][4][P];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
             for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
-    float r1[4][4][NZ];
+    float r1[PY][4][NZ];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
-    float r2[4][2][NZ];
+    float r2[PY][2][NZ];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int k = 0; k < NZ; ++k)
             at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
-    float o[2][2][NZ];
+    float o[WNY][2][NZ];
 #pragma unroll
     for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-        for (int k = 0; k < NZ; ++k)
-            at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
+        for (int k = 0; k < NZ; ++k) {
+            float col[PY], oy[WNY];
+#pragma unroll
+            for (int a = 0; a < PY; ++a) col[a] = r2[a][bb][k];
+            YT::at(col, oy);
+#pragma unroll
+            for (int a = 0; a < WNY; ++a) o[a][bb][k] = oy[a];
+        }
     const float bias = e.bias ? e.bias[n] : 0.0f;
     const float sc = e.scale ? e.scale[n] : 1.0f, sh = e.scale ? e.shift[n] : 0.0f;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int y = 2 * ty + a;
+    for (int a = 0; a < WNY; ++a) {
+        const int y = WNY * ty + a;
         if (y >= g.H) continue;
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
@@ -2179,46 +2201,52 @@ __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __rest
         tile_coords(t, g, b, ty, tx, tz);
         const int64_t stride = g.T * N;
         const float* src = Mt + t * N + n;
-        float m[4][4][P];
+        float m[PY][4][P];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < PY; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
                 for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
-        float r1[4][4][NZ];
+        float r1[PY][4][NZ];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < PY; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
-        float r2[4][2][NZ];
+        float r2[PY][2][NZ];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < PY; ++a)
 #pragma unroll
             for (int k = 0; k < NZ; ++k)
                 at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
-        float o[2][2][NZ];
+        float o[WNY][2][NZ];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-            for (int k = 0; k < NZ; ++k)
-                at4(r2[0][bb][k], r2[1][bb][k], r2[2][bb][k], r2[3][bb][k], o[0][bb][k], o[1][bb][k]);
+            for (int k = 0; k < NZ; ++k) {
+                float col[PY], oy[WNY];
+#pragma unroll
+                for (int a = 0; a < PY; ++a) col[a] = r2[a][bb][k];
+                YT::at(col, oy);
+#pragma unroll
+                for (int a = 0; a < WNY; ++a) o[a][bb][k] = oy[a];
+            }
         const float sc = e.fscale ? e.fscale[n] : 1.0f;
         const float mu = e.fz ? e.fmean[n] : 0.0f, rs = e.fz ? e.frstd[n] : 1.0f;
         // per output row pair a: its loads (old dx, y, z) before its stores -- a load
         // issued after a store to a possibly aliasing address waits for it -- in two
         // halves, so only 2 x 2 x NZ x 3 loaded values are live beside o
         const int64_t ostr = (int64_t)g.D * e.ldy;             // output x step
-        const int64_t obase = ((((int64_t)b * g.H + 2 * ty) * g.W + 2 * tx) * g.D + NZ * tz) * e.ldy + n;
+        const int64_t obase = ((((int64_t)b * g.H + WNY * ty) * g.W + 2 * tx) * g.D + NZ * tz) * e.ldy + n;
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
+        for (int a = 0; a < WNY; ++a) {
             float ov[2][NZ], yv[2][NZ], zv[2][NZ];
             bool in[2][NZ];
 #pragma unroll
             for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) {
-                    in[bb][k] = 2 * ty + a < g.H && 2 * tx + bb < g.W && NZ * tz + k < g.D;
+                    in[bb][k] = WNY * ty + a < g.H && 2 * tx + bb < g.W && NZ * tz + k < g.D;
                     const int64_t off = obase + (a * (int64_t)g.W + bb) * ostr + k * e.ldy;
                     ov[bb][k] = in[bb][k] && e.accumulate ? e.y[off] : 0.0f;
                     yv[bb][k] = in[bb][k] && e.frelu ? e.fy[off] : 1.0f;
@@ -2281,26 +2309,26 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
     const int64_t t = i / N;
     int b, ty, tx, tz;
     tile_coords(t, g, b, ty, tx, tz);
-    float ev[2][2][NZ];
+    float ev[WNY][2][NZ];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WNY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
             for (int k = 0; k < NZ; ++k) {
-                const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
+                const int y = WNY * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
                 ev[a][bb][k] = (y < g.H && xx < g.W && z < g.D)
                                    ? dz[((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * N + n]
                                    : 0.0f;
             }
-    float t1[2][2][P];
+    float t1[WNY][2][P];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WNY; ++a)
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) ZT<NZ>::a(ev[a][bb], t1[a][bb]);
-    float t2[2][4][P];
+    float t2[WNY][4][P];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WNY; ++a)
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             float o[4];
@@ -2314,10 +2342,12 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            float o[4];
-            a4(t2[0][bb][k], t2[1][bb][k], o);
+            float ey[WNY], o[PY];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) wino_st(out + (int64_t)((a * 4 + bb) * P + k) * stride, o[a]);
+            for (int a = 0; a < WNY; ++a) ey[a] = t2[a][bb][k];
+            YT::a(ey, o);
+#pragma unroll
+            for (int a = 0; a < PY; ++a) wino_st(out + (int64_t)((a * 4 + bb) * P + k) * stride, o[a]);
         }
 }
 
@@ -2331,6 +2361,7 @@ template <int NZ>
 __global__ __launch_bounds__(256) void wino_grad4_kernel(const float* __restrict__ dz, WinoGeom g,
                                                          int N, float* __restrict__ DY) {
     constexpr int P = ZT<NZ>::P;
+    static_assert(WNY == 2, "wino_grad4_kernel: F(2,3) on y only");
     const int N4 = N >> 2;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.T * N4) return;
@@ -2398,21 +2429,21 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t CN = (int64_t)C * N;
     if (i >= CN) return;
-    float v[4][4][P];
+    float v[PY][4][P];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int k = 0; k < P; ++k) v[a][b][k] = dWh[(int64_t)((a * 4 + b) * P + k) * CN + i];
-    float t1[4][4][3];
+    float t1[PY][4][3];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) ZT<NZ>::gt(v[a][b], t1[a][b]);
-    float t2[4][3][3];
+    float t2[PY][3][3];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < PY; ++a)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             float o[3];
@@ -2424,8 +2455,10 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
     for (int b = 0; b < 3; ++b)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            float o[3];
-            gt4(t2[0][b][k], t2[1][b][k], t2[2][b][k], t2[3][b][k], o);
+            float vy[PY], o[3];
+#pragma unroll
+            for (int a = 0; a < PY; ++a) vy[a] = t2[a][b][k];
+            YT::gt(vy, o);
 #pragma unroll
             for (int a = 0; a < 3; ++a) dw[(int64_t)((a * 3 + b) * 3 + k) * CN + i] += o[a];
         }
@@ -3148,7 +3181,7 @@ static int wino_dgrad_nz() {
     static constexpr int v = M3D_TUNE_WINO_DGRAD_NZ;   // 0: the forward's tile
     return v ? v : wino_nz();
 }
-static int wino_points(int nz) { return 16 * (nz + 2); }
+static int wino_points(int nz) { return PY * 4 * (nz + 2); }
 static int wino_points() { return wino_points(wino_nz()); }
 
 static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz,
@@ -3156,7 +3189,7 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     WinoGeom g;
     if (nz < 0) nz = wino_nz();
     g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
-    g.TY = (int)((H + 1) / 2); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
+    g.TY = (int)((H + WNY - 1) / WNY); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
     g.T = B * g.TY * g.TX * g.TZ;
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
@@ -4574,6 +4607,7 @@ static bool wino_per_item(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD
 
 extern "C" int32_t m3d_conv3d_wino_tile_z(void) { return wino_nz(); }
 extern "C" int32_t m3d_conv3d_wino_wgrad_tile_z(void) { return wino_wgrad_nz(); }
+extern "C" int32_t m3d_conv3d_wino_tile_y(void) { return WNY; }
 
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {

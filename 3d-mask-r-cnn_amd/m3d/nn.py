@@ -179,9 +179,10 @@ def _wgrad1_x3(geo, cin, cout, in_sp):
 
 
 def _wino_exec(B, OH, OW, OD, cin, cout, nz):
-    """MFMA FLOPs of the Winograd point GEMMs, F(2x2xnz): 16*(nz+2) points."""
-    tiles = B * -(-OH // 2) * -(-OW // 2) * -(-OD // nz)
-    return 2.0 * 16 * (nz + 2) * tiles * cin * cout
+    """MFMA FLOPs of the Winograd point GEMMs, F(ny x 2 x nz): (ny+2)*4*(nz+2) points."""
+    ny = int(_L().m3d_conv3d_wino_tile_y())
+    tiles = B * -(-OH // ny) * -(-OW // 2) * -(-OD // nz)
+    return 2.0 * (ny + 2) * 4 * (nz + 2) * tiles * cin * cout
 
 
 def _L():

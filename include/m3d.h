@@ -331,6 +331,7 @@ int32_t m3d_conv3d_wino_tile_z(void);
 /* z extent of the weight gradient's output tile (4: F(2x2x4), the forward's, whose
  * transformed input the forward keeps -- m3d_conv3d_wino_u_bytes > 0; 2: F(2x2x2)). */
 int32_t m3d_conv3d_wino_wgrad_tile_z(void);
+int32_t m3d_conv3d_wino_tile_y(void);   /* output tile rows along y (2: F(2,3), 4: F(4,3)) */
 size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin);
 int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
                              const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,

@@ -350,8 +350,11 @@ def test_batch_items_past_operand_bound(tmp_path):
         if k == "ws_bytes":
             continue
         if k.endswith("dw"):
+            # fp32 reassociation of the per-item sums; the Winograd weight gradient's
+            # G^T rows (4, 8/3, ... for F(4,3) axes) amplify it: 4e-5 there
             scale = float(np.abs(a[k]).max())
-            assert float(np.abs(a[k] - b[k]).max()) <= 1e-5 * scale, k
+            tol = 4e-5 if k.startswith("w") else 1e-5
+            assert float(np.abs(a[k] - b[k]).max()) <= tol * scale, k
         else:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
