@@ -99,28 +99,30 @@ def _pmc_traffic(kernel_key):
 
 def wgrad_gemm_shape(S):
     """The largest launch of the step's second kernel, x3_wgrad_tr_kernel: the
-    16*(NZ+2) batched Winograd weight-gradient GEMMs of rpn_conv_shared1
+    (NY+2)*4*(NZ+2) batched Winograd weight-gradient GEMMs of rpn_conv_shared1
     (3x3x3, 256->512) on P2 [S/4, S/4, S] -- F(2x2x4) tiles by default (96
     GEMMs on the forward's kept U; M3D_WINO_WGRAD_NZ=2: F(2x2x2), 64 GEMMs),
     reduction over M = T tiles, K = 256, N = 512."""
     from m3d import _lib
     nz = int(_lib.load().m3d_conv3d_wino_wgrad_tile_z())
+    ny = int(_lib.load().m3d_conv3d_wino_tile_y())
     q = S // 4
-    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
-    return 16 * (nz + 2), T, 256, 512
+    T = ((q + ny - 1) // ny) * ((q + 1) // 2) * ((S + nz - 1) // nz)
+    return (ny + 2) * 4 * (nz + 2), T, 256, 512
 
 
 def wino_gemm_shape(S):
     """The largest launch of the step's dominant kernel, x3_gemm256_af_kernel
     (17.7 % of the step's kernel time, profiles/r02i_bench_kernels_128.txt): the
-    16*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
+    (NY+2)*4*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
     256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles, K = 256,
     N = 512 (NZ = 4 by default: 96 GEMMs)."""
     from m3d import _lib
     nz = int(_lib.load().m3d_conv3d_wino_tile_z())
+    ny = int(_lib.load().m3d_conv3d_wino_tile_y())
     q = S // 4
-    T = ((q + 1) // 2) * ((q + 1) // 2) * ((S + nz - 1) // nz)
-    return 16 * (nz + 2), T, 256, 512
+    T = ((q + ny - 1) // ny) * ((q + 1) // 2) * ((S + nz - 1) // nz)
+    return (ny + 2) * 4 * (nz + 2), T, 256, 512
 
 
 def time_wino_gemm(S, reps=5):
@@ -207,9 +209,10 @@ def time_wino_fwd(S, reps=5):
                    "wino fwd")
     t = _event_time(launch, reps)
     nz = int(L.m3d_conv3d_wino_tile_z())
-    T = ((H + 1) // 2) * ((W + 1) // 2) * ((D + nz - 1) // nz)
+    ny = int(L.m3d_conv3d_wino_tile_y())
+    T = ((H + ny - 1) // ny) * ((W + 1) // 2) * ((D + nz - 1) // nz)
     return {"ms": round(t * 1e3, 4),
-            "gemm_tflops": round(2.0 * 16 * (nz + 2) * T * Cin * Cout / t / 1e12, 2),
+            "gemm_tflops": round(2.0 * (ny + 2) * 4 * (nz + 2) * T * Cin * Cout / t / 1e12, 2),
             "direct_conv_equivalent_tflops": round(2.0 * H * W * D * 27 * Cin * Cout / t / 1e12, 2)}
 
 
