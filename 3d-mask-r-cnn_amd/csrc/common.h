@@ -115,9 +115,12 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_X3_256
 #define M3D_TUNE_X3_256 1
 #endif
-// Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z
+// Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z.
+// 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
+// 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at
+// 128^3 (same box, r04ny4_ab), parity suite green (profiles/r04ny4_parity_tests.log)
 #ifndef M3D_TUNE_WINO_NY
-#define M3D_TUNE_WINO_NY 2
+#define M3D_TUNE_WINO_NY 4
 #endif
 #ifndef M3D_TUNE_WINO_NZ
 #define M3D_TUNE_WINO_NZ 4
