@@ -1715,8 +1715,10 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
 }
 
 // =========================================================================
-// Winograd F(2x2xNZ, 3x3x3) for stride-1 'same' 3x3x3 convs: F(2,3) along y
-// and x, F(NZ,3) along z (NZ = 2, or 4 by default).
+// Winograd F(NYx2xNZ, 3x3x3) for stride-1 'same' 3x3x3 convs: F(NY,3) along y
+// (NY = M3D_TUNE_WINO_NY: 4 by default since round 4, 2), F(2,3) along x,
+// F(NZ,3) along z (NZ = 2, or 4 by default).  The F(2,3) formulas below are
+// written for y and x; with NY = 4 the y axis takes the F(4,3) ones (ZT<4>).
 //   fwd:   Y   = A^T [ (G W G^T) . (B^T X B) ] A        (per 2x2xNZ output tile)
 //   dgrad: dX  = same with W'[t][n][c] = W[flip t][c][n]
 //   wgrad: dW  = G^T [ sum_tiles (B^T X B) . (A dZ A^T) ] G
