@@ -100,6 +100,13 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 #ifndef M3D_TUNE_X3W_DBG
 #define M3D_TUNE_X3W_DBG 0
 #endif
+// wave-quantised m-splits for the 256x256 weight-gradient kernel (A/B only):
+// Q = 8 / 16 measured 25.5 / 25.45 vs 25.2-25.4 ms at 128^3 and 149.2-149.6 vs
+// 148.3-148.5 ms at 256^3 (profiles/r04q_wgrad_quant_ab.txt): the kernel runs on
+// the side stream beside the data gradient, which fills the tail wave anyway.
+#ifndef M3D_TUNE_X3W_TR_QUANT
+#define M3D_TUNE_X3W_TR_QUANT 0
+#endif
 #ifndef M3D_TUNE_X3W_TR_MIN_M
 #define M3D_TUNE_X3W_TR_MIN_M 0
 #endif

@@ -1660,6 +1660,19 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
+    // M3D_X3W_TR_QUANT=Q (A/B): pick splits in [1, max(splits, Q)] minimising
+    // the number of one-per-CU waves per unit of work, ceil(tiles * s / CUs) / s
+    // (e.g. the F(4x2x4) RPN gradient: 288 tiles = 1.125 waves run as 2 at
+    // s = 1, 9 / 8 at s = 8), within the m floor above.
+    static constexpr int quant = M3D_TUNE_X3W_TR_QUANT;
+    if constexpr (quant > 1) {
+        double best = 1e30;
+        const int64_t qmax = splits > quant ? splits : quant;
+        for (int64_t q = 1; q <= qmax && q <= max_splits; ++q) {
+            const double cost = (double)((tiles * q + cus - 1) / cus) / (double)q;
+            if (cost < best - 1e-9) { best = cost; splits = q; }
+        }
+    }
     const WgOut wo = wg_out(splits, nbatch, K, N);
     int64_t mper = (M + splits - 1) / splits;
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
