@@ -104,6 +104,13 @@ int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, con
 // Q = 8 / 16 measured 25.5 / 25.45 vs 25.2-25.4 ms at 128^3 and 149.2-149.6 vs
 // 148.3-148.5 ms at 256^3 (profiles/r04q_wgrad_quant_ab.txt): the kernel runs on
 // the side stream beside the data gradient, which fills the tail wave anyway.
+// small-m weight gradients: lower the m floor until the grid fills the chip
+// (A/B only): 128^3 25.19 vs 25.18 ms with the RPN heads' gradient on the side
+// stream, 25.19 vs 25.31-25.38 ms without (profiles/r04s_rpn_wgrad_ab.txt) --
+// the side stream alone removes the same cost from the critical path.
+#ifndef M3D_TUNE_WGRAD_FILL
+#define M3D_TUNE_WGRAD_FILL 0
+#endif
 #ifndef M3D_TUNE_X3W_TR_QUANT
 #define M3D_TUNE_X3W_TR_QUANT 0
 #endif

@@ -1291,7 +1291,16 @@ template <int BI, int BJ, int WI, int WJ, bool AVEC, bool HALO = false>
 static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s, int nbatch = 1) {
     const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;                   // aim >= 1024 blocks
-    const int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
+    int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
+    // M3D_TUNE_WGRAD_FILL: a launch whose grid at that floor is below one
+    // workgroup per CU (small-m gradients: the RPN heads' 1x1x1 weight gradient
+    // on P3-P6 ran 4-32 workgroups of 512 rows, ~38 us each regardless of m)
+    // halves the floor down to 64 rows until it fills the chip.
+    static constexpr int fill = M3D_TUNE_WGRAD_FILL;
+    if constexpr (fill != 0) {
+        const int64_t cus = num_cus();
+        while (minm > 64 && tiles * ((p.M + minm - 1) / minm) < cus) minm /= 2;
+    }
     const int64_t max_splits = (p.M + minm - 1) / minm;             // >= minm m per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -1710,7 +1719,12 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     // M3D_X3W_MINM: this kernel's m-split floor (default: M3D_WGRAD_MINM's)
     static constexpr int x3w_minm = M3D_TUNE_X3W_MINM;
     const int64_t mfloor = x3w_minm > 0 ? x3w_minm : wgrad_minm_env();
-    const int64_t minm = mfloor > 32 ? mfloor : 32;
+    int64_t minm = mfloor > 32 ? mfloor : 32;
+    static constexpr int fill = M3D_TUNE_WGRAD_FILL;   // as in launch_wgrad
+    if constexpr (fill != 0) {
+        const int64_t cus = num_cus();
+        while (minm > 64 && tiles * ((M + minm - 1) / minm) < cus) minm /= 2;
+    }
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;

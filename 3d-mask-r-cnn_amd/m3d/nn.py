@@ -1045,6 +1045,11 @@ def subsample221(x):
     return _Subsample221.apply(x.contiguous())
 
 
+# M3D_RPN_OUT_SIDE=0 keeps the RPN class/bbox heads' weight gradient on the
+# compute stream (A/B)
+RPN_OUT_SIDE = os.environ.get("M3D_RPN_OUT_SIDE", "1") != "0"
+
+
 class _RPNOut(torch.autograd.Function):
     """The RPN class/bbox 1x1x1 heads (rpn_class_raw, rpn_bbox_pred;
     core/models.py:540-556) of all pyramid levels in one function.  Each level's
@@ -1128,9 +1133,16 @@ class _RPNOut(torch.autograd.Function):
                     bn_act_bwd(dz, None, None, r, npad, False, None, None, None, None, None, None,
                                None, grads["bias"])
                 if grads.get("kernel") is not None:
-                    check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
-                                                  W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
-                                                  stream()), "rpn_out_wgrad")
+                    # on the weight-gradient stream like every conv unit's (joined before the
+                    # update); the data gradients below do not wait for it
+                    side = _wgrad_stream(dev) if RPN_OUT_SIDE else None
+                    if side is not None:
+                        dz_all.record_stream(side)
+                        s.record_stream(side)
+                    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                        check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
+                                                      W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
+                                                      stream()), "rpn_out_wgrad")
                 if fws[li] is not None:
                     # rpn_conv_shared2's ReLU backward (and bias sums) in this data gradient's epilogue
                     dres_f, bws, bwsb = fws[li]
