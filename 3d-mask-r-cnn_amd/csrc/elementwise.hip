@@ -207,17 +207,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float4* __restr
     }
 }
 
+// IDX: the index type of the element loop (uint32_t when the source has < 2^32
+// float4s: the 64-bit div/mod of the decomposition are software sequences)
+template <typename IDX>
 __global__ void upsample221_bwd_kernel(const float4* __restrict__ dup, int B, int H, int W, int D,
                                        int C4, float4* __restrict__ dsrc, int accumulate) {
-    const int64_t total = (int64_t)B * H * W * D * C4;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C4);
-        int64_t t = i / C4;
-        const int z = (int)(t % D); t /= D;
-        const int x = (int)(t % W); t /= W;
-        const int y = (int)(t % H);
-        const int b = (int)(t / H);
+    const IDX total = (IDX)B * H * W * D * C4;
+    for (IDX i = (IDX)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (IDX)gridDim.x * blockDim.x) {
+        const int c = (int)(i % (IDX)C4);
+        IDX t = i / (IDX)C4;
+        const int z = (int)(t % (IDX)D); t /= (IDX)D;
+        const int x = (int)(t % (IDX)W); t /= (IDX)W;
+        const int y = (int)(t % (IDX)H);
+        const int b = (int)(t / (IDX)H);
         float4 acc = accumulate ? dsrc[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         for (int a = 0; a < 2; ++a)
             for (int q = 0; q < 2; ++q) {
@@ -725,9 +728,14 @@ extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int6
     if (C == 0) return einval("upsample221_bwd: C must be a positive multiple of 4");
     const int64_t total = B * H * W * D * (C / 4);
     if (total == 0) return M3D_OK;
-    hipLaunchKernelGGL(upsample221_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st(s),
-                       (const float4*)d_up, (int)B, (int)H, (int)W, (int)D, (int)(C / 4),
-                       (float4*)d_src, accumulate);
+    if (total + (int64_t)ew_grid(total) * 256 < ((int64_t)1 << 32))
+        hipLaunchKernelGGL(upsample221_bwd_kernel<uint32_t>, dim3(ew_grid(total)), dim3(256), 0, st(s),
+                           (const float4*)d_up, (int)B, (int)H, (int)W, (int)D, (int)(C / 4),
+                           (float4*)d_src, accumulate);
+    else
+        hipLaunchKernelGGL(upsample221_bwd_kernel<int64_t>, dim3(ew_grid(total)), dim3(256), 0, st(s),
+                           (const float4*)d_up, (int)B, (int)H, (int)W, (int)D, (int)(C / 4),
+                           (float4*)d_src, accumulate);
     return check_launch("upsample221_bwd_kernel");
 }
 
