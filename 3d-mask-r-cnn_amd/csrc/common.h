@@ -28,16 +28,30 @@ inline int check_launch(const char* what) {
 
 inline hipStream_t st(m3d_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Deterministic mode (m3d_set_deterministic): the reductions that would add
-// fp32 partial sums with atomics in arrival order (weight-gradient m-splits,
-// per-tensor clip norms) write the partials into the registered scratch and
-// sum them in a fixed order instead.
+// Deterministic reductions (m3d_det_t, include/m3d.h): the reductions that
+// would add fp32 partial sums with atomics in arrival order (weight-gradient
+// m-splits, per-tensor clip norms) write the partials into the call's scratch
+// and sum them in a fixed order instead.  The entry points taking a det open a
+// DetScope for the duration of the call (M3D_DET_SCOPE): the launch helpers
+// below them read it through det().  The scope is thread-local and ends with
+// the call, so the library holds no mode between calls (reentrant).
 struct DetState {
     int on;
     void* scratch;
     size_t bytes;
 };
-const DetState& det();
+DetState det();
+int det_check(const m3d_det_t* d);
+struct DetScope {
+    const m3d_det_t* prev;
+    explicit DetScope(const m3d_det_t* d);
+    ~DetScope();
+    DetScope(const DetScope&) = delete;
+    DetScope& operator=(const DetScope&) = delete;
+};
+#define M3D_DET_SCOPE(d)                                   \
+    if (int det_rc_ = ::m3d::det_check(d)) return det_rc_; \
+    ::m3d::DetScope det_scope_(d)
 
 inline unsigned grid_for(int64_t n, int per_block, int64_t cap = 1 << 30) {
     int64_t g = (n + per_block - 1) / per_block;
@@ -56,6 +70,13 @@ int bn_sums_reduce(const float* part, int64_t rows, int64_t C, float* s0, float*
 int64_t bn_act_bwd_rows(int64_t M, int64_t C);
 int bn_act_bwd_splitk(const float* slices, int splits, int64_t M, int64_t C, const m3d_bn_bwd_t* bn,
                       float* dx, int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
+
+// topk.hip: stable sort of n uint64 keys (ascending / descending) with their
+// positions (pos[i], or i when pos is NULL) through rank_sort_scratch_bytes(n)
+// of device scratch; signed_out: write key ^ 2^63 (int64 order)
+size_t rank_sort_scratch_bytes(int64_t n);
+int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, bool signed_out, uint32_t* scratch,
+                  uint64_t* out_u, int64_t* out_pos, hipStream_t s);
 
 }  // namespace m3d
 

@@ -916,7 +916,7 @@ __global__ __launch_bounds__(256) void wg_reduce_kernel(const float* __restrict_
 // (splits may be lowered to what the scratch holds)
 static WgOut wg_out(int64_t& splits, int64_t nbatch, int64_t K, int64_t N) {
     WgOut o{nullptr, 0, 0};
-    const DetState& d = det();
+    const DetState d = det();
     if (!d.on) return o;
     const int64_t per = nbatch * K * N;
     const int64_t fit = (int64_t)(d.bytes / sizeof(float)) / per;
@@ -1154,15 +1154,13 @@ static int gemm_persist_env() {
     static constexpr int v = M3D_TUNE_GEMM_PERSIST;
     return v;
 }
+// CUs of the calling thread's current device, asked per call (the runtime
+// answers from its device table): nothing is cached across calls or devices
 static int num_cus() {
-    static int v = [] {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
-    return v;
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
 }
 
 // M3D_GEMM_X3 (bit mask, default 31): fp32 GEMMs on the exact 3-way bf16 split
@@ -3268,7 +3266,8 @@ extern "C" int m3d_gemm_f32(const float* A, const float* Bm, float* C, int64_t b
 }
 
 extern "C" int m3d_gemm_wgrad_f32(const float* A, const float* Bm, float* C, int64_t batch, int64_t M,
-                                  int64_t K, int64_t N, m3d_stream_t s) {
+                                  int64_t K, int64_t N, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     if (batch <= 0 || M <= 0 || K <= 0 || N <= 0) return einval("gemm_wgrad: dimensions must be positive");
     if (K % 4 || N % 4) return einval("gemm_wgrad: K and N must be multiples of 4");
     const int64_t lim = (int64_t)0xFFFFFFF0 / 4;
@@ -4069,13 +4068,7 @@ static bool stem_wgrad_env() {
 }
 
 static int launch_stem_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s) {
-    static int ncu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
+    const int ncu = num_cus();
     const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
     const int64_t ntiles = (int64_t)p.B * p.OH * p.OW * tz_n;
     // two workgroups per CU (LDS 2 x 23.4 KB each, 8 waves), >= 8 m-tiles each
@@ -4089,13 +4082,7 @@ static int launch_stem_wgrad(const ConvP& p, const float* dz, float* dw, hipStre
 }
 
 static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
-    static int ncu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
+    const int ncu = num_cus();
     const int tz_n = (p.OD + STEM_TZ - 1) / STEM_TZ;
     const int64_t ntiles = (int64_t)p.B * p.OH * p.OW * tz_n;
     // about four workgroups per CU, not one persistent workgroup per CU: the
@@ -4491,13 +4478,14 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
                                      int64_t W, int64_t D, int64_t Cin, int32_t kh, int32_t kw,
                                      int32_t kd, int64_t Cout, int64_t OH, int64_t OW, int64_t OD,
                                      int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px,
-                                     int32_t pz, float* dw, m3d_stream_t s) {
+                                     int32_t pz, float* dw, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     int rc = conv_check(B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
     if (rc) return rc;
     if (per_item(B, H * W * D, Cin, OH * OW * OD, Cout)) {      // dw accumulates over the items
         for (int64_t b = 0; b < B; ++b) {
             rc = m3d_conv3d_bwd_weight(x + b * H * W * D * Cin, dz + b * OH * OW * OD * Cout, 1, H, W, D, Cin, kh,
-                                       kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px, pz, dw, s);
+                                       kw, kd, Cout, OH, OW, OD, sy, sx, sz, py, px, pz, dw, det, s);
             if (rc) return rc;
         }
         return M3D_OK;
@@ -4580,7 +4568,8 @@ extern "C" int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int
                                           int32_t r, const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl,
                                           int64_t Cin, int32_t kh, int32_t kw, int32_t kd, int64_t Cout,
                                           int64_t OH, int64_t OW, int64_t OD, int32_t sy, int32_t sx, int32_t sz,
-                                          int32_t py, int32_t px, int32_t pz, float* dw, m3d_stream_t s) {
+                                          int32_t py, int32_t px, int32_t pz, float* dw, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     int rc = conv_check(B, H, W, Dl, Cin, kh, kw, kd, Cout, OH, OW, OD, sy, sx, sz);
     if (rc) return rc;
     if (B * H * W * (Dl + 2 * r) * Cin >= op_lim() || B * OH * OW * OD * Cout >= op_lim())
@@ -5205,7 +5194,8 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
 extern "C" int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H,
                                           int64_t W, int64_t D, int64_t Cin, int64_t Cout,
                                           int64_t OD, int32_t pz, float* dw, void* workspace,
-                                          size_t ws_bytes, m3d_stream_t s) {
+                                          size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     return bwd_weight_wino(x, nullptr, dz, B, H, W, D, Cin, Cout, OD, pz, dw, workspace, ws_bytes, s);
 }
 
@@ -5274,7 +5264,8 @@ extern "C" int m3d_conv3d_bwd_data_wino_halo(const float* dz, const float* w, in
 extern "C" int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_halo, int32_t has_lo,
                                                int32_t has_hi, const float* dz, int64_t B, int64_t H, int64_t W,
                                                int64_t Dl, int64_t Cin, int64_t Cout, float* dw, void* workspace,
-                                               size_t ws_bytes, m3d_stream_t s) {
+                                               size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     int rc = halo_check(x_halo, has_lo, has_hi);
     if (rc) return rc;
     return bwd_weight_wino(x, nullptr, dz, B, H, W, Dl, Cin, Cout, Dl, 1, dw, workspace, ws_bytes, s, x_halo,
@@ -5284,7 +5275,8 @@ extern "C" int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_ha
 extern "C" int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H,
                                             int64_t W, int64_t D, int64_t Cin, int64_t Cout,
                                             int64_t OD, int32_t pz, float* dw, void* workspace,
-                                            size_t ws_bytes, m3d_stream_t s) {
+                                            size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     if (!u) return einval("conv3d winograd: u must not be NULL");
     return bwd_weight_wino(nullptr, u, dz, B, H, W, D, Cin, Cout, OD, pz, dw, workspace, ws_bytes, s);
 }

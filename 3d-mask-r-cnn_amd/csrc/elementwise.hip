@@ -882,7 +882,7 @@ static int clip_norms(const float* params, const float* grads, int64_t n_chunks,
                       const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
                       float clipnorm, float* norms, m3d_stream_t s) {
     if (!(clipnorm > 0.f)) return M3D_OK;
-    const DetState& d = det();
+    const DetState d = det();
     if (d.on) {
         if (d.bytes < sizeof(float) * (size_t)n_chunks)
             return einval("clip norms (deterministic mode): scratch smaller than n_chunks floats");
@@ -905,7 +905,8 @@ static int clip_norms(const float* params, const float* grads, int64_t n_chunks,
 extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
                              const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
                              float lr, float momentum, float clipnorm, float* norms,
-                             m3d_stream_t s) {
+                             const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     if (n_chunks < 0 || n_segments < 0) return einval("sgd: negative chunk or segment count");
     if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !moments || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
@@ -920,7 +921,8 @@ extern "C" int m3d_sgd_keras(float* params, const float* grads, float* moments, 
 extern "C" int m3d_adam_keras(float* params, const float* grads, float* m, float* v, float* vhat,
                               int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                               int32_t n_segments, float lr_t, float beta_1, float beta_2,
-                              float epsilon, float clipnorm, float* norms, m3d_stream_t s) {
+                              float epsilon, float clipnorm, float* norms, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     if (n_chunks < 0 || n_segments < 0) return einval("adam: negative chunk or segment count");
     if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !m || !v || !seg_of_chunk || !l2_coef || (clipnorm > 0.f && !norms))
@@ -942,7 +944,8 @@ extern "C" int m3d_adam_keras(float* params, const float* grads, float* m, float
 extern "C" int m3d_adadelta_keras(float* params, const float* grads, float* accum, float* delta_accum,
                                   int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                                   int32_t n_segments, float lr, float rho, float epsilon,
-                                  float clipnorm, float* norms, m3d_stream_t s) {
+                                  float clipnorm, float* norms, const m3d_det_t* det, m3d_stream_t s) {
+    M3D_DET_SCOPE(det);
     if (n_chunks < 0 || n_segments < 0) return einval("adadelta: negative chunk or segment count");
     if (n_chunks == 0) return M3D_OK;
     if (!params || !grads || !accum || !delta_accum || !seg_of_chunk || !l2_coef ||

@@ -1579,15 +1579,18 @@ __global__ __launch_bounds__(256) void crop_bwd_det_col_kernel(
 }
 
 // launch of the deterministic grad_image into one image set: the column-list
-// kernel when the boxes fit its list, else crop_bwd_det_kernel
+// kernel when the boxes fit its list and its one-block-per-(column, chunk
+// group) grid fits the launch limit (grid x * 256 threads < 2^32), else
+// crop_bwd_det_kernel (block-strided, capped grid); both are bit-identical to
+// the sequential replay
 static void launch_det_bwd(const float* grads, const float* boxes, const int32_t* box_ind, int64_t N, int ch,
                            int cw, int cd, int64_t B, int64_t H, int64_t W, int64_t D, int64_t C, int method,
                            float* gimg, hipStream_t s) {
     const bool v4 = (C & 3) == 0;
     const int64_t cvn = v4 ? C / 4 : C;
     const int64_t nchunks = (D * cvn + 255) / 256;
-    if (N <= DET_CAP) {
-        const int64_t bpc = (nchunks + DET_CHUNKS - 1) / DET_CHUNKS;
+    const int64_t bpc = (nchunks + DET_CHUNKS - 1) / DET_CHUNKS;
+    if (N <= DET_CAP && B * H * W * bpc < ((int64_t)1 << 24)) {
         const int64_t nblk = B * H * W * bpc;
         if (v4)
             hipLaunchKernelGGL(crop_bwd_det_col_kernel<4>, dim3((unsigned)nblk), dim3(256), 0, s, grads, boxes,

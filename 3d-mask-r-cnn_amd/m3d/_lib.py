@@ -25,6 +25,11 @@ c_p = ctypes.c_void_p
 c_sz = ctypes.c_size_t
 
 
+class Det(ctypes.Structure):
+    """m3d_det_t (include/m3d.h): the deterministic-reduction target of one call."""
+    _fields_ = [("on", ctypes.c_int32), ("scratch", ctypes.c_void_p), ("bytes", ctypes.c_size_t)]
+
+
 class BnBwd(ctypes.Structure):
     """m3d_bn_bwd_t (include/m3d.h): the producing unit's BN-ReLU backward fused
     into a data-gradient epilogue."""
@@ -57,6 +62,8 @@ _SIGS = {
     "m3d_nms3d_workspace_bytes": [c_i64],
     "m3d_nms3d": [c_p, c_p, c_i64, c_i32, c_f, c_i32, c_p, c_p, c_p, c_sz, c_p],
     "m3d_score_keys": [c_p, c_i64, c_p, c_p],
+    "m3d_topk_workspace_bytes": [c_i64, c_i64],
+    "m3d_topk_keys": [c_p, c_i64, c_i64, c_p, c_p, c_p, c_sz, c_p],
     "m3d_score_keys_mapped": [c_p, c_i64, c_p, c_p, c_p],
     "m3d_proposal_decode": [c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_f, c_p, c_p, c_p, c_p],
     "m3d_proposal_gather": [c_p, c_p, c_p, c_i32, c_p, c_p],
@@ -89,7 +96,7 @@ _SIGS = {
                             c_p, c_i32, c_p],
     "m3d_conv3d_bwd_weight": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
                               c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
-                              c_p, c_p],
+                              c_p, c_p, c_p],
     "m3d_conv3d_fwd_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p,
                                  c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p],
     "m3d_conv3d_fwd_wino_halo_phase": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
@@ -97,9 +104,9 @@ _SIGS = {
     "m3d_conv3d_bwd_data_wino_halo": [c_p, c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
                                       c_p, c_i32, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_weight_wino_halo": [c_p, c_p, c_i32, c_i32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
-                                        c_p, c_p, c_sz, c_p],
+                                        c_p, c_p, c_sz, c_p, c_p],
     "m3d_gemm_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_i32, c_p],
-    "m3d_gemm_wgrad_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
+    "m3d_gemm_wgrad_f32": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_split3_f32": [c_p, c_i64, c_p, c_p],
     "m3d_gemm_x3": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
     "m3d_gemm_x3_af": [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p],
@@ -109,7 +116,7 @@ _SIGS = {
     "m3d_conv3d_bwd_data_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32,
                                  c_p, c_i32, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_weight_wino": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
-                                   c_i32, c_p, c_p, c_sz, c_p],
+                                   c_i32, c_p, c_p, c_sz, c_p, c_p],
     "m3d_conv3d_wino_u_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "m3d_conv3d_wino_tile_z": [],
     "m3d_conv3d_wino_wgrad_tile_z": [],
@@ -117,7 +124,7 @@ _SIGS = {
     "m3d_conv3d_fwd_wino_keep": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
                                  c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_weight_wino_u": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
-                                     c_i32, c_p, c_p, c_sz, c_p],
+                                     c_i32, c_p, c_p, c_sz, c_p, c_p],
     "m3d_gemm_f32_ex": [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
                         c_i32, c_i32, c_p],
     "m3d_splitk_reduce": [c_p, c_i32, c_i64, c_i64, c_p, c_p, c_p, c_i32, c_p, c_p],
@@ -150,7 +157,7 @@ _SIGS = {
                             c_p, c_i32, c_p, c_p, c_p],
     "m3d_conv3d_bwd_weight_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32,
                                    c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32,
-                                   c_i32, c_p, c_p],
+                                   c_i32, c_p, c_p, c_p],
     "m3d_maxpool3d_fwd_halo": [c_p, c_p, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32,
                                c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_p,
                                c_p],
@@ -164,22 +171,22 @@ _SIGS = {
     "m3d_bn_act_bwd_workspace_bytes": [c_i64, c_i64],
     "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
                        c_p, c_p, c_p, c_sz, c_p],
-    "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p],
+    "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p, c_p],
     "m3d_adam_keras": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_f, c_p,
-                       c_p],
-    "m3d_adadelta_keras": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_p, c_p],
-    "m3d_set_deterministic": [c_i32, c_p, c_sz],
-    "m3d_stream_fork": [c_p, c_p, c_i32],
-    "m3d_get_deterministic": [],
+                       c_p, c_p],
+    "m3d_adadelta_keras": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_p, c_p, c_p],
+    "m3d_fork_event_create": [c_i32, ctypes.POINTER(c_p)],
+    "m3d_fork_event_destroy": [c_p],
+    "m3d_stream_fork": [c_p, c_p, c_p],
 }
 _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_sz,
+             "m3d_topk_workspace_bytes": c_sz,
              "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_rpn_loss_workspace_bytes": c_sz,
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
-             "m3d_conv3d_wino_tile_y": c_i32,
-             "m3d_get_deterministic": c_i32}
+             "m3d_conv3d_wino_tile_y": c_i32}
 
 EXPORTED = tuple(_SIGS)
 
@@ -202,8 +209,37 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
-    _lib = lib
-    return lib
+    _lib = _Lib(lib)
+    return _lib
+
+
+# Entry points taking a per-call m3d_det_t before their stream (ABI 3).  Called
+# through load() with the ABI-2 argument list, they receive the deterministic
+# target of this process's mode (set_deterministic) -- the mode is the host's
+# choice, kept here; libm3d itself holds none.
+DET_ENTRY_POINTS = ("m3d_conv3d_bwd_weight", "m3d_conv3d_bwd_weight_halo", "m3d_conv3d_bwd_weight_wino",
+                    "m3d_conv3d_bwd_weight_wino_u", "m3d_conv3d_bwd_weight_wino_halo", "m3d_gemm_wgrad_f32",
+                    "m3d_sgd_keras", "m3d_adam_keras", "m3d_adadelta_keras")
+
+
+class _Lib:
+    """The loaded CDLL; the DET_ENTRY_POINTS called without their det argument
+    get det_arg() inserted before the stream."""
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        for name in DET_ENTRY_POINTS:
+            fn = getattr(cdll, name)
+            n = len(fn.argtypes)
+
+            def call(*args, _fn=fn, _n=n):
+                if len(args) == _n - 1:
+                    args = args[:-1] + (det_arg(),) + args[-1:]
+                return _fn(*args)
+            setattr(self, name, call)
+
+    def __getattr__(self, name):
+        return getattr(self._cdll, name)
 
 
 def check(rc: int, what: str = "") -> None:
@@ -226,24 +262,34 @@ def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-_DET_SCRATCH = None
+_DET = None            # (Det struct, scratch tensor) while deterministic mode is on
+
+
+def det_arg():
+    """The m3d_det_t pointer the DET_ENTRY_POINTS get in this process's mode
+    (None = atomic reductions)."""
+    return None if _DET is None else ctypes.addressof(_DET[0])
+
+
+def deterministic() -> bool:
+    return _DET is not None
 
 
 def set_deterministic(on: bool = True, scratch_bytes: int = 256 << 20, device=None) -> None:
-    """Bitwise run-to-run reproducible training (m3d_set_deterministic): the
-    weight-gradient m-splits and the clip norms are summed in a fixed order
-    through a device scratch of ``scratch_bytes`` instead of fp32 atomics.  The
-    scratch is shared by those reductions, so they must stay ordered on one
-    stream at a time (the training step's weight-gradient stream, then the
-    optimizer after the join).  A weight gradient larger than half the scratch
-    runs unsplit (still deterministic, slower)."""
-    global _DET_SCRATCH
-    lib = load()
+    """Bitwise run-to-run reproducible training: the weight-gradient m-splits
+    and the clip norms are summed in a fixed order through a device scratch of
+    ``scratch_bytes`` instead of fp32 atomics (every weight-gradient / optimizer
+    call of this process passes it as its m3d_det_t).  The scratch is shared by
+    those reductions, so they must stay ordered on one stream at a time (the
+    training step's weight-gradient stream, then the optimizer after the join).
+    A weight gradient larger than half the scratch runs unsplit (still
+    deterministic, slower).  The PyramidROIAlign backward follows the same mode
+    (m3d.ops)."""
+    global _DET
+    load()
     if not on:
-        check(lib.m3d_set_deterministic(0, None, 0), "set_deterministic")
-        _DET_SCRATCH = None
+        _DET = None
         return
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     buf = torch.empty(max(int(scratch_bytes), 4096) // 4, dtype=torch.float32, device=dev)
-    check(lib.m3d_set_deterministic(1, buf.data_ptr(), buf.numel() * 4), "set_deterministic")
-    _DET_SCRATCH = buf
+    _DET = (Det(1, buf.data_ptr(), buf.numel() * 4), buf)

@@ -134,13 +134,25 @@ def rpn_row_count(config, image_shape=None):
     return int(sum(-(-H // s) * -(-W // s) * D * apl for s in FEATURE_STRIDES_YX))
 
 
-def model_anchors(config, image_shape=None):
+def model_anchors(config, image_shape=None, inplace=True):
     """The anchors a model built from ``config`` uses: the z-stride patch
     (patch_backbone_strides), then RPN.get_anchors, checked against the RPN
     head's row count.  Raises ValueError when the preset cannot give one anchor
     per RPN row (y/x strides other than 4..64, several scales per level), where
-    the reference would gather past its anchor constant."""
+    the reference would gather past its anchor constant.
+
+    ``inplace``: patch the caller's config, as RPN.train does to its own
+    (core/models.py:3408-3419; m3d.model.RPN).  MaskRCNN (inference,
+    m3d.heads) passes False: the reference never patches there, so a z-stride-2
+    preset leaves its anchors short of the head's rows and its tf.gather fails;
+    here the anchors are built from a patched copy (one anchor per head row)
+    and the caller's config is left as it was (a documented deviation,
+    INTEGRATION.md)."""
+    import copy
     import warnings
+    if not inplace:
+        config = copy.copy(config)
+        config.BACKBONE_STRIDES = list(config.BACKBONE_STRIDES)
     if patch_backbone_strides(config):
         warnings.warn("BACKBONE_STRIDES z-components set to 1 as RPN.train does "
                       "(core/models.py:3408-3419): the network never strides depth", stacklevel=3)

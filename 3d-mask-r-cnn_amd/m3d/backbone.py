@@ -9,16 +9,14 @@ trainable gamma/beta (TRAIN_BN=False), every conv has a bias.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .nn import BNFuse, GradLink, _RPNOut, conv_bn_act, conv_geom, max_pool3d, subsample221
 from .params import BNLayer, ConvLayer
 
 # the RPN head's shared conv transforms its weights once per pass for all
-# pyramid levels (M3D_SHARE_WINO_WEIGHTS=0: once per level, A/B)
-SHARE_WINO_WEIGHTS = os.environ.get("M3D_SHARE_WINO_WEIGHTS", "1") != "0"
+# pyramid levels (False: once per level, A/B; tests/test_gpu_determinism.py)
+SHARE_WINO_WEIGHTS = True
 
 
 class _Unit:
@@ -47,7 +45,7 @@ class _Block:
         self.c = _Unit(store, c + "2c", b + "2c", (1, 1, 1), f2, f3, (1, 1, 1), "valid")
         self.sc = _Unit(store, c + "1", b + "1", (1, 1, 1), cin, f3, strides, "valid") if shortcut else None
 
-    def __call__(self, x, links=None, fuse_in=None, fuse_out=None):
+    def __call__(self, x, links=None, fuse_in=None, fuse_out=None, fuses=None):
         """``fuse_in``: the BNFuse of the unit that made x, when this block is
         x's only consumer (an identity block inside a stage: its 2a data
         gradient, after the GradLink summed 2c's residual gradient, is x's whole
@@ -59,7 +57,7 @@ class _Block:
         train = torch.is_grad_enabled() and x.requires_grad
         # 2a -> 2b -> 2c: each unit's output has one consumer, whose data
         # gradient applies its BN-ReLU backward (nn.BNFuse)
-        fa, fb = (BNFuse(), BNFuse()) if train else (None, None)
+        fa, fb = (BNFuse(fuses), BNFuse(fuses)) if train else (None, None)
         if self.sc is None:
             link = GradLink("res", x, links) if train else None
             y = self.a(x, relu=True, link=link, fuse=fa, fuse_in=fuse_in)
@@ -95,9 +93,11 @@ class ResNet3D:
             self.stages.append(blocks)
         self.stage5 = stage5
         self.links = []
+        self.fuses = []
 
     def __call__(self, image):
         self.links = []                 # GradLinks of this forward (checked by check_links)
+        self.fuses = []                 # BNFuse records of this forward (checked by check_fuses)
         x = self.stem(image, relu=True, need_dx=False)
         c1 = x = max_pool3d(x, (3, 3, 3), (2, 2, 1), "same")
         outs = [c1]
@@ -107,8 +107,8 @@ class ResNet3D:
             # as its only consumer; a stage's last output also feeds the FPN
             fuse = None
             for i, blk in enumerate(blocks):
-                nxt = BNFuse() if train and i + 1 < len(blocks) else None
-                x = blk(x, self.links, fuse_in=fuse, fuse_out=nxt)
+                nxt = BNFuse(self.fuses) if train and i + 1 < len(blocks) else None
+                x = blk(x, self.links, fuse_in=fuse, fuse_out=nxt, fuses=self.fuses)
                 fuse = nxt
             outs.append(x)
         if not self.stage5:
@@ -165,17 +165,20 @@ class RPNHead:
                               kernel_init=("normal", 0.001))
         self.w_grad = None
         self.b_grad = None
-        self.backbone = backbone        # its GradLinks are checked in finish_backward
+        self.backbone = backbone        # its GradLinks / BNFuse records are checked in finish_backward
+        self.fuse_records = []
 
     def __call__(self, feature_maps):
         shared, fuses = [], []
+        self.fuse_records = []
         # rpn_conv_shared1 is one kernel on every level: its Winograd weight
         # transform is done once per pass (forward and data gradient) and reused
         wshare = {} if SHARE_WINO_WEIGHTS else None
         for p in feature_maps:
             g1 = conv_geom(tuple(p.shape[1:4]), (3, 3, 3), (1, 1, 1), "same")
             # shared1 -> shared2 -> the class / bbox heads: sole consumers (nn.BNFuse)
-            f1, f2 = (BNFuse(), BNFuse()) if torch.is_grad_enabled() else (None, None)
+            f1, f2 = (BNFuse(self.fuse_records), BNFuse(self.fuse_records)) if torch.is_grad_enabled() \
+                else (None, None)
             s = conv_bn_act(p, self.shared1, g1, relu=True, wshare=wshare, fuse=f1)
             g2 = conv_geom(tuple(s.shape[1:4]), (1, 1, 1), (1, 1, 1), "valid")
             shared.append(conv_bn_act(s, self.shared2, g2, relu=True, fuse=f2, fuse_in=f1))
@@ -201,10 +204,12 @@ class RPNHead:
     def finish_backward(self):
         """Join the side-stream weight gradients (m3d.nn.join_wgrad) and fold the
         padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
-        from .nn import check_links, join_wgrad
+        from .nn import check_fuses, check_links, join_wgrad
         join_wgrad()
+        check_fuses(self.fuse_records)
         if self.backbone is not None:
             check_links(self.backbone.links)
+            check_fuses(self.backbone.fuses)
         if self.w_grad is None:
             return
         apl, cin = self.apl, 256

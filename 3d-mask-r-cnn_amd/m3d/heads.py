@@ -236,7 +236,7 @@ class MaskRCNN:
     mrcnn_bbox, mrcnn_mask [B,max_inst,2M,2M,2M,C], rpn_rois."""
 
     def __init__(self, config, device="cuda", seed=1):
-        anchors = model_anchors(config)          # z-stride patch + row-count check (m3d.anchors)
+        anchors = model_anchors(config, inplace=False)  # patched copy + row-count check (m3d.anchors)
         _lib.load()
         self.config = c = config
         self.device = torch.device(device)

@@ -72,15 +72,17 @@ class ProposalLayer:
             db = deltas[0].detach().float().contiguous()
             keys = ops.score_keys(pb, local_index)
             kl = min(k, keys.shape[0])
-            vals, pos = torch.topk(keys, kl, sorted=False)
-            ck = torch.full((k,), torch.iinfo(torch.int64).min, device=pb.device, dtype=torch.int64)
+            vals, pos = ops.topk_keys(keys, kl, positions=True)
+            # padding keys below every score key and distinct (m3d_topk_keys wants distinct keys);
+            # never selected: the slabs hold at least k real candidates together (sum A_local = A >= k)
+            ck = torch.iinfo(torch.int64).min + torch.arange(k, device=pb.device, dtype=torch.int64)
             cp = torch.zeros((k, 2), device=pb.device)
             cd = torch.zeros((k, 6), device=pb.device)
             ck[:kl], cp[:kl], cd[:kl] = vals, pb[pos], db[pos]
             gk = sg.all_gather(ck).reshape(-1)
             gp = sg.all_gather(cp).reshape(-1, 2)
             gd = sg.all_gather(cd).reshape(-1, 6)
-            top, where = torch.topk(gk, k, sorted=True)
+            top, where = ops.topk_keys(gk, k, positions=True)
             gidx = 0xFFFFFFFF - (top & 0xFFFFFFFF)
             sel_p = gp.index_select(0, where).contiguous()
             sel_d = gd.index_select(0, where).contiguous()

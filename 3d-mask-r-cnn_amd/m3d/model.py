@@ -16,7 +16,6 @@ NMS work is libm3d.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -171,7 +170,6 @@ def rpn_bbox_loss(t: RPNTargets, rpn_bbox):
     return (h_xy + h_z).sum() / (6 * t.pos_denom)
 
 
-FUSED_RPN_LOSS = os.environ.get("M3D_FUSED_RPN_LOSS", "1") != "0"   # 0: the framework-op form (A/B)
 
 
 class _RPNLossFused(torch.autograd.Function):
@@ -226,7 +224,7 @@ def rpn_losses(t, rpn_class_logits, rpn_bbox, w_cls=1.0, w_box=1.0, alpha=0.90, 
     """(total, rpn_class_loss, rpn_bbox_loss): core/models.py:1589-1673 weighted
     as 3366-3376.  On the GPU through the fused libm3d kernel; host tensors
     (the CPU depth-slab tests) take the framework-op form below."""
-    if rpn_class_logits.is_cuda and FUSED_RPN_LOSS:
+    if rpn_class_logits.is_cuda:
         if isinstance(t, DeviceRPNTargets):
             pos = (t.match == 1).to(torch.int32)
             match8, row32 = t.match.to(torch.int8), torch.cumsum(pos, 0, dtype=torch.int32) - 1

@@ -52,8 +52,8 @@ GRAD_HOOK = None
 # The side stream waits for the compute stream before each weight gradient
 # (dz ready), and join_wgrad() -- called by RPNHead.finish_backward, i.e.
 # before anything reads the gradients -- makes the compute stream wait for it.
-# M3D_WGRAD_STREAM=0 runs them in line.
-WGRAD_STREAM = os.environ.get("M3D_WGRAD_STREAM", "1") != "0"
+# False runs them in line (bench.py --wgrad-inline: serialized kernel traces).
+WGRAD_STREAM = True
 _SIDE = {}
 _SIDE_USED = set()
 
@@ -68,8 +68,8 @@ _SIDE_USED = set()
 # allocator frees and re-allocates segments inside the step.  When more than
 # this fraction of the device is reserved, the host waits for the side stream
 # every WGRAD_THROTTLE_EVERY weight gradients (0: off).
-WGRAD_THROTTLE = float(os.environ.get("M3D_WGRAD_THROTTLE", "0.5"))
-WGRAD_THROTTLE_EVERY = int(os.environ.get("M3D_WGRAD_THROTTLE_EVERY", "4"))
+WGRAD_THROTTLE = 0.5
+WGRAD_THROTTLE_EVERY = 4
 _THROTTLE = {}
 
 
@@ -98,7 +98,31 @@ def _throttle(key, side):
 # Stream.wait_stream.  The fork showed as a ~7.5 us compute-queue bubble per
 # layer in the 128^3 kernel trace; A/B (scripts/gpu_r03x.sh, same box): mode 2
 # 29.80 / 29.90 ms per step, torch / 0 / 1 30.05-30.10 ms.
-FORK_EVENT = os.environ.get("M3D_FORK_EVENT", "2")
+FORK_EVENT = "2"
+
+
+_EV_RING = 64
+_FORK_EVENTS = {}       # (device, mode) -> [events, next]: the caller-owned events of m3d_stream_fork
+
+
+def fork_event(dev_index, mode):
+    """Next event of the (device, mode) ring (m3d_fork_event_create): an event
+    is recorded again only after 63 later forks were enqueued, long after the
+    wait that used it."""
+    key = (dev_index, mode)
+    ring = _FORK_EVENTS.get(key)
+    if ring is None:
+        L = _lib.load()
+        evs = []
+        with torch.cuda.device(dev_index):
+            for _ in range(_EV_RING):
+                ev = ctypes.c_void_p()
+                check(L.m3d_fork_event_create(mode, ctypes.byref(ev)), "fork_event_create")
+                evs.append(ev.value)
+        ring = _FORK_EVENTS[key] = [evs, 0]
+    ev = ring[0][ring[1]]
+    ring[1] = (ring[1] + 1) % _EV_RING
+    return ev
 
 
 def _fork(src, dst):
@@ -106,7 +130,9 @@ def _fork(src, dst):
     if FORK_EVENT == "torch":
         dst.wait_stream(src)
         return
-    check(_lib.load().m3d_stream_fork(src.cuda_stream, dst.cuda_stream, int(FORK_EVENT)), "stream_fork")
+    ev = fork_event(src.device.index if src.device.index is not None else torch.cuda.current_device(),
+                    int(FORK_EVENT))
+    check(_lib.load().m3d_stream_fork(src.cuda_stream, dst.cuda_stream, ev), "stream_fork")
 
 
 def _wgrad_stream(dev):
@@ -192,35 +218,35 @@ def _L():
 # depth-slab sharding: the Winograd convs read the neighbours' halo planes beside
 # the slab (m3d_conv3d_*_wino_halo); M3D_SLAB_HALO_PLANES=0 builds the
 # halo-extended copy of every z-window input instead (torch.cat, the old path)
-SLAB_HALO_PLANES = os.environ.get("M3D_SLAB_HALO_PLANES", "1") != "0"
+SLAB_HALO_PLANES = True
 
 # ... and post the exchange before the Winograd conv's first launch phase
 # (m3d_conv3d_fwd_wino_halo_phase 1: weights + interior z tiles), waiting only
-# before phase 2 (M3D_SLAB_OVERLAP=0: exchange, then the one-launch conv)
-SLAB_OVERLAP = os.environ.get("M3D_SLAB_OVERLAP", "1") != "0"
+# before phase 2 (False: exchange, then the one-launch conv)
+SLAB_OVERLAP = True
 
-# big-K 1x1x1 stride-1 convs on the bf16-split GEMM (M3D_CONV1_X3=0: the f32 direct kernel)
-CONV1_X3 = os.environ.get("M3D_CONV1_X3", "1") != "0"
-# split-K 1x1x1 convs where the output tiles do not fill the chip (M3D_SPLITK=0: one pass)
-SPLITK = os.environ.get("M3D_SPLITK", "1") != "0"
+# big-K 1x1x1 stride-1 convs on the bf16-split GEMM (False: the f32 direct kernel)
+CONV1_X3 = True
+# split-K 1x1x1 convs where the output tiles do not fill the chip (False: one pass)
+SPLITK = True
 # largest transformed input U a Winograd conv keeps from its forward for its
 # weight gradient (per layer; at 256^3 the P2 layers' U is 6.4 GB each).  With
 # the side-stream throttle below holding the allocator's reservations down,
 # keeping them is 4 ms faster per 256^3 step (177.6 vs 181.8 ms, 141 vs 133 GB
 # peak, r03r); above the cap the weight gradient re-transforms x
-WINO_KEEP_MAX_BYTES = int(float(os.environ.get("M3D_WINO_KEEP_MAX_GB", "8")) * 2**30)
+WINO_KEEP_MAX_BYTES = 8 * 2**30
 # largest Winograd workspace a shared kernel keeps across its calls
-SHARE_WINO_MAX_BYTES = int(float(os.environ.get("M3D_SHARE_WINO_MAX_GB", "6")) * 2**30)
+SHARE_WINO_MAX_BYTES = 6 * 2**30
 
-# Winograd F(2^3,3^3) for stride-1 'same' 3x3x3 convs (M3D_WINOGRAD=0 disables)
-WINOGRAD = os.environ.get("M3D_WINOGRAD", "1") != "0"
-WINO_MIN_C = int(os.environ.get("M3D_WINO_MIN_C", "64"))
+# Winograd F(4x2x4, 3^3) for stride-1 'same' 3x3x3 convs (False disables)
+WINOGRAD = True
+WINO_MIN_C = 64
 # below this channel count the weight gradient runs as a direct implicit GEMM.
 # Round 2 kept the 64-channel res2*_branch2b on the direct kernel (its own
 # F(2x2x2) input transform cost more than it saved: 0.35 vs 0.33 ms); with the
 # weight gradient on the forward's kept F(2x2x4) U there is no input transform
 # left to pay, and 64 is faster: step 29.8 -> 29.5 ms (same-box A/B, r03n)
-WINO_WGRAD_MIN_C = int(os.environ.get("M3D_WINO_WGRAD_MIN_C", "64"))
+WINO_WGRAD_MIN_C = 64
 
 
 def use_winograd(geo, cin, cout, in_sp):
@@ -429,8 +455,8 @@ def _link_park(link, dx, acc):
 # in its epilogue (dz and dres stored, the beta / gamma / bias sums reduced from
 # per-tile partials), so the unit's own backward skips bn_act_bwd -- one
 # read-modify-write pass over the activation gradient less per fused unit.
-# M3D_BN_FUSE=0 runs bn_act_bwd everywhere (A/B).
-BN_FUSE = os.environ.get("M3D_BN_FUSE", "1") != "0"
+# BN_FUSE = False runs bn_act_bwd everywhere (A/B; tests/test_gpu_bnfuse.py).
+BN_FUSE = True
 
 
 class BNFuse:
@@ -443,14 +469,24 @@ class BNFuse:
     arms it in forward; the consumer fuses when its data-gradient kernel has the
     fused form and its result is final, and marks it ``done``; the producer's
     backward then takes the incoming gradient as its dz (checked to be the
-    consumer's buffer: any other contribution raises instead of being lost)."""
+    consumer's buffer: any other contribution raises instead of being lost).
+
+    While ``done`` is set, the consumer has already written the unit's dz (not
+    dL/dy) into the gradient it returns, and added the unit's beta / gamma /
+    bias sums: a hook on the unit's output, or autograd.grad stopping at it,
+    sees dz.  ``registry`` (a list owned by the model's forward) collects the
+    records; check_fuses() after the backward raises if one was applied by its
+    consumer but never consumed by its producer's backward (a partial backward),
+    as check_links() does for a parked GradLink."""
     __slots__ = ("armed", "done", "y", "z", "bn", "relu", "need_res", "grads", "buf", "dres", "name")
 
-    def __init__(self):
+    def __init__(self, registry=None):
         self.armed = self.done = False
         self.y = self.z = self.bn = self.grads = self.buf = self.dres = None
         self.relu = self.need_res = False
         self.name = ""
+        if registry is not None:
+            registry.append(self)
 
     def arm(self, y, z, bn, relu, need_res, grads, name):
         self.armed, self.done = True, False
@@ -478,6 +514,16 @@ class BNFuse:
                        ptr(dres), ptr(g.get("beta")), ptr(g.get("gamma") if z is not None else None),
                        ptr(g.get("bias")))
         return d
+
+
+def check_fuses(records):
+    """Raise if a BNFuse record was applied by its consumer's data gradient but
+    its producer's backward never took it (see BNFuse)."""
+    bad = [r.name for r in records if r.done]
+    if bad:
+        raise RuntimeError(f"fused BN-ReLU backward of {bad[:4]} was applied by the consumer's data gradient, "
+                           "but the producing unit's backward never ran in this pass (its BN sums are already "
+                           "accumulated and its output gradient holds dz, not dL/dy)")
 
 
 def _per_item(B, vin, cin, vout, cout):
@@ -630,9 +676,11 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.res_shape = None if residual is None else tuple(residual.shape)
         # this unit's BN-ReLU backward handed to its consumer (BNFuse)
         ctx.fuse = None
+        # (res_mode 2, the FPN's upsampled residual, has no fused form: its residual
+        # gradient needs the upsample adjoint, so such a unit is never armed)
         if (fuse is not None and BN_FUSE and grads is not None and (bn is not None or relu)
-                and Cout % 4 == 0):
-            fuse.arm(y, z, ctx.bn, relu, res_mode == 1, grads, name)
+                and Cout % 4 == 0 and res_mode in (0, 1)):
+            fuse.arm(y, z, ctx.bn, relu, res_mode != 0, grads, name)
             ctx.fuse = fuse
         # ... and the producer's, applied in this unit's data gradient
         ctx.fuse_in = None
@@ -1045,9 +1093,8 @@ def subsample221(x):
     return _Subsample221.apply(x.contiguous())
 
 
-# M3D_RPN_OUT_SIDE=0 keeps the RPN class/bbox heads' weight gradient on the
-# compute stream (A/B)
-RPN_OUT_SIDE = os.environ.get("M3D_RPN_OUT_SIDE", "1") != "0"
+# False keeps the RPN class/bbox heads' weight gradient on the compute stream (A/B)
+RPN_OUT_SIDE = True
 
 
 class _RPNOut(torch.autograd.Function):

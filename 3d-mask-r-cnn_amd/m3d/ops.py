@@ -242,7 +242,7 @@ class _PyramidROIAlign(torch.autograd.Function):
         ph, pw, pd = ctx.pool
         gptrs = (_lib.c_p * 4)(*[g.data_ptr() for g in gmaps])
         fshape = ((_lib.c_i64 * 3) * 4)(*[(_lib.c_i64 * 3)(*s[1:4]) for s in ctx.shapes])
-        if _L().m3d_get_deterministic() and max(ph, pw, pd) <= 64:
+        if _lib.deterministic() and max(ph, pw, pd) <= 64:
             # bitwise reproducible: per level, the destination-owned sums in the reference's order
             bi = torch.empty(4 * B * N, device=grad.device, dtype=torch.int32)
             check(_L().m3d_pyramid_roi_align3d_bwd_det(ptr(grad), ptr(boxes_adj), ptr(levels), B, N, ph, pw,
@@ -278,13 +278,27 @@ def pyramid_roi_align(boxes, image_meta, feature_maps, pool_shape, return_levels
 # ---------------------------------------------------------------------------
 # ProposalLayer device pipeline (core/models.py:382-500), one image.
 # ---------------------------------------------------------------------------
+def topk_keys(keys, k, positions=False):
+    """tf.nn.top_k(keys, k, sorted=True) on distinct int64 keys (m3d_topk_keys,
+    the hand-written radix select + rank sort; core/models.py:403-404):
+    values [k] descending, and with ``positions`` their indices in ``keys``."""
+    keys = _c(keys, torch.int64)
+    n = keys.shape[0]
+    vals = torch.empty(k, device=keys.device, dtype=torch.int64)
+    pos = torch.empty(k, device=keys.device, dtype=torch.int64) if positions else None
+    nb = int(_L().m3d_topk_workspace_bytes(n, k))
+    ws = torch.empty(nb // 8 + 1, device=keys.device, dtype=torch.int64)
+    check(_L().m3d_topk_keys(ptr(keys), n, k, ptr(vals), ptr(pos), ptr(ws), nb, stream()), "topk_keys")
+    return (vals, pos) if positions else vals
+
+
 def topk_order(probs, k):
     """tf.nn.top_k(probs[:,1], k, sorted=True).indices with TF's tie order
     (lower index first) via unique int64 keys built on the GPU."""
     A = probs.shape[0]
     keys = torch.empty(A, device=probs.device, dtype=torch.int64)
     check(_L().m3d_score_keys(ptr(probs), A, ptr(keys), stream()), "score_keys")
-    vals = torch.topk(keys, k, sorted=True).values
+    vals = topk_keys(keys, k)
     return (0xFFFFFFFF - (vals & 0xFFFFFFFF)).to(torch.int64)
 
 

@@ -46,13 +46,26 @@ def init_from_env(backend=None, timeout_s=None):
 # ---------------------------------------------------------------------------
 # self-validation of a multi-rank run (bench.py N > 1)
 # ---------------------------------------------------------------------------
+_INT_OF_WIDTH = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+
+
 def tensor_digest(t: torch.Tensor) -> torch.Tensor:
-    """Bit-level digest of a tensor: int64 [3] = (element count, sum of its
-    32-bit words, sum of word * (i mod 65521 + 1)) -- equal digests for
-    bit-identical tensors; any single changed word changes both sums."""
+    """Bit-level digest of a tensor: int64 [3] = (element count, sum of its raw
+    words, sum of word * (i mod 65521 + 1)), the words being the elements' bytes
+    read as an integer of the element's width (bf16 / fp16 as int16, fp64 as
+    int64: no value conversion, so tensors that differ in any bit differ in
+    their words) -- equal digests for bit-identical tensors; any single changed
+    word changes both sums (int64 sums wrap, identically on every rank)."""
     w = t.detach().contiguous().reshape(-1)
-    if w.element_size() == 4:
-        w = w.view(torch.int32)
+    if w.dtype == torch.bool:
+        w = w.view(torch.uint8)
+    if w.is_floating_point() or w.is_complex():
+        if w.is_complex():
+            w = torch.view_as_real(w).reshape(-1)
+        it = _INT_OF_WIDTH.get(w.element_size())
+        if it is None:
+            raise TypeError(f"tensor_digest: no integer type of width {w.element_size()} for {t.dtype}")
+        w = w.view(it)
     w = w.to(torch.int64)
     idx = (torch.arange(w.numel(), device=w.device, dtype=torch.int64) % 65521) + 1
     return torch.stack([torch.tensor(w.numel(), device=w.device, dtype=torch.int64), w.sum(), (w * idx).sum()])
@@ -60,11 +73,14 @@ def tensor_digest(t: torch.Tensor) -> torch.Tensor:
 
 def ranks_identical(tensors: dict, group=None) -> dict:
     """For each named tensor: is it bit-identical on every rank of ``group``?
-    One all_gather of the digests (works on gloo and RCCL)."""
+    One all_gather of the digests; under gloo (which gathers host tensors only)
+    the digests are moved to the host first."""
     names = sorted(tensors)
     if not names:
         return {}
     d = torch.stack([tensor_digest(tensors[n]) for n in names])
+    if dist.get_backend(group) == "gloo":
+        d = d.cpu()
     world = dist.get_world_size(group)
     out = [torch.empty_like(d) for _ in range(world)]
     dist.all_gather(out, d, group=group)

@@ -35,6 +35,10 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICRO
 # fp32-FLOP ceiling is a sixth of it
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 X3_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
+# the step's largest kernel by time in the rocprof table of this tree
+# (profiles/dominant_kernel_table.txt, line 1): the headline `roofline` prices
+# its largest launch
+DOMINANT_KERNEL = "x3_wgrad_tr_kernel"
 
 
 class LegWatchdog:
@@ -98,11 +102,12 @@ def _pmc_traffic(kernel_key):
 
 
 def wgrad_gemm_shape(S):
-    """The largest launch of the step's second kernel, x3_wgrad_tr_kernel: the
+    """The largest launch of the step's dominant kernel, x3_wgrad_tr_kernel: the
     (NY+2)*4*(NZ+2) batched Winograd weight-gradient GEMMs of rpn_conv_shared1
-    (3x3x3, 256->512) on P2 [S/4, S/4, S] -- F(2x2x4) tiles by default (96
-    GEMMs on the forward's kept U; M3D_WINO_WGRAD_NZ=2: F(2x2x2), 64 GEMMs),
-    reduction over M = T tiles, K = 256, N = 512."""
+    (3x3x3, 256->512) on P2 [S/4, S/4, S] -- the (NY+2)*4*(NZ+2) point GEMMs of
+    the weight gradient's tile (m3d_conv3d_wino_wgrad_tile_z / _tile_y; 144 for
+    F(4x2x4)) on the forward's kept U, reduction over M = T tiles, K = 256,
+    N = 512."""
     from m3d import _lib
     nz = int(_lib.load().m3d_conv3d_wino_wgrad_tile_z())
     ny = int(_lib.load().m3d_conv3d_wino_tile_y())
@@ -112,8 +117,8 @@ def wgrad_gemm_shape(S):
 
 
 def wino_gemm_shape(S):
-    """The largest launch of the step's dominant kernel, x3_gemm256_af_kernel
-    (17.7 % of the step's kernel time, profiles/r02i_bench_kernels_128.txt): the
+    """The largest launch of x3_gemm256_af_kernel (the step's second kernel by
+    time since round 4, profiles/dominant_kernel_table.txt): the
     (NY+2)*4*(NZ+2) batched Winograd point GEMMs of rpn_conv_shared1 (3x3x3,
     256->512) on P2 [S/4, S/4, S]: M = T = 2x2xNZ output tiles, K = 256,
     N = 512 (NZ = 4 by default: 96 GEMMs)."""
@@ -179,6 +184,8 @@ def time_wgrad_gemm(S, reps=5):
     return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": X3_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / X3_PEAK_TFLOPS, 4),
             "traffic": _pmc_traffic(f"wino_wgrad_gemm_rpn_shared1_S{S}"),
+            "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes "
+                            "(scripts/gpu_prof.sh -> profiles/traffic.json)",
             "kernel": f"x3_wgrad_tr_kernel (fp32 GEMM as 6 bf16 MFMAs per product, 256x256 tiles, operands "
                       f"split in the LDS store): {nb} batched Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2, "
                       f"C[K][N] += A[M][K]^T B[M][N], M={T} K={K} N={N}",
@@ -499,6 +506,8 @@ def depth_slab_leg(S, steps, warmup, rank, world, dev, proposals=True):
     from m3d.config import synthetic_rpn_config
     from m3d.model import RPN, synthetic_rpn_targets, synthetic_volume
     from m3d.parallel import SlabRPN
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)      # peak_mem_gb is this leg's own
     cfg = synthetic_rpn_config(S)
     model = RPN(cfg, device=dev, seed=1)
     sg = slab.SlabGroup(S, rank, world)
@@ -764,15 +773,118 @@ def roi_leg_large(S, dev, n_rois=512):
     return r
 
 
+def inference_roofline(model, image, meta, reps=3):
+    """Per-stage roofline of MaskRCNN.detect (BASELINE configs[3],
+    core/models.py:5473-5754): every stage of the inference pass timed alone
+    with HIP events (the host enqueued ahead), and priced at
+    max(executed MFMA FLOPs / the ceiling of the kernel that ran them,
+    compulsory HBM bytes / HBM peak):
+      backbone / fpn / rpn_head / mask_head convs: m3d.nn.LAYER_LOG (Winograd
+        layers at their point-GEMM FLOPs), plus the mask head's dilated conv3b,
+        transposed conv and sigmoid conv counted here;
+      roi_align7 / roi_align14: output + 4*C*|unique voxels| (HBM);
+      classifier: mrcnn_class_conv1 (a pool^3 x C GEMM, f32 MFMA), conv2 and the
+        dense heads, weights + activations (whichever bound);
+      proposal_layer (top-k + 3-D NMS) and detection (2-D NMS): latency-bound by
+        definition (the serial greedy reduction), reported without a roof.
+    frac = sum of the roofs / sum of the measured stage times."""
+    from m3d import nn as mnn
+    P = HBM_PEAK_GBS * 1e9
+    stages = {}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        _host_ahead(0.2)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            r = fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return r, e0.elapsed_time(e1) / reps / 1e3
+
+    def logged(name, fn, extra_flop=0.0, extra_bytes=0.0, engine="f32"):
+        mnn.LAYER_LOG = []
+        try:
+            r = fn()
+            torch.cuda.synchronize()
+            rec = mnn.LAYER_LOG
+        finally:
+            mnn.LAYER_LOG = None
+        r, t = timed(fn)
+        roof = sum(_roof_s(x) for x in rec) + max(extra_flop / _peak_flops(engine), extra_bytes / P)
+        stages[name] = {"ms": round(t * 1e3, 3), "roofline_ms": round(roof * 1e3, 3),
+                        "frac_roofline": round(roof / t, 4), "layers": len(rec)}
+        return r
+
+    def priced(name, fn, flop, nbytes, engine="f32"):
+        r, t = timed(fn)
+        roof = max(flop / _peak_flops(engine), nbytes / P)
+        stages[name] = {"ms": round(t * 1e3, 3), "roofline_ms": round(roof * 1e3, 3),
+                        "frac_roofline": round(roof / t, 4), "bound": "mfma" if flop / _peak_flops(engine) >=
+                        nbytes / P else "hbm", "tflop": round(flop / 1e12, 4), "gb": round(nbytes / 1e9, 4)}
+        return r
+
+    def latency(name, fn):
+        r, t = timed(fn)
+        stages[name] = {"ms": round(t * 1e3, 3), "roofline_ms": None, "bound": "latency"}
+        return r
+
+    with torch.no_grad():
+        _, C2, C3, C4, C5 = logged("backbone", lambda: model.backbone(image))
+        fmaps = logged("fpn", lambda: model.fpn(C2, C3, C4, C5))
+        _, rpn_probs, rpn_bbox = logged("rpn_head", lambda: model.rpn(fmaps))
+        rois = latency("proposal_layer", lambda: model.proposal_layer([rpn_probs, rpn_bbox, model.anchors]))
+        maps4 = fmaps[:4]
+        fshapes = [tuple(f.shape[1:4]) for f in maps4]
+        C = int(maps4[0].shape[-1])
+        S = int(image.shape[1])
+        cfg = model.config
+
+        def roi_bytes(boxes, pool):
+            n = int(boxes.shape[1])
+            u = unique_voxels(boxes[:1].detach().float().cpu().numpy(), fshapes, (pool,) * 3, S)
+            return 4.0 * (n * pool ** 3 * C + C * u)
+        p7 = int(cfg.POOL_SIZE)
+        pooled = priced("roi_align7", lambda: model.roi_align_classifier([rois, meta] + maps4), 0.0,
+                        roi_bytes(rois, p7))
+        M = int(pooled.shape[0] * pooled.shape[1])
+        K, fc, ncls = p7 ** 3 * C, model.classifier.fc, model.classifier.C
+        f_cls = 2.0 * M * (K * fc + fc * fc + fc * 7 * ncls)
+        b_cls = 4.0 * (M * K + K * fc + fc * fc + fc * 7 * ncls + 2 * M * fc + M * 8 * ncls)
+        _, mclass, mbbox = priced("classifier", lambda: model.classifier(pooled), f_cls, b_cls)
+        det = latency("detection", lambda: model.detection([rois, mclass, mbbox, meta]))
+        dboxes = det[..., :6].contiguous()
+        p14 = int(cfg.MASK_POOL_SIZE)
+        mpooled = priced("roi_align14", lambda: model.roi_align_mask([dboxes, meta] + maps4), 0.0,
+                         roi_bytes(dboxes, p14))
+        Mm = int(mpooled.shape[0] * mpooled.shape[1])
+        ch = model.mask_head.ch
+        v = Mm * p14 ** 3
+        f_extra = 2.0 * v * 27 * ch * ch + 2.0 * v * 8 * ch * ch + 2.0 * 8 * v * ch * ncls
+        b_extra = 4.0 * (3 * v * ch + 27 * ch * ch + v * ch + 8 * ch * ch + 8 * v * ch + 8 * v * ch + 8 * v * ncls)
+        logged("mask_head", lambda: model.mask_head(mpooled), f_extra, b_extra)
+    tot = sum(v["ms"] for v in stages.values())
+    roof = sum(v["roofline_ms"] or 0.0 for v in stages.values())
+    return {"stages": stages, "ms": round(tot, 3), "roofline_ms": round(roof, 3), "frac": round(roof / tot, 4),
+            "note": "sum over stages timed alone of max(MFMA FLOPs / ceiling, compulsory bytes / HBM peak) / "
+                    "sum of stage times; NMS stages are latency-bound and carry no roof (lower bound)"}
+
+
 def mrcnn_inference_leg(S, steps, warmup, dev):
     """BASELINE configs[3]: full Mask R-CNN inference on one S^3 volume --
     backbone + FPN + RPN forward, ProposalLayer (3-D NMS, 512 proposals),
     PyramidROIAlign 7^3 -> classifier head -> DetectionLayer (2-D NMS) ->
     PyramidROIAlign 14^3 -> mask head.  Random-init weights: the detection
-    count is whatever the synthetic volume yields (reported)."""
+    count is whatever the synthetic volume yields (reported).  `roofline`:
+    inference_roofline (per stage); its rocprof kernel table is
+    profiles/r05*_infer_kernels*.txt (scripts/infer_prof.py)."""
     from m3d.config import synthetic_mrcnn_config
     from m3d.heads import MaskRCNN
     from m3d.model import compose_image_meta, synthetic_volume
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)      # peak_mem_gb is this leg's own
     cfg = synthetic_mrcnn_config(S)
     model = MaskRCNN(cfg, device=dev, seed=1)
     image = synthetic_volume(S, seed=100).to(dev)
@@ -792,12 +904,16 @@ def mrcnn_inference_leg(S, steps, warmup, dev):
            "size": S, "ms_per_volume": round(el / steps * 1e3, 2), "volumes_per_s": round(steps / el, 4),
            "detections": n_det, "max_instances": int(cfg.DETECTION_MAX_INSTANCES),
            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
-    del model, out
+    del out
+    try:
+        res["roofline"] = inference_roofline(model, image, meta)
+    except Exception as e:  # report, never hide
+        res["roofline"] = {"error": repr(e)}
+    del model
     torch.cuda.empty_cache()
     return res
 
 
-# ---------------------------------------------------------------- CPU baseline
 def _host_cpus():
     """The box's CPUs beside the thread count the baseline used: os.cpu_count()
     (the whole machine), the CPUs this process may run on (its affinity / the
@@ -1001,7 +1117,12 @@ def main():
     ap.add_argument("--infer-size", type=int, default=256, help="MaskRCNN inference leg size (0: off)")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
     ap.add_argument("--graph", action="store_true", help="HIP-graph capture of the N=1 step")
+    ap.add_argument("--wgrad-inline", action="store_true",
+                    help="weight gradients on the compute stream (serialized kernel traces)")
     args = ap.parse_args()
+    if args.wgrad_inline:
+        from m3d import nn as mnn
+        mnn.WGRAD_STREAM = False
 
     from m3d.config import synthetic_rpn_config
     from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
@@ -1118,12 +1239,17 @@ def main():
         with torch.no_grad():
             fmaps = model.features(image)
         try:
-            # dominant kernel of the step: x3_gemm256_af_kernel (17.7 % of the step's
-            # kernel time: the Winograd point GEMMs plus the big-K 1x1x1 convs,
-            # profiles/r02i_bench_kernels_128.txt), then x3_wgrad_tr_kernel (15.7 %)
+            # the headline roofline prices the step's dominant kernel, DOMINANT_KERNEL
+            # (line 1 of the committed rocprof table of the same tree,
+            # profiles/dominant_kernel_table.txt; tests/test_bench_contract.py checks
+            # the two agree); the other point-GEMM kernel is a sub-leg
             log(f"[bench] leg roofline ({time.strftime('%H:%M:%S')})")
-            out["roofline"] = time_wino_gemm(S)
-            out["roofline"]["wgrad_gemm"] = time_wgrad_gemm(S)
+            legs = {"x3_wgrad_tr_kernel": lambda: time_wgrad_gemm(S), "x3_gemm256_af_kernel": lambda: time_wino_gemm(S)}
+            out["roofline"] = legs[DOMINANT_KERNEL]()
+            for k, f in legs.items():
+                if k != DOMINANT_KERNEL:
+                    out["roofline"]["wino_gemm" if k == "x3_gemm256_af_kernel" else "wgrad_gemm"] = f()
+            out["roofline"]["dominant_kernel_table"] = "profiles/dominant_kernel_table.txt"
             out["roofline"]["direct_conv"] = time_direct_conv(model, fmaps)
             out["roofline"]["wino_fwd_conv"] = time_wino_fwd(S)
         except Exception as e:  # report, never hide
@@ -1217,6 +1343,7 @@ def summary(out):
             "dominant_kernel_frac": g("roofline", "frac"),
             "roi14_256_frac_hbm": g("roi_align_256", "pool14", "frac_hbm"),
             "mrcnn_inference_256_ms": g("mrcnn_inference", "ms_per_volume"),
+            "mrcnn_inference_256_roofline_frac": g("mrcnn_inference", "roofline", "frac"),
             "validation_ok": all(v.get("ok", True) for v in out.get("validation", {}).values()
                                  if isinstance(v, dict))}
 

@@ -14,8 +14,10 @@
  *   - return 0 (M3D_OK) on success, M3D_EINVAL for an argument the reference
  *     op would reject (m3d_last_error() then holds the reference's
  *     InvalidArgument text), M3D_EHIP for a HIP launch error.
- *   - no global mutable state apart from the thread-local error string and
- *     the process-wide deterministic-mode switch (m3d_set_deterministic).
+ *   - reentrant: no global mutable state apart from the thread-local error
+ *     string.  The deterministic-reduction target is an argument of the calls
+ *     that use it (m3d_det_t), the fork events of m3d_stream_fork are the
+ *     caller's (m3d_fork_event_create).
  */
 #ifndef M3D_H
 #define M3D_H
@@ -36,25 +38,39 @@ typedef struct ihipStream_t* m3d_stream_t; /* == hipStream_t */
 const char* m3d_last_error(void);
 int m3d_abi_version(void);
 
-/* Deterministic mode (process-wide; the analogue of TF_DETERMINISTIC_OPS for
- * the reference's training graph, core/models.py:3340-3387).  on = 1: every
- * weight-gradient GEMM (m3d_conv3d_bwd_weight*, m3d_gemm_wgrad_f32) stores its
- * m-split partial tiles into `scratch` and adds them to dW in split order
- * instead of fp32 atomics, and the optimizers' clip norms are summed in chunk
- * order; results are then bitwise identical run to run.  `scratch` (device,
- * 16-B aligned, >= 4096 bytes) is shared by those reductions: launch them on
- * one stream at a time.  A gradient whose two splits do not fit runs unsplit.
- * The ROIAlign backward keeps its atomics (use crop_and_resize3d_bwd_image's
- * deterministic flag).  on = 0 restores the atomic reductions. */
-int m3d_set_deterministic(int32_t on, void* scratch, size_t bytes);
-int32_t m3d_get_deterministic(void);
+/* Deterministic reductions (the analogue of TF_DETERMINISTIC_OPS for the
+ * reference's training graph, core/models.py:3340-3387), chosen per call: the
+ * weight-gradient entry points (m3d_conv3d_bwd_weight*, m3d_gemm_wgrad_f32)
+ * and the optimizers (m3d_sgd_keras, m3d_adam_keras, m3d_adadelta_keras) take
+ * a `const m3d_det_t* det`.  det == NULL or det->on == 0: m-split partial
+ * tiles and clip norms are added with fp32 atomics (fast; the last bits vary
+ * with arrival order).  det->on == 1: every weight-gradient GEMM stores its
+ * m-split partial tiles into det->scratch and adds them to dW in split order,
+ * and the clip norms are summed in chunk order; results are then bitwise
+ * identical run to run.  det->scratch (device, 16-B aligned, >= 4096 bytes)
+ * is used by that call's kernels only until the call's last kernel on `s`
+ * finishes: calls sharing one scratch must be ordered (one stream, or
+ * joined); concurrent calls need scratches of their own.  A gradient whose two
+ * splits do not fit runs unsplit.  A bad det (on, but NULL / short /
+ * misaligned scratch) is M3D_EINVAL.  (ABI 3; replaces the process-wide
+ * m3d_set_deterministic of ABI 2.)  The ROIAlign backward keeps its own flag
+ * (crop_and_resize3d_bwd_image's `deterministic`, m3d_pyramid_roi_align3d_bwd_det). */
+typedef struct m3d_det {
+    int32_t on;
+    void* scratch;
+    size_t bytes;
+} m3d_det_t;
 
 /* Stream fork / join of the training step (weight gradients on a side stream):
- * `to` waits for everything enqueued on `from` so far, through a pooled event
- * (hipEventDisableTiming; mode 1: + hipEventReleaseToDevice, mode 2: +
- * hipEventDisableSystemFence, mode 0: neither).  Both streams must be on the
- * same device: the event's release need not reach the host. */
-int m3d_stream_fork(m3d_stream_t from, m3d_stream_t to, int32_t mode);
+ * `to` waits for everything enqueued on `from` so far, through the caller's
+ * event `ev` (m3d_fork_event_create: hipEventDisableTiming; mode 1: +
+ * hipEventReleaseToDevice, mode 2: + hipEventDisableSystemFence, mode 0:
+ * neither), recorded on `from`.  Both streams must be on the same device: the
+ * event's release need not reach the host.  An event may be re-recorded once
+ * the wait that used it is enqueued (a ring of events per device suffices). */
+int m3d_fork_event_create(int32_t mode, void** ev);
+int m3d_fork_event_destroy(void* ev);
+int m3d_stream_fork(m3d_stream_t from, m3d_stream_t to, void* ev);
 
 /* ---------------------------------------------------------------------------
  * CropAndResize3D family.  Replaces the TF custom ops of the vendored wheel
@@ -178,6 +194,17 @@ int m3d_nms3d(const float* boxes, const float* scores, int64_t N, int32_t max_ou
  *   zero rows after (core/models.py:476-485).
  * ------------------------------------------------------------------------- */
 int m3d_score_keys(const float* probs /*[A,2]*/, int64_t A, int64_t* keys, m3d_stream_t s);
+/* tf.nn.top_k(keys, k, sorted=True) (core/models.py:403-404) on distinct int64
+ * keys (the m3d_score_keys keys): out_keys [k] the k largest in descending
+ * order, out_pos [k] (nullable) their positions in keys.  Radix select of the
+ * k-th largest key (six digit passes over the keys, no sort of all n), then a
+ * stable sort of the k selected.  Keys equal to the k-th largest are taken in
+ * arbitrary order (the count stays exact): distinct keys give a deterministic
+ * result.  k > n is M3D_EINVAL (tf.nn.top_k's InvalidArgument).
+ * workspace: m3d_topk_workspace_bytes(n, k) bytes of device scratch. */
+size_t m3d_topk_workspace_bytes(int64_t n, int64_t k);
+int m3d_topk_keys(const int64_t* keys, int64_t n, int64_t k, int64_t* out_keys, int64_t* out_pos, void* workspace,
+                  size_t ws_bytes, m3d_stream_t s);
 /* Same keys for a depth slab of the volume: gidx[i] is local anchor i's index
  * in the whole volume's (y,x,z,a)-ordered anchor list (NULL = identity), so
  * the merged top-k over all slabs has the single-volume order. */
@@ -277,7 +304,7 @@ int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B, int64_t H,
                           int64_t D, int64_t Cin, int32_t kh, int32_t kw, int32_t kd,
                           int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
                           int32_t sx, int32_t sz, int32_t py, int32_t px, int32_t pz, float* dw,
-                          m3d_stream_t s);
+                          const m3d_det_t* det, m3d_stream_t s);
 /* Depth-slab forms of the direct convs (no halo-extended copy of the slab): x
  * [B,H,W,Dl,Cin] is the local slab, halo [B,H,W,2r,Cin] the neighbours' r
  * boundary planes (planes [0,r) from below, [r,2r) from above; has_lo / has_hi:
@@ -296,7 +323,7 @@ int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int32_t has_lo
                                const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
                                int32_t kh, int32_t kw, int32_t kd, int64_t Cout, int64_t OH, int64_t OW,
                                int64_t OD, int32_t sy, int32_t sx, int32_t sz, int32_t py, int32_t px,
-                               int32_t pz, float* dw, m3d_stream_t s);
+                               int32_t pz, float* dw, const m3d_det_t* det, m3d_stream_t s);
 
 /* Winograd F(2x2x2,3x3x3) versions of the three passes for stride-1 3x3x3
  * convs with 'same' padding in y/x (every 3x3x3 conv of the graph:
@@ -321,7 +348,7 @@ int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t
                              m3d_stream_t s);
 int m3d_conv3d_bwd_weight_wino(const float* x, const float* dz, int64_t B, int64_t H, int64_t W,
                                int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
-                               float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
+                               float* dw, void* workspace, size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s);
 /* Training variants: the forward keeps its transformed input U = B^T x B
  * ([64][T][Cin], m3d_conv3d_wino_u_bytes) in caller memory (u_keep) and the
  * weight gradient reuses it instead of transforming x again. */
@@ -340,7 +367,7 @@ int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, in
                              size_t ws_bytes, m3d_stream_t s);
 int m3d_conv3d_bwd_weight_wino_u(const float* u, const float* dz, int64_t B, int64_t H, int64_t W,
                                  int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz,
-                                 float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
+                                 float* dw, void* workspace, size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s);
 /* Depth-slab forms (multi-GPU sharding of one volume, m3d/slab.py): x is this
  * rank's slab [B,H,W,Dl,C] and x_halo [B,H,W,2,C] the neighbours' boundary
  * planes (plane 0 = z -1 from the lower rank, valid if has_lo; plane 1 = z Dl
@@ -372,7 +399,7 @@ int m3d_conv3d_bwd_data_wino_halo(const float* dz, const float* w, int32_t has_l
                                   m3d_stream_t s);
 int m3d_conv3d_bwd_weight_wino_halo(const float* x, const float* x_halo, int32_t has_lo, int32_t has_hi,
                                     const float* dz, int64_t B, int64_t H, int64_t W, int64_t Dl, int64_t Cin,
-                                    int64_t Cout, float* dw, void* workspace, size_t ws_bytes, m3d_stream_t s);
+                                    int64_t Cout, float* dw, void* workspace, size_t ws_bytes, const m3d_det_t* det, m3d_stream_t s);
 
 /* Data gradients with the producing unit's BN-ReLU backward fused into their
  * epilogue (the bn_act_bwd pass of core/models.py:102-114 / 157-232 folded
@@ -434,7 +461,7 @@ int m3d_gemm_f32(const float* A, const float* B, float* C, int64_t batch, int64_
  * call with batch = 64 on the transformed input and output gradient; bench.py
  * prices the RPN head's largest one. */
 int m3d_gemm_wgrad_f32(const float* A, const float* B, float* C, int64_t batch, int64_t M, int64_t K,
-                       int64_t N, m3d_stream_t s);
+                       int64_t N, const m3d_det_t* det, m3d_stream_t s);
 
 /* The exact 3-way bf16 split of fp32 data (x = hi + mid + lo, each bf16; exact
  * for normal x): x3 receives the three uint16 planes, plane p at x3 + p*n. */
@@ -653,7 +680,7 @@ int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, i
  * chunk to its segment; norms is [n_segments] device scratch. */
 int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_chunks,
                   const int32_t* seg_of_chunk, const float* l2_coef, int32_t n_segments,
-                  float lr, float momentum, float clipnorm, float* norms, m3d_stream_t s);
+                  float lr, float momentum, float clipnorm, float* norms, const m3d_det_t* det, m3d_stream_t s);
 /* Keras 2.3.1 Adam (keras.optimizers.Adam, the `else` branch of RPN.compile,
  * core/models.py:3356-3357) on the same flat buffers: m, v (and vhat when
  * amsgrad; NULL otherwise) are [n_chunks*1024] moment buffers, lr_t =
@@ -662,13 +689,13 @@ int m3d_sgd_keras(float* params, const float* grads, float* moments, int64_t n_c
 int m3d_adam_keras(float* params, const float* grads, float* m, float* v, float* vhat,
                    int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                    int32_t n_segments, float lr_t, float beta_1, float beta_2, float epsilon,
-                   float clipnorm, float* norms, m3d_stream_t s);
+                   float clipnorm, float* norms, const m3d_det_t* det, m3d_stream_t s);
 /* Keras 2.3.1 Adadelta (core/models.py:3354-3355): accum / delta_accum are the
  * accumulators of keras.optimizers.Adadelta, lr the decayed learning rate. */
 int m3d_adadelta_keras(float* params, const float* grads, float* accum, float* delta_accum,
                        int64_t n_chunks, const int32_t* seg_of_chunk, const float* l2_coef,
                        int32_t n_segments, float lr, float rho, float epsilon, float clipnorm,
-                       float* norms, m3d_stream_t s);
+                       float* norms, const m3d_det_t* det, m3d_stream_t s);
 
 #ifdef __cplusplus
 }

@@ -31,10 +31,11 @@ def main():
     calls = []
     orig = backbone.conv_bn_act
 
-    def rec(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None):
+    def rec(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx=True, link=None, **kw):
         calls.append((tuple(x.shape), layer, geo, relu, None if residual is None else tuple(residual.shape),
                       res_mode, bn, need_dx))
-        return orig(x, layer, geo, relu, residual=residual, res_mode=res_mode, bn=bn, need_dx=need_dx, link=link)
+        return orig(x, layer, geo, relu, residual=residual, res_mode=res_mode, bn=bn, need_dx=need_dx, link=link,
+                    **kw)
 
     backbone.conv_bn_act = rec
     with torch.no_grad():

@@ -36,7 +36,7 @@ int main() {
     const int64_t fshape[4][3] = {{8, 8, 8}, {4, 4, 8}, {2, 2, 8}, {1, 1, 8}};
     const int64_t bad_fshape[4][3] = {{8, 8, 8}, {0, 4, 8}, {2, 2, 8}, {1, 1, 8}};
 
-    if (m3d_abi_version() != 2) { std::printf("FAIL abi version\n"); return 1; }
+    if (m3d_abi_version() != 3) { std::printf("FAIL abi version\n"); return 1; }
 
     // CropAndResize3D family (wheel ops)
     EXPECT_EINVAL(m3d_crop_and_resize3d_fwd(nf, 1, 4, 4, 4, 1, nf, ni, 1, 0, 2, 2, 0, 0.f, of, s));
@@ -93,27 +93,28 @@ int main() {
         EXPECT_EINVAL(m3d_conv3d_bwd_data_wino_bn(nf, nf, 1, 8, 8, 8, 96, 64, 8, 1, of, 0, nullptr, 0, 0, &bn,
                                                   nullptr, 0, s));                      // Cin 96: no fused form
     }
-    EXPECT_EINVAL(m3d_conv3d_bwd_weight(nf, nf, 1, 8, 8, -8, 4, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, of, s));
+    EXPECT_EINVAL(m3d_conv3d_bwd_weight(nf, nf, 1, 8, 8, -8, 4, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, of, nullptr,
+                                         s));
     EXPECT_EINVAL(m3d_conv3d_fwd_dil(nf, 1, 8, 8, 8, 4, nf, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, 0, 1, 1, nf,
                                      nf, nf, nf, 0, 0, of, of, 0, of, 0, 0, s));
     EXPECT_EINVAL(m3d_deconv3d_k2s2(nf, 1, 4, 4, 4, 0, nf, 8, nf, 0, of, s));
     EXPECT_EINVAL(m3d_conv3d_fwd_wino(nf, 1, 8, 8, 8, 128, nf, 128, 8, 1, nf, nf, nf, nf, 0, of, of, nullptr, 0, s));
     EXPECT_EINVAL(m3d_conv3d_bwd_data_wino(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, 0, nullptr, 0, s));
-    EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, nullptr, 0, s));
+    EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, nullptr, 0, nullptr, s));
     EXPECT_EINVAL(m3d_conv3d_fwd_wino_keep(nf, 1, 8, 8, 8, 128, nf, 128, 8, 1, nf, nf, nf, nf, 0, of, of, of,
                                            nullptr, 0, s));
-    EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino_u(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, nullptr, 0, s));
+    EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino_u(nf, nf, 1, 8, 8, 8, 128, 128, 8, 1, of, nullptr, 0, nullptr, s));
 
     EXPECT_EINVAL(m3d_conv3d_fwd_wino_halo(nf, nf, 2, 0, 1, 8, 8, 8, 128, nf, 128, nf, nf, nf, nf, 0, of, of,
                                            of, nullptr, 0, s));
     EXPECT_EINVAL(m3d_conv3d_bwd_data_wino_halo(nf, nf, 1, 0, 1, 8, 8, 8, 128, 128, of, nullptr, 0, nullptr, 0,
                                                 s));
     EXPECT_EINVAL(m3d_conv3d_bwd_weight_wino_halo(nf, nullptr, 0, 1, nf, 1, 8, 8, 8, 128, 128, of, nullptr, 0,
-                                                  s));
+                                                  nullptr, s));
 
     // GEMMs
     EXPECT_EINVAL(m3d_gemm_f32(nf, nf, of, 1, 0, 4, 4, nf, 0, 0, s));
-    EXPECT_EINVAL(m3d_gemm_wgrad_f32(nf, nf, of, 1, 4, -4, 4, s));
+    EXPECT_EINVAL(m3d_gemm_wgrad_f32(nf, nf, of, 1, 4, -4, 4, nullptr, s));
     EXPECT_EINVAL(m3d_split3_f32(nf, 0, nullptr, s));
     EXPECT_EINVAL(m3d_gemm_x3(nullptr, nullptr, of, 1, 64, 48, 64, s));        // K % 32
     EXPECT_EINVAL(m3d_gemm_x3(nullptr, nullptr, of, 1, 1LL << 40, 64, 64, s)); // > 4 GiB operand
@@ -142,14 +143,18 @@ int main() {
     EXPECT_EINVAL(m3d_subsample221_bwd(nf, 1, 4, 4, -4, 4, of, s));
     EXPECT_EINVAL(m3d_bn_affine(nf, nf, nf, nf, 1e-3f, 0, of, of, of, s));
     EXPECT_EINVAL(m3d_bn_act_bwd(nf, nf, nf, 0, 8, 1, nf, nf, nf, of, of, 0, of, of, of, nullptr, 0, s));
-    EXPECT_EINVAL(m3d_sgd_keras(of, nf, of, -1, ni, nf, 1, 0.01f, 0.9f, 5.f, of, s));
-    EXPECT_EINVAL(m3d_adam_keras(of, nf, of, of, of, -1, ni, nf, 1, 1e-3f, 0.9f, 0.999f, 1e-7f, 5.f, of, s));
-    EXPECT_EINVAL(m3d_adadelta_keras(of, nf, of, of, -1, ni, nf, 1, 1.f, 0.95f, 1e-7f, 5.f, of, s));
-    EXPECT_EINVAL(m3d_set_deterministic(1, nullptr, 1 << 20));
-    EXPECT_EINVAL(m3d_set_deterministic(1, of, 64));
-    if (m3d_set_deterministic(0, nullptr, 0) != M3D_OK || m3d_get_deterministic() != 0) {
-        fprintf(stderr, "set_deterministic(0) failed\n");
-        return 1;
+    EXPECT_EINVAL(m3d_sgd_keras(of, nf, of, -1, ni, nf, 1, 0.01f, 0.9f, 5.f, of, nullptr, s));
+    EXPECT_EINVAL(m3d_adam_keras(of, nf, of, of, of, -1, ni, nf, 1, 1e-3f, 0.9f, 0.999f, 1e-7f, 5.f, of, nullptr,
+                                 s));
+    EXPECT_EINVAL(m3d_adadelta_keras(of, nf, of, of, -1, ni, nf, 1, 1.f, 0.95f, 1e-7f, 5.f, of, nullptr, s));
+    {   // per-call deterministic targets (ABI 3): on with no / short / misaligned scratch
+        alignas(16) static char scratch[8192];
+        const m3d_det_t d0 = {1, nullptr, 1 << 20}, d1 = {1, scratch, 64}, d2 = {1, scratch + 4, 4096};
+        EXPECT_EINVAL(m3d_gemm_wgrad_f32(nf, nf, of, 1, 4, 4, 4, &d0, s));
+        EXPECT_EINVAL(m3d_sgd_keras(of, nf, of, 1, ni, nf, 1, 0.01f, 0.9f, 5.f, of, &d1, s));
+        EXPECT_EINVAL(m3d_conv3d_bwd_weight(nf, nf, 1, 8, 8, 8, 4, 3, 3, 3, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, of, &d2, s));
+        EXPECT_EINVAL(m3d_fork_event_create(3, nullptr));
+        EXPECT_EINVAL(m3d_stream_fork(s, s, nullptr));
     }
 
     // workspace sizing: pure host arithmetic over small .. huge shapes

@@ -1,6 +1,7 @@
 """m3d_stream_fork (the weight-gradient stream's fork / join, m3d.nn._fork):
 work enqueued on the destination after the fork sees everything the source
-stream wrote before it, for every event kind; a bad mode is rejected."""
+stream wrote before it, for every event kind (the caller-owned events of
+m3d_fork_event_create, ABI 3); a bad mode / NULL event is rejected."""
 import pytest
 import torch
 
@@ -10,6 +11,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_stream_fork_orders_work(cuda, mode):
     import m3d._lib as lib
+    from m3d.nn import fork_event
     L = lib.load()
     a, b = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
     n = 1 << 24
@@ -20,18 +22,27 @@ def test_stream_fork_orders_work(cuda, mode):
             for _ in range(8):                         # keep stream a busy past the fork
                 x.mul_(1.0000001)
             y = x * 2.0
-        lib.check(L.m3d_stream_fork(a.cuda_stream, b.cuda_stream, mode), "stream_fork")
+        lib.check(L.m3d_stream_fork(a.cuda_stream, b.cuda_stream, fork_event(cuda.index or 0, mode)), "stream_fork")
         with torch.cuda.stream(b):
             s = y.sum()
         y.record_stream(b)
-        lib.check(L.m3d_stream_fork(b.cuda_stream, torch.cuda.current_stream(cuda).cuda_stream, mode),
-                  "stream_fork")
+        lib.check(L.m3d_stream_fork(b.cuda_stream, torch.cuda.current_stream(cuda).cuda_stream,
+                                    fork_event(cuda.index or 0, mode)), "stream_fork")
         want = 2.0 * (it + 1) * (1.0000001 ** 8) * n
         assert abs(float(s) - want) <= 1e-5 * want
 
 
 def test_stream_fork_bad_mode(cuda):
+    import ctypes
+
     import m3d._lib as lib
     s = torch.cuda.current_stream(cuda).cuda_stream
+    ev = ctypes.c_void_p()
     with pytest.raises(ValueError):
-        lib.check(lib.load().m3d_stream_fork(s, s, 3), "stream_fork")
+        lib.check(lib.load().m3d_fork_event_create(3, ctypes.byref(ev)), "fork_event_create")
+    with pytest.raises(ValueError):
+        lib.check(lib.load().m3d_stream_fork(s, s, None), "stream_fork")
+    lib.check(lib.load().m3d_fork_event_create(2, ctypes.byref(ev)), "fork_event_create")
+    lib.check(lib.load().m3d_stream_fork(s, s, ev.value), "stream_fork")
+    torch.cuda.synchronize()
+    lib.check(lib.load().m3d_fork_event_destroy(ev.value), "fork_event_destroy")

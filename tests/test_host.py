@@ -230,6 +230,26 @@ def test_hela_and_default_counts_before_the_patch():
     assert (A.get_anchors(dflt).shape[0], A.rpn_row_count(dflt)) == (326880, 327360)
 
 
+def test_maskrcnn_anchors_leave_the_config_alone():
+    """MaskRCNN (inference) builds its anchors from a patched COPY
+    (model_anchors(inplace=False)): the targeting hela preset keeps its
+    z-stride-2 BACKBONE_STRIDES and ANCHOR_NB, and the anchors still match the
+    head rows.  RPN (inplace=True) patches the caller's config as RPN.train
+    does (core/models.py:3408-3419)."""
+    import copy
+    f = _preset_fields()
+    cfg = C.Config(**f["targeting/scp_target_hela.json"])
+    before = (copy.deepcopy(cfg.BACKBONE_STRIDES), cfg.ANCHOR_NB)
+    assert any((s[2] if isinstance(s, (list, tuple)) else s) != 1 for s in cfg.BACKBONE_STRIDES)
+    with pytest.warns(UserWarning, match="RPN.train"):
+        a = A.model_anchors(cfg, inplace=False)
+    assert (cfg.BACKBONE_STRIDES, cfg.ANCHOR_NB) == before
+    assert a.shape == (A.rpn_row_count(cfg), 6)
+    with pytest.warns(UserWarning, match="RPN.train"):
+        b = A.model_anchors(cfg)
+    assert np.array_equal(a, b) and all(s[2] == 1 for s in cfg.BACKBONE_STRIDES)
+
+
 def test_inconsistent_preset_raises():
     """y/x strides the network does not have, or several scales per level,
     cannot give one anchor per row: ValueError, never a silent gather."""

@@ -134,6 +134,25 @@ def _replicas(rank, world):
             "close": rel_close(1.0, 1.0 + 5e-6, 1e-5), "far": rel_close(1.0, 1.0 + 5e-5, 1e-5)}
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float64, torch.float32, torch.int64,
+                                   torch.bool])
+def test_tensor_digest_is_bit_level_at_every_width(dtype):
+    """tensor_digest reads each element's bytes as an integer of the element's
+    width: a change in the last fraction bit of one bf16 / fp16 / fp64 element
+    changes the digest (a value cast to int64 would truncate it away)."""
+    from m3d.parallel import tensor_digest
+    g = torch.Generator().manual_seed(3)
+    w = (torch.rand(4096, generator=g) * 8).to(dtype) if dtype != torch.bool else torch.rand(4096, generator=g) > .5
+    bad = w.clone()
+    if dtype == torch.bool:
+        bad[77] = ~bad[77]
+    else:
+        it = {2: torch.int16, 4: torch.int32, 8: torch.int64}[w.element_size()]
+        bad.view(it)[77] ^= 1
+    assert torch.equal(tensor_digest(w), tensor_digest(w.clone()))
+    assert not torch.equal(tensor_digest(w), tensor_digest(bad))
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_validate_replicas(world):
     out = run(_replicas, world)
