@@ -207,6 +207,147 @@ __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float4* __restr
     }
 }
 
+// z-stride-1 pools (the stem's MaxPooling3D((3,3,3),(2,2,1),'same'),
+// core/models.py:245) over runs of R consecutive output (fwd) / input (bwd) z
+// planes per thread: the windows of neighbouring z overlap in all but one
+// plane, so each input plane (fwd) or dy / argmax plane (bwd) is loaded once
+// per run instead of up to kd times (the per-element forms re-read every
+// window: 27 float4 loads per output, L2-bound at 2.3 TB/s of HBM bytes at
+// 256^3).  Per output the window is visited in the same (ky, kx, kz) order with
+// the same first-valid / strict '>' rule, and per input the backward adds its
+// windows in the same (oy, ox, oz) order: bit-identical to the kernels above.
+template <bool HALO, int R>
+__global__ __launch_bounds__(256) void maxpool_fwd4z_kernel(const float4* __restrict__ x, int H, int W, int D,
+                                                            int C4, int kh, int kw, int kd, int sy, int sx,
+                                                            int py, int px, int pz, int OH, int OW, int OD,
+                                                            int nrun, uint32_t total, float4* __restrict__ y,
+                                                            uchar4* __restrict__ am, PoolHalo hz) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int run = (int)(t % (uint32_t)nrun); t /= (uint32_t)nrun;
+        const int ox = (int)(t % (uint32_t)OW); t /= (uint32_t)OW;
+        const int oy = (int)(t % (uint32_t)OH);
+        const uint32_t b = t / (uint32_t)OH;
+        const int oz0 = run * R;
+        const int nr = OD - oz0 < R ? OD - oz0 : R;
+        float best[R][4];
+        int bi[R][4];
+        bool any[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            any[r] = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { best[r][q] = -INFINITY; bi[r][q] = 0; }
+        }
+        for (int ky = 0; ky < kh; ++ky) {
+            const int iy = oy * sy - py + ky;
+            if (iy < 0 || iy >= H) continue;
+            for (int kx = 0; kx < kw; ++kx) {
+                const int ix = ox * sx - px + kx;
+                if (ix < 0 || ix >= W) continue;
+                const uint32_t bhw = (b * (uint32_t)H + iy) * (uint32_t)W + ix;
+                const int base = (ky * kw + kx) * kd;
+                const int iz_lo = oz0 - pz < 0 ? 0 : oz0 - pz;
+                const int iz_end = oz0 + nr - 1 - pz + kd;
+                for (int iz = iz_lo; iz < iz_end && iz < D; ++iz) {
+                    bool hal;
+                    const uint32_t zo = pool_zoff<HALO>(hz, bhw, D, iz, C4, hal);
+                    const float4 v = (HALO && hal ? hz.h : x)[zo + c];
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kz = iz - (oz0 + r - pz);
+                        if (r < nr && kz >= 0 && kz < kd) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                if (!any[r] || vv[q] > best[r][q]) { best[r][q] = vv[q]; bi[r][q] = base + kz; }
+                            any[r] = true;
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t o0 = ((b * (uint32_t)OH + oy) * (uint32_t)OW + ox) * (uint32_t)OD + oz0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r >= nr) break;
+            const uint32_t o = (o0 + r) * (uint32_t)C4 + c;
+            y[o] = make_float4(best[r][0], best[r][1], best[r][2], best[r][3]);
+            if (am) am[o] = make_uchar4((unsigned char)bi[r][0], (unsigned char)bi[r][1], (unsigned char)bi[r][2],
+                                        (unsigned char)bi[r][3]);
+        }
+    }
+}
+
+template <bool HALO, int R>
+__global__ __launch_bounds__(256) void maxpool_bwd4z_kernel(const float4* __restrict__ dy,
+                                                            const uchar4* __restrict__ am, int H, int W, int D,
+                                                            int C4, int kh, int kw, int kd, int sy, int sx, int py,
+                                                            int px, int pz, int OH, int OW, int OD, int nrun,
+                                                            uint32_t total, float4* __restrict__ dx, PoolHalo hz) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int run = (int)(t % (uint32_t)nrun); t /= (uint32_t)nrun;
+        const int ix = (int)(t % (uint32_t)W); t /= (uint32_t)W;
+        const int iy = (int)(t % (uint32_t)H);
+        const uint32_t b = t / (uint32_t)H;
+        const int iz0 = run * R;
+        const int nr = D - iz0 < R ? D - iz0 : R;
+        float acc[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] = 0.0f;
+        const int oy_lo = max(0, (iy + py - kh + 1 + sy - 1) / sy), oy_hi = min(OH - 1, (iy + py) / sy);
+        const int ox_lo = max(0, (ix + px - kw + 1 + sx - 1) / sx), ox_hi = min(OW - 1, (ix + px) / sx);
+        // outputs oz with oz - pz <= iz <= oz - pz + kd - 1 for some iz of the run
+        const int oz_lo = max(0, iz0 + pz - kd + 1), oz_hi = min(OD - 1, iz0 + nr - 1 + pz);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const int ky = iy - (oy * sy - py);
+            if (ky < 0 || ky >= kh) continue;
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int kx = ix - (ox * sx - px);
+                if (kx < 0 || kx >= kw) continue;
+                const uint32_t row = ((b * (uint32_t)OH + oy) * (uint32_t)OW + ox) * (uint32_t)OD;
+                const int base = (ky * kw + kx) * kd;
+                for (int oz = oz_lo; oz <= oz_hi; ++oz) {
+                    const uint32_t o = (row + oz) * (uint32_t)C4 + c;
+                    const uchar4 a = am[o];
+                    const float4 g = dy[o];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kz = iz0 + r - (oz - pz);
+                        if (r < nr && kz >= 0 && kz < kd) {
+                            const unsigned char id = (unsigned char)(base + kz);
+                            if (a.x == id) acc[r][0] += g.x;
+                            if (a.y == id) acc[r][1] += g.y;
+                            if (a.z == id) acc[r][2] += g.z;
+                            if (a.w == id) acc[r][3] += g.w;
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t bhw = (b * (uint32_t)H + iy) * (uint32_t)W + ix;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r >= nr) break;
+            const float4 v = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+            if (HALO) {
+                bool hal;
+                const uint32_t zo = pool_zoff<true>(hz, bhw, D, iz0 + r, C4, hal);
+                (hal ? hz.dh : dx)[zo + c] = v;
+            } else {
+                dx[(bhw * (uint32_t)D + iz0 + r) * (uint32_t)C4 + c] = v;
+            }
+        }
+    }
+}
+
+constexpr int POOL_ZRUN = 8;
+
 // IDX: the index type of the element loop (uint32_t when the source has < 2^32
 // float4s: the 64-bit div/mod of the decomposition are software sequences)
 template <typename IDX>
@@ -625,6 +766,15 @@ extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && B * H * W * D * C / 4 < 0x7FFFFFFF && total / 4 < 0x7FFFFFFF &&
         ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        if (sz == 1) {
+            const int nrun = (int)((OD + POOL_ZRUN - 1) / POOL_ZRUN);
+            const int64_t nt = B * OH * OW * nrun * (C / 4);
+            hipLaunchKernelGGL((maxpool_fwd4z_kernel<false, POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                               (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, py, px,
+                               pz, (int)OH, (int)OW, (int)OD, nrun, (uint32_t)nt, (float4*)y, (uchar4*)argmax,
+                               PoolHalo{});
+            return check_launch("maxpool_fwd4z_kernel");
+        }
         hipLaunchKernelGGL(maxpool_fwd4_kernel<false>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
                            (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, sz,
                            py, px, pz, (int)OH, (int)OW, (int)OD, (uint32_t)(total / 4), (float4*)y,
@@ -648,6 +798,15 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && total / 4 < 0x7FFFFFFF && B * OH * OW * OD * C / 4 < 0x7FFFFFFF &&
         ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        if (sz == 1) {
+            const int nrun = (int)((D + POOL_ZRUN - 1) / POOL_ZRUN);
+            const int64_t nt = B * H * W * nrun * (C / 4);
+            hipLaunchKernelGGL((maxpool_bwd4z_kernel<false, POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                               (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4), kh,
+                               kw, kd, sy, sx, py, px, pz, (int)OH, (int)OW, (int)OD, nrun, (uint32_t)nt,
+                               (float4*)dx, PoolHalo{});
+            return check_launch("maxpool_bwd4z_kernel");
+        }
         hipLaunchKernelGGL(maxpool_bwd4_kernel<false>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
                            (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
                            kh, kw, kd, sy, sx, sz, py, px, pz, (int)OH, (int)OW, (int)OD,
@@ -690,11 +849,12 @@ extern "C" int m3d_maxpool3d_fwd_halo(const float* x, const float* halo, int32_t
     const int64_t total = B * OH * OW * OD * C;
     if (total == 0) return M3D_OK;
     PoolHalo hz{(const float4*)halo, nullptr, nlo, (int)Dl, r};
-    hipLaunchKernelGGL(maxpool_fwd4_kernel<true>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
-                       (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, sz,
-                       py, px, pz - nlo, (int)OH, (int)OW, (int)OD, (uint32_t)(total / 4), (float4*)y,
-                       (uchar4*)argmax, hz);
-    return check_launch("maxpool_fwd4_kernel<halo>");
+    const int nrun = (int)((OD + POOL_ZRUN - 1) / POOL_ZRUN);      // (sz == 1: pool_halo_args)
+    const int64_t nt = B * OH * OW * nrun * (C / 4);
+    hipLaunchKernelGGL((maxpool_fwd4z_kernel<true, POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                       (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd, sy, sx, py, px,
+                       pz - nlo, (int)OH, (int)OW, (int)OD, nrun, (uint32_t)nt, (float4*)y, (uchar4*)argmax, hz);
+    return check_launch("maxpool_fwd4z_kernel<halo>");
 }
 
 // Backward of m3d_maxpool3d_fwd_halo: dx [B,H,W,Dl,C] (the slab's own planes)
@@ -715,11 +875,12 @@ extern "C" int m3d_maxpool3d_bwd_halo(const float* dy, const uint8_t* argmax, in
     const int64_t total = B * H * W * D * C;
     if (total == 0) return M3D_OK;
     PoolHalo hz{nullptr, (float4*)dhalo, nlo, (int)Dl, r};
-    hipLaunchKernelGGL(maxpool_bwd4_kernel<true>, dim3(ew_grid(total / 4)), dim3(256), 0, st(s),
-                       (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
-                       kh, kw, kd, sy, sx, sz, py, px, pz - nlo, (int)OH, (int)OW, (int)OD,
-                       (uint32_t)(total / 4), (float4*)dx, hz);
-    return check_launch("maxpool_bwd4_kernel<halo>");
+    const int nrun = (int)((D + POOL_ZRUN - 1) / POOL_ZRUN);       // the virtual grid [lo halo | slab | hi halo]
+    const int64_t nt = B * H * W * nrun * (C / 4);
+    hipLaunchKernelGGL((maxpool_bwd4z_kernel<true, POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                       (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4), kh, kw, kd,
+                       sy, sx, py, px, pz - nlo, (int)OH, (int)OW, (int)OD, nrun, (uint32_t)nt, (float4*)dx, hz);
+    return check_launch("maxpool_bwd4z_kernel<halo>");
 }
 
 extern "C" int m3d_upsample221_bwd(const float* d_up, int64_t B, int64_t H, int64_t W, int64_t D,

@@ -6,12 +6,12 @@
 // of m3d_nms3d's candidates.
 //
 //   select: radix select of the k-th largest key, six digit passes over the
-//           keys (11, 11, 11, 11, 11, 9 bits from the top).  Every pass is one
-//           launch: each workgroup first replays the earlier passes'
-//           histograms (2048 bins, a block-wide suffix scan) to get the digit
-//           prefix of the threshold and the number of keys still needed below
-//           the prefix, then counts the next digit of the keys that share the
-//           prefix in an LDS histogram and adds it to the pass's global one.
+//           keys (11, 11, 11, 11, 11, 9 bits from the top).  Every pass counts
+//           the next digit of the keys that share the threshold's prefix in an
+//           LDS histogram (wave-aggregated adds: the first digits of score keys
+//           are few) added to the pass's global one; a one-block kernel then
+//           scans it (2048 bins, largest first) for the next digit of the
+//           prefix and the keys still needed below it.
 //           The keys are read once per pass (33 MB per pass at 256^3's 4.2 M
 //           anchors); no sort of the n keys.
 //   gather: the keys >= the threshold (exactly k of them for distinct keys)
@@ -37,63 +37,59 @@ constexpr int TK_BINS = 2048;
 __device__ __host__ constexpr int tk_shift(int p) { return p < 5 ? 53 - 11 * p : 0; }
 __device__ __host__ constexpr int tk_width(int p) { return p < 5 ? 11 : 9; }
 
-// Replay passes [0, pass) of the histograms: the threshold's digit prefix
-// (bits above tk_shift(pass - 1)) and how many keys are still needed among the
-// keys sharing it.  Every thread of the 256-thread block gets the result.
-__device__ void tk_prefix(const uint32_t* __restrict__ hists, int pass, int64_t k, uint64_t& prefix_out,
-                          int64_t& need_out) {
-    __shared__ uint32_t part[256];
-    __shared__ uint64_t s_prefix;
-    __shared__ int64_t s_need;
-    const int t = threadIdx.x;
-    if (t == 0) {
-        s_prefix = 0;
-        s_need = k;
-    }
-    __syncthreads();
-    for (int q = 0; q < pass; ++q) {
-        const int64_t need = s_need;                   // read by every thread before anyone updates it
-        const uint32_t* h = hists + (size_t)q * TK_BINS;
-        const int nb = 1 << tk_width(q);
-        const int per = nb / 256;                      // 8 bins per thread (2 in the 9-bit pass)
-        // thread t owns bins [nb - per*(t+1), nb - per*t): t = 0 holds the largest digits
-        const int hi = nb - per * t;
-        uint32_t sum = 0;
-        for (int b = hi - per; b < hi; ++b) sum += h[b];
-        part[t] = sum;
-        __syncthreads();
-        // inclusive prefix over threads (largest digits first), Hillis-Steele in LDS
-        for (int off = 1; off < 256; off <<= 1) {
-            const uint32_t v = t >= off ? part[t - off] : 0u;
-            __syncthreads();
-            part[t] += v;
-            __syncthreads();
-        }
-        const uint32_t before = t ? part[t - 1] : 0u;  // keys in larger digits than this thread's bins
-        if ((int64_t)before < need && need <= (int64_t)part[t]) {
-            uint32_t c = before;
-            for (int b = hi - 1; b >= hi - per; --b) {
-                if (need <= (int64_t)(c + h[b])) {
-                    s_prefix |= (uint64_t)b << tk_shift(q);
-                    s_need = need - c;
-                    break;
-                }
-                c += h[b];
-            }
-        }
-        __syncthreads();
-    }
-    prefix_out = s_prefix;
-    need_out = s_need;
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void topk_hist_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t k,
-                                                        uint32_t* __restrict__ hists, int pass) {
-    __shared__ uint32_t lh[TK_BINS];
+// Selection state after each digit pass: the threshold's digit prefix (bits
+// at and above the pass's shift) and how many keys are still needed among the
+// keys sharing it.  st[0] = (0, k); st[p + 1] = tk_state_kernel(st[p], hist[p]).
+struct TkState {
     uint64_t prefix;
     int64_t need;
-    tk_prefix(hists, pass, k, prefix, need);
+};
+
+// one 256-thread block: the digit of pass `pass` holding the need-th largest
+// key below the prefix (a suffix scan over the pass's histogram, largest digit
+// first), written to st[pass + 1]
+__global__ __launch_bounds__(256) void tk_state_kernel(const uint32_t* __restrict__ hists, int pass, int64_t k,
+                                                       TkState* __restrict__ st) {
+    __shared__ uint32_t part[256];
+    const int t = threadIdx.x;
+    const TkState cur = pass ? st[pass] : TkState{0, k};
+    const uint32_t* h = hists + (size_t)pass * TK_BINS;
+    const int nb = 1 << tk_width(pass);
+    const int per = nb / 256;                          // 8 bins per thread (2 in the 9-bit pass)
+    const int hi = nb - per * t;                       // thread t owns bins [hi - per, hi): t = 0 the largest
+    uint32_t sum = 0;
+    for (int b = hi - per; b < hi; ++b) sum += h[b];
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {         // inclusive prefix over threads, Hillis-Steele
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const int64_t need = cur.need;
+    const uint32_t before = t ? part[t - 1] : 0u;      // keys in larger digits than this thread's bins
+    if ((int64_t)before < need && need <= (int64_t)part[t]) {
+        uint32_t c = before;
+        for (int b = hi - 1; b >= hi - per; --b) {
+            if (need <= (int64_t)(c + h[b])) {
+                st[pass + 1] = TkState{cur.prefix | ((uint64_t)b << tk_shift(pass)), need - (int64_t)c};
+                break;
+            }
+            c += h[b];
+        }
+    }
+}
+
+// LDS histogram of the pass's digit over the keys sharing the prefix; the
+// first pass's digits are few (the scores' sign / exponent bits), so the adds
+// of a wave are aggregated per distinct digit (up to 4 rounds of readfirstlane
+// + ballot) before the per-lane fallback
+__global__ __launch_bounds__(256) void topk_hist_kernel(const int64_t* __restrict__ keys, int64_t n,
+                                                        const TkState* __restrict__ st, uint32_t* __restrict__ hists,
+                                                        int pass) {
+    __shared__ uint32_t lh[TK_BINS];
+    const uint64_t prefix = pass ? st[pass].prefix : 0;
     const int nb = 1 << tk_width(pass);
     for (int b = threadIdx.x; b < nb; b += 256) lh[b] = 0;
     __syncthreads();
@@ -101,9 +97,27 @@ __global__ __launch_bounds__(256) void topk_hist_kernel(const int64_t* __restric
     const uint64_t dmask = (uint64_t)nb - 1;
     const int hsh = pass ? tk_shift(pass - 1) : 64;    // bits at and above hsh must match the prefix
     const uint64_t want = hsh < 64 ? (prefix >> hsh) : 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const uint64_t u = (uint64_t)keys[i] ^ 0x8000000000000000ull;
-        if (hsh == 64 || (u >> hsh) == want) atomicAdd(&lh[(u >> sh) & dmask], 1u);
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < n; i0 += (int64_t)gridDim.x * 256) {   // block-uniform trip
+        const int64_t i = i0 + threadIdx.x;
+        bool live = false;
+        uint32_t bin = 0;
+        if (i < n) {
+            const uint64_t u = (uint64_t)keys[i] ^ 0x8000000000000000ull;
+            live = hsh == 64 || (u >> hsh) == want;
+            bin = (uint32_t)((u >> sh) & dmask);
+        }
+#pragma unroll
+        for (int round = 0; round < 4; ++round) {
+            const uint64_t act = __ballot(live);
+            if (!act) break;
+            const int leader = __ffsll((long long)act) - 1;
+            const uint32_t lb = (uint32_t)__shfl(bin, leader);
+            const uint64_t same = __ballot(live && bin == lb);
+            if (lane == leader) atomicAdd(&lh[lb], (uint32_t)__popcll(same));
+            if (live && bin == lb) live = false;
+        }
+        if (live) atomicAdd(&lh[bin], 1u);
     }
     __syncthreads();
     uint32_t* gh = hists + (size_t)pass * TK_BINS;
@@ -113,13 +127,12 @@ __global__ __launch_bounds__(256) void topk_hist_kernel(const int64_t* __restric
 
 // the keys >= the threshold, unordered; among keys EQUAL to the threshold only
 // the `need` first to claim a slot are taken (distinct keys: exactly one)
-__global__ __launch_bounds__(256) void topk_gather_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t k,
-                                                          const uint32_t* __restrict__ hists,
+__global__ __launch_bounds__(256) void topk_gather_kernel(const int64_t* __restrict__ keys, int64_t n,
+                                                          const TkState* __restrict__ st,
                                                           unsigned long long* __restrict__ counters,
                                                           uint64_t* __restrict__ sel_u, int64_t* __restrict__ sel_pos) {
-    uint64_t thr;
-    int64_t need;
-    tk_prefix(hists, TK_PASSES, k, thr, need);
+    const uint64_t thr = st[TK_PASSES].prefix;
+    const int64_t need = st[TK_PASSES].need;
     __shared__ uint32_t cnt, base;
     __shared__ uint64_t su[256];
     __shared__ int64_t sp[256];
@@ -155,24 +168,37 @@ constexpr int RS_CHUNK = 2048;
 template <bool DESC>
 __global__ __launch_bounds__(256) void rank_count_kernel(const uint64_t* __restrict__ u, int64_t n,
                                                          uint32_t* __restrict__ rank) {
-    __shared__ uint64_t su[RS_CHUNK];
+    __shared__ __attribute__((aligned(16))) uint64_t su[RS_CHUNK];
     const int64_t c0 = (int64_t)blockIdx.y * RS_CHUNK;
     const int cn = (int)((n - c0) < RS_CHUNK ? (n - c0) : RS_CHUNK);
-    for (int j = threadIdx.x; j < cn; j += 256) su[j] = u[c0 + j];
+    const int cp = (cn + 7) & ~7;
+    // padding never counts: DESC pads 0 (never above a key; an equal 0 sits at j >= jt),
+    // ascending pads ~0
+    for (int j = threadIdx.x; j < cp; j += 256) su[j] = j < cn ? u[c0 + j] : (DESC ? 0ull : ~0ull);
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t ui = u[i];
-    // j < jt (chunk-local) are the positions below i: they win ties
+    // chunk positions j < jt are below i: equal keys there come first (stable)
     const int64_t jt64 = i - c0;
     const int jt = jt64 < 0 ? 0 : (jt64 > cn ? cn : (int)jt64);
     uint32_t r = 0;
-    if constexpr (DESC) {
-        for (int j = 0; j < jt; ++j) r += su[j] >= ui;
-        for (int j = jt; j < cn; ++j) r += su[j] > ui;
-    } else {
-        for (int j = 0; j < jt; ++j) r += su[j] <= ui;
-        for (int j = jt; j < cn; ++j) r += su[j] < ui;
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(su);
+    for (int j = 0; j < cp; j += 8) {                  // 4 x ds_read_b128 in flight per step
+        ulonglong2 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = s2[(j >> 1) + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ja = j + 2 * q;
+            if constexpr (DESC) {
+                r += (v[q].x > ui) | ((v[q].x == ui) & (ja < jt));
+                r += (v[q].y > ui) | ((v[q].y == ui) & (ja + 1 < jt));
+            } else {
+                r += (v[q].x < ui) | ((v[q].x == ui) & (ja < jt));
+                r += (v[q].y < ui) | ((v[q].y == ui) & (ja + 1 < jt));
+            }
+        }
     }
     if (gridDim.y == 1) rank[i] = r;
     else if (r) atomicAdd(&rank[i], r);
@@ -286,6 +312,7 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 struct TopkWs {
     uint32_t* hists;
     unsigned long long* counters;
+    TkState* st;
     uint64_t* sel_u;
     int64_t* sel_pos;
     uint32_t* rank;
@@ -304,6 +331,7 @@ static TopkWs topk_ws(int64_t k, void* base) {
     const int64_t kk = k > 0 ? k : 1;
     w.hists = (uint32_t*)take(sizeof(uint32_t) * TK_PASSES * TK_BINS + 2 * sizeof(unsigned long long));
     w.counters = w.hists ? (unsigned long long*)(w.hists + TK_PASSES * TK_BINS) : nullptr;
+    w.st = (TkState*)take(sizeof(TkState) * (TK_PASSES + 1));
     w.sel_u = (uint64_t*)take(sizeof(uint64_t) * kk);
     w.sel_pos = (int64_t*)take(sizeof(int64_t) * kk);
     w.rank = (uint32_t*)take(rank_sort_scratch_bytes(kk));
@@ -335,11 +363,12 @@ extern "C" int m3d_topk_keys(const int64_t* keys, int64_t n, int64_t k, int64_t*
         return check_launch("topk: memset");
     const unsigned grid = (unsigned)std::min<int64_t>((n + 1023) / 1024, 1024);
     for (int p = 0; p < TK_PASSES; ++p) {
-        hipLaunchKernelGGL(topk_hist_kernel, dim3(grid), dim3(256), 0, st(s), keys, n, k, w.hists, p);
+        hipLaunchKernelGGL(topk_hist_kernel, dim3(grid), dim3(256), 0, st(s), keys, n, w.st, w.hists, p);
+        hipLaunchKernelGGL(tk_state_kernel, dim3(1), dim3(256), 0, st(s), w.hists, p, k, w.st);
         int rc = check_launch("topk_hist_kernel");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(topk_gather_kernel, dim3(grid), dim3(256), 0, st(s), keys, n, k, w.hists, w.counters,
+    hipLaunchKernelGGL(topk_gather_kernel, dim3(grid), dim3(256), 0, st(s), keys, n, w.st, w.counters,
                        w.sel_u, w.sel_pos);
     int rc = check_launch("topk_gather_kernel");
     if (rc) return rc;

@@ -277,3 +277,21 @@ def test_reference_presets_load_in_place():
             warnings.simplefilter("ignore")
             a = A.model_anchors(cfg)
         assert a.shape[0] == A.rpn_row_count(cfg), p
+
+
+def test_check_fuses_flags_an_unconsumed_fused_backward():
+    """nn.check_fuses: a BNFuse record whose consumer applied the
+    fused BN-ReLU backward (done) but whose producer's backward never took it
+    raises; armed-but-unused and consumed records pass."""
+    from m3d import nn as mnn
+    reg = []
+    a, b, c = mnn.BNFuse(reg), mnn.BNFuse(reg), mnn.BNFuse(reg)
+    assert reg == [a, b, c]
+    a.name, b.name = "res2a_branch2a", "res2a_branch2b"
+    a.armed = b.armed = True
+    mnn.check_fuses(reg)                  # armed, not applied: fine
+    b.done = True
+    with pytest.raises(RuntimeError, match="res2a_branch2b"):
+        mnn.check_fuses(reg)
+    b.clear()                             # the producer's backward consumed it
+    mnn.check_fuses(reg)
