@@ -62,6 +62,15 @@ inline unsigned grid_for(int64_t n, int per_block, int64_t cap = 1 << 30) {
 
 // std::min / std::max semantics (NaN behaviour identical to the reference's
 // TF 2.2 CPU kernels).
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, then
+// s_barrier.  __syncthreads() also fences global memory (s_waitcnt vmcnt(0)
+// before the barrier), which drains every prefetch in flight -- a serial
+// kernel that loads the next step's global operands before a barrier pays a
+// full memory round trip per step with it.  Use only where the barrier orders
+// LDS traffic alone (global results are not read by other waves after it).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
 
@@ -154,6 +163,12 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
 // 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at
 // 128^3 (same box, r04ny4_ab), parity suite green (profiles/r04ny4_parity_tests.log)
+// x3 GEMM accumulation (conv3d.hip x3_mac): 1 = each 16-deep k step's six
+// bf16 MFMAs into a fresh accumulator, added to the running sum by one VALU
+// add (round 5: half the fp32 error); 0 = one MFMA accumulator chain
+#ifndef M3D_TUNE_X3_ACC
+#define M3D_TUNE_X3_ACC 1
+#endif
 #ifndef M3D_TUNE_WINO_NY
 #define M3D_TUNE_WINO_NY 4
 #endif
@@ -165,6 +180,12 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #endif
 #ifndef M3D_TUNE_WINO_DGRAD_NZ
 #define M3D_TUNE_WINO_DGRAD_NZ 0
+#endif
+// the data gradient's y tile (conv3d.hip wino_dgrad_ny): 2 = F(2x2x4) data
+// gradients beside F(4x2x4) forwards / weight gradients (round 5, accuracy);
+// 0 = the forward's
+#ifndef M3D_TUNE_WINO_DGRAD_NY
+#define M3D_TUNE_WINO_DGRAD_NY 2
 #endif
 #ifndef M3D_TUNE_WINO_XCD
 #define M3D_TUNE_WINO_XCD 0

@@ -189,6 +189,72 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2* o) {
     o[1] = make_uint2(m0, m1);
     o[2] = make_uint2(l0, l1);
 }
+// M3D_TUNE_X3_ACC bit 0: the point-GEMM kernels (x3_gemm*), bit 1: the
+// implicit-GEMM convs (conv_gemm_kernel X3), bit 2: the weight-gradient GEMMs
+constexpr int X3ACC_GEMM = M3D_TUNE_X3_ACC & 1, X3ACC_CONV = (M3D_TUNE_X3_ACC >> 1) & 1,
+              X3ACC_WG = (M3D_TUNE_X3_ACC >> 2) & 1;
+// One 16-deep k step of an fp32 product sum on the split: acc += sum_k a_k b_k
+// as the six bf16 MFMAs (small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi)
+// (hi,mid) (hi,hi)).  M3D_TUNE_X3_ACC 1 (round 5): the six run into a fresh
+// accumulator (C = 0) and the step's partial is added to acc by one VALU add
+// -- one rounding of |acc| per k step instead of six (each MFMA rounds its
+// result to fp32 at the accumulator's magnitude, however small its own
+// terms).  Halves the fp32 error of every x3 GEMM: a Winograd F(4x2x4) conv
+// 5.5e-6 -> 2.7e-6, F(2x2x4) 1.4e-6 -> 0.65e-6 of the output scale
+// (scripts/wino_stage_error.py, modes x3 / x3sep).  0: one accumulator chain.
+template <int X3ACC>
+__device__ __forceinline__ void x3_mac(floatx16& acc, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                       const bf16x8& bh, const bf16x8& bm, const bf16x8& bl) {
+    if constexpr (X3ACC == 1) {
+        floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, floatx16{}, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, t, 0, 0, 0);
+        acc += t;
+    } else {
+        floatx16 c = acc;
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+    }
+}
+// x3_mac over a wave's TM x TN accumulator tiles with fragments af[i][plane],
+// bf[j][plane].  X3ACC 1: a lag-1 pipeline -- tile q's six MFMAs issue beside
+// tile q-1's VALU add, a scheduling barrier per tile keeps two step partials
+// live (without it the compiler runs every tile's chain first and holds all
+// their partials: spills in the 128x128 kernels).
+template <int TM, int TN, int X3ACC>
+__device__ __forceinline__ void x3_mac_tiles(floatx16 (&acc)[TM][TN], const bf16x8 (&af)[TM][3],
+                                             const bf16x8 (&bf)[TN][3]) {
+    if constexpr (X3ACC == 1) {
+        floatx16 pend;
+#pragma unroll
+        for (int q = 0; q < TM * TN; ++q) {
+            const int i = q / TN, j = q % TN;
+            floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bf[j][0], floatx16{}, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bf[j][1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][2], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bf[j][0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][0], t, 0, 0, 0);
+            if (q > 0) acc[(q - 1) / TN][(q - 1) % TN] += pend;
+            pend = t;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        acc[TM - 1][TN - 1] += pend;
+    } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                x3_mac<0>(acc[i][j], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2]);
+    }
+}
 // byte offset of (row, k) in an X3 LDS plane: 32 k x bf16 = 64-B rows, 16-B
 // chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 phase over
 // 16 consecutive rows of one chunk hits 16 distinct 4-bank groups.
@@ -650,19 +716,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) vo
                     for (int pl = 0; pl < 3; ++pl)
                         bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * (BN * BK * 2) + off);
                 }
-                // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        floatx16 c = acc[i][j];
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
-                    }
+                x3_mac_tiles<TM, TN, X3ACC_CONV>(acc, af, bfr);
             }
         } else {
         const float* As = smem + buf * (A_SZ + B_SZ);
@@ -1414,18 +1468,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PL + off);
             }
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) {
-                    floatx16 c = acc[i][j];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
-                }
+            x3_mac_tiles<TI, TJ, X3ACC_WG>(acc, af, bfr);
         }
         __syncthreads();
         if (t + 1 < nchunks) {
@@ -1597,13 +1640,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
                     continue;
                 }
-                floatx16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+                x3_mac<X3ACC_WG>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
             }
         }
     };
@@ -1915,10 +1952,10 @@ __device__ __forceinline__ void tile_coords(int64_t t, const WinoGeom& g, int& b
 // (2ty-1, 2tx-1, NZ*tz-pz); xi = (a*4 + b)*P + k.
 // X3O: U is written as the three bf16 planes of split3 (uint16 [3][points][T][C])
 // for x3_gemm_kernel -- the split is done once here, not per GEMM k-tile.
-template <int NZ, bool X3O = false, bool HALO = false>
+template <int NZ, bool X3O = false, bool HALO = false, int NYT = WNY>
 __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, WinoGeom g,
                                                          int C, float* __restrict__ U) {
-    constexpr int P = ZT<NZ>::P;
+    constexpr int P = ZT<NZ>::P, PYt = ZT<NYT>::P;
     const int64_t i = wino_block(g) * blockDim.x + threadIdx.x;
     if (i >= g.T * C) return;
     const int c = (int)(i % C);
@@ -1929,7 +1966,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
         const bool edge = tz == 0 || tz == g.TZ - 1;
         if ((g.tz_mode == 1) == edge) return;
     }
-    float d[PY][4][P];
+    float d[PYt][4][P];
     // branch-free window loads: raw buffer loads whose out-of-range offset
     // returns 0 (the zero padding), so all 16*P loads issue back to back
     // (conditional global loads compiled to a branch + wait per element)
@@ -1937,8 +1974,8 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     __amdgpu_buffer_rsrc_t rh;
     if constexpr (HALO) rh = make_rsrc(g.halo, (uint64_t)g.B * g.H * g.W * 2 * C * 4);
 #pragma unroll
-    for (int a = 0; a < PY; ++a) {
-        const int y = WNY * ty - 1 + a;
+    for (int a = 0; a < PYt; ++a) {
+        const int y = NYT * ty - 1 + a;
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int xx = 2 * tx - 1 + bb;
@@ -1965,30 +2002,30 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
         }
     }
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) ZT<NZ>::bt(d[a][bb]);
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int k = 0; k < P; ++k) bt4(d[a][0][k], d[a][1][k], d[a][2][k], d[a][3][k]);
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            float col[PY];
+            float col[PYt];
 #pragma unroll
-            for (int a = 0; a < PY; ++a) col[a] = d[a][bb][k];
-            YT::bt(col);
+            for (int a = 0; a < PYt; ++a) col[a] = d[a][bb][k];
+            ZT<NYT>::bt(col);
 #pragma unroll
-            for (int a = 0; a < PY; ++a) d[a][bb][k] = col[a];
+            for (int a = 0; a < PYt; ++a) d[a][bb][k] = col[a];
         }
     const int64_t stride = g.T * C;
     if constexpr (X3O) {
         unsigned short* o = reinterpret_cast<unsigned short*>(U) + t * C + c;
-        const int64_t pstride = (int64_t)PY * 4 * P * stride;
+        const int64_t pstride = (int64_t)PYt * 4 * P * stride;
 #pragma unroll
-        for (int a = 0; a < PY; ++a)
+        for (int a = 0; a < PYt; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
@@ -2004,7 +2041,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
     }
     float* o = U + t * C + c;
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
@@ -2030,11 +2067,11 @@ __global__ __launch_bounds__(256) void x3_wt_kernel(const float* __restrict__ w,
 }
 
 // X3O: V is written as split3 planes, transposed: uint16 [3][points][n'][k'].
-template <int NZ, bool X3O = false>
+template <int NZ, bool X3O = false, int NYT = WNY>
 __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restrict__ w, int Cin,
                                                           int Cout, int transpose_flip,
                                                           float* __restrict__ V) {
-    constexpr int P = ZT<NZ>::P;
+    constexpr int P = ZT<NZ>::P, PYt = ZT<NYT>::P;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t KN = (int64_t)Cin * Cout;
     if (i >= KN) return;
@@ -2075,16 +2112,16 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
         }
     if constexpr (X3O) {
         unsigned short* out = reinterpret_cast<unsigned short*>(V) + (int64_t)np_ * (KN / Np) + kp;
-        const int64_t pstride = (int64_t)PY * 4 * P * KN;
+        const int64_t pstride = (int64_t)PYt * 4 * P * KN;
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                float o[PY];
+                float o[PYt];
                 const float gy[3] = {t2[0][b][k], t2[1][b][k], t2[2][b][k]};
-                YT::g(gy, o);
+                ZT<NYT>::g(gy, o);
 #pragma unroll
-                for (int a = 0; a < PY; ++a) {
+                for (int a = 0; a < PYt; ++a) {
                     uint32_t hh, mm, ll;
                     split3(o[a], hh, mm, ll);
                     unsigned short* q = out + (int64_t)((a * 4 + b) * P + k) * KN;
@@ -2100,34 +2137,34 @@ __global__ __launch_bounds__(256) void wino_weight_kernel(const float* __restric
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            float o[PY];
+            float o[PYt];
             const float gy[3] = {t2[0][b][k], t2[1][b][k], t2[2][b][k]};
-            YT::g(gy, o);
+            ZT<NYT>::g(gy, o);
 #pragma unroll
-            for (int a = 0; a < PY; ++a) out[(int64_t)((a * 4 + b) * P + k) * KN] = o[a];
+            for (int a = 0; a < PYt; ++a) out[(int64_t)((a * 4 + b) * P + k) * KN] = o[a];
         }
 }
 
 // Y tile (2x2xNZ) = (A^T (x) A^T (x) Az^T) M[.][t][n], then the conv epilogue.
-template <int NZ, bool HALO>
+template <int NZ, bool HALO, int NYT>
 __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, const WinoGeom& g,
                                                  int N, const Epi& e);
-template <int NZ>
+template <int NZ, int NYT = WNY>
 __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, WinoGeom g,
                                                           int N, Epi e) {
-    wino_output_body<NZ, false>(Mt, g, N, e);
+    wino_output_body<NZ, false, NYT>(Mt, g, N, e);
 }
 // depth-slab data gradient: interior planes into e.y, halo planes into e.yh
-template <int NZ>
+template <int NZ, int NYT = WNY>
 __global__ __launch_bounds__(256) void wino_output_halo_kernel(const float* __restrict__ Mt, WinoGeom g,
                                                                int N, Epi e) {
-    wino_output_body<NZ, true>(Mt, g, N, e);
+    wino_output_body<NZ, true, NYT>(Mt, g, N, e);
 }
 
-template <int NZ, bool HALO>
+template <int NZ, bool HALO, int NYT>
 __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, const WinoGeom& g,
                                                  int N, const Epi& e) {
-    constexpr int P = ZT<NZ>::P;
+    constexpr int P = ZT<NZ>::P, PYt = ZT<NYT>::P;
     const int64_t i = wino_block(g) * blockDim.x + threadIdx.x;
     if (i >= g.T * N) return;
     const int n = (int)(i % N);
@@ -2136,41 +2173,41 @@ __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, c
     tile_coords(t, g, b, ty, tx, tz);
     const int64_t stride = g.T * N;
     const float* src = Mt + t * N + n;
-    float m[PY][4][P];
+    float m[PYt][4][P];
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
             for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
-    float r1[PY][4][NZ];
+    float r1[PYt][4][NZ];
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
-    float r2[PY][2][NZ];
+    float r2[PYt][2][NZ];
 #pragma unroll
-    for (int a = 0; a < PY; ++a)
+    for (int a = 0; a < PYt; ++a)
 #pragma unroll
         for (int k = 0; k < NZ; ++k)
             at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
-    float o[WNY][2][NZ];
+    float o[NYT][2][NZ];
 #pragma unroll
     for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
         for (int k = 0; k < NZ; ++k) {
-            float col[PY], oy[WNY];
+            float col[PYt], oy[NYT];
 #pragma unroll
-            for (int a = 0; a < PY; ++a) col[a] = r2[a][bb][k];
-            YT::at(col, oy);
+            for (int a = 0; a < PYt; ++a) col[a] = r2[a][bb][k];
+            ZT<NYT>::at(col, oy);
 #pragma unroll
-            for (int a = 0; a < WNY; ++a) o[a][bb][k] = oy[a];
+            for (int a = 0; a < NYT; ++a) o[a][bb][k] = oy[a];
         }
     const float bias = e.bias ? e.bias[n] : 0.0f;
     const float sc = e.scale ? e.scale[n] : 1.0f, sh = e.scale ? e.shift[n] : 0.0f;
 #pragma unroll
-    for (int a = 0; a < WNY; ++a) {
-        const int y = WNY * ty + a;
+    for (int a = 0; a < NYT; ++a) {
+        const int y = NYT * ty + a;
         if (y >= g.H) continue;
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
@@ -2213,10 +2250,10 @@ __device__ __forceinline__ void wino_output_body(const float* __restrict__ Mt, c
 // -- and per-block channel sums, one partial row per 256 (tile, channel)
 // pairs: N < 256 (256 % N == 0): the block's 256 / N tiles, row = block;
 // N % 256 == 0: one tile's 256 channels, row = tile.
-template <int NZ>
+template <int NZ, int NYT = WNY>
 __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __restrict__ Mt, WinoGeom g, int N,
                                                              Epi e) {
-    constexpr int P = ZT<NZ>::P;
+    constexpr int P = ZT<NZ>::P, PYt = ZT<NYT>::P;
     const int tid = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * 256 + tid;
     const bool valid = i < g.T * N;
@@ -2228,35 +2265,35 @@ __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __rest
         tile_coords(t, g, b, ty, tx, tz);
         const int64_t stride = g.T * N;
         const float* src = Mt + t * N + n;
-        float m[PY][4][P];
+        float m[PYt][4][P];
 #pragma unroll
-        for (int a = 0; a < PY; ++a)
+        for (int a = 0; a < PYt; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
                 for (int k = 0; k < P; ++k) m[a][bb][k] = wino_ld(src + (int64_t)((a * 4 + bb) * P + k) * stride);
-        float r1[PY][4][NZ];
+        float r1[PYt][4][NZ];
 #pragma unroll
-        for (int a = 0; a < PY; ++a)
+        for (int a = 0; a < PYt; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) ZT<NZ>::at(m[a][bb], r1[a][bb]);
-        float r2[PY][2][NZ];
+        float r2[PYt][2][NZ];
 #pragma unroll
-        for (int a = 0; a < PY; ++a)
+        for (int a = 0; a < PYt; ++a)
 #pragma unroll
             for (int k = 0; k < NZ; ++k)
                 at4(r1[a][0][k], r1[a][1][k], r1[a][2][k], r1[a][3][k], r2[a][0][k], r2[a][1][k]);
-        float o[WNY][2][NZ];
+        float o[NYT][2][NZ];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
             for (int k = 0; k < NZ; ++k) {
-                float col[PY], oy[WNY];
+                float col[PYt], oy[NYT];
 #pragma unroll
-                for (int a = 0; a < PY; ++a) col[a] = r2[a][bb][k];
-                YT::at(col, oy);
+                for (int a = 0; a < PYt; ++a) col[a] = r2[a][bb][k];
+                ZT<NYT>::at(col, oy);
 #pragma unroll
-                for (int a = 0; a < WNY; ++a) o[a][bb][k] = oy[a];
+                for (int a = 0; a < NYT; ++a) o[a][bb][k] = oy[a];
             }
         const float sc = e.fscale ? e.fscale[n] : 1.0f;
         const float mu = e.fz ? e.fmean[n] : 0.0f, rs = e.fz ? e.frstd[n] : 1.0f;
@@ -2264,16 +2301,16 @@ __global__ __launch_bounds__(256) void wino_output_bn_kernel(const float* __rest
         // issued after a store to a possibly aliasing address waits for it -- in two
         // halves, so only 2 x 2 x NZ x 3 loaded values are live beside o
         const int64_t ostr = (int64_t)g.D * e.ldy;             // output x step
-        const int64_t obase = ((((int64_t)b * g.H + WNY * ty) * g.W + 2 * tx) * g.D + NZ * tz) * e.ldy + n;
+        const int64_t obase = ((((int64_t)b * g.H + NYT * ty) * g.W + 2 * tx) * g.D + NZ * tz) * e.ldy + n;
 #pragma unroll
-        for (int a = 0; a < WNY; ++a) {
+        for (int a = 0; a < NYT; ++a) {
             float ov[2][NZ], yv[2][NZ], zv[2][NZ];
             bool in[2][NZ];
 #pragma unroll
             for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
                 for (int k = 0; k < NZ; ++k) {
-                    in[bb][k] = WNY * ty + a < g.H && 2 * tx + bb < g.W && NZ * tz + k < g.D;
+                    in[bb][k] = NYT * ty + a < g.H && 2 * tx + bb < g.W && NZ * tz + k < g.D;
                     const int64_t off = obase + (a * (int64_t)g.W + bb) * ostr + k * e.ldy;
                     ov[bb][k] = in[bb][k] && e.accumulate ? e.y[off] : 0.0f;
                     yv[bb][k] = in[bb][k] && e.frelu ? e.fy[off] : 1.0f;
@@ -2651,22 +2688,15 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                     for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PLB + off);
                 }
                 // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
+#if M3D_X3_DBG == 1   // timing probe: no MFMA (fragments still consumed)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-#if M3D_X3_DBG == 1   // timing probe: no MFMA (fragments still consumed)
+                    for (int j = 0; j < TN; ++j)
                         acc[i][j][0] += (float)(af[i][0][0] ^ af[i][1][1] ^ af[i][2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
 #else
-                        floatx16 c = acc[i][j];
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], c, 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], c, 0, 0, 0);
+                x3_mac_tiles<TM, TN, X3ACC_GEMM>(acc, af, bfr);
 #endif
-                    }
             }
             if constexpr (NBUF == 2) {
                 // the other stage was last read in iteration kt-1, before its closing barrier
@@ -2805,13 +2835,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
                     continue;
                 }
-                floatx16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
             }
         }
     }
@@ -2981,13 +3005,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                floatx16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
             }
         }
 #if M3D_TUNE_X3AF & 2
@@ -3136,13 +3154,7 @@ __global__ __launch_bounds__(256, 2) void x3_gemm_af128_kernel(X3G g) {
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G3_PLA + off);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                floatx16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[j][0], c, 0, 0, 0);
+                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
             }
         }
     };
@@ -3208,15 +3220,27 @@ static int wino_dgrad_nz() {
     static constexpr int v = M3D_TUNE_WINO_DGRAD_NZ;   // 0: the forward's tile
     return v ? v : wino_nz();
 }
-static int wino_points(int nz) { return PY * 4 * (nz + 2); }
+// The data gradient's y tile (round 5): F(2,3) along y by default, i.e.
+// F(2x2x4) tiles, while the forward and the weight gradient keep F(4x2x4).
+// The data gradients carry the step's gradient error (every layer's dx feeds
+// all earlier layers): F(4,3) on two axes amplifies the point GEMMs' fp32
+// accumulation error ~4x over F(2x2x4) (scripts/wino_stage_error.py), and the
+// 128^3 step's gradient median against float64 was 6.6e-6 with F(4x2x4) data
+// gradients, 2.3e-6 with F(2x2x4) (scripts/grad_table.py, gpurun_out/r05grad).
+// M3D_TUNE_WINO_DGRAD_NY=0: the forward's tile.
+static int wino_dgrad_ny() {
+    static constexpr int v = M3D_TUNE_WINO_DGRAD_NY;
+    return v ? v : WNY;
+}
+static int wino_points(int nz, int ny = WNY) { return (ny + 2) * 4 * (nz + 2); }
 static int wino_points() { return wino_points(wino_nz()); }
 
 static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz,
-                          int nz = -1) {
+                          int nz = -1, int ny = WNY) {
     WinoGeom g;
     if (nz < 0) nz = wino_nz();
     g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
-    g.TY = (int)((H + WNY - 1) / WNY); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
+    g.TY = (int)((H + ny - 1) / ny); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
     g.T = B * g.TY * g.TX * g.TZ;
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
@@ -4626,15 +4650,19 @@ static bool wino_per_item(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD
 extern "C" int32_t m3d_conv3d_wino_tile_z(void) { return wino_nz(); }
 extern "C" int32_t m3d_conv3d_wino_wgrad_tile_z(void) { return wino_wgrad_nz(); }
 extern "C" int32_t m3d_conv3d_wino_tile_y(void) { return WNY; }
+extern "C" int32_t m3d_conv3d_wino_dgrad_tile_y(void) { return wino_dgrad_ny(); }
+extern "C" int32_t m3d_conv3d_wino_dgrad_tile_z(void) { return wino_dgrad_nz(); }
 
 extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D,
                                                   int64_t OD, int64_t Cin, int64_t Cout) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     if (wino_per_item(B, H, W, D, OD, Cin, Cout)) B = 1;     // run one batch item at a time
     size_t best = 0;
-    for (int nz : {wino_nz(), wino_wgrad_nz(), wino_dgrad_nz()}) {
-        const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz);
-        const size_t P = (size_t)wino_points(nz);
+    const int tiles[3][2] = {{wino_nz(), WNY}, {wino_wgrad_nz(), WNY}, {wino_dgrad_nz(), wino_dgrad_ny()}};
+    for (const auto& zy : tiles) {
+        const int nz = zy[0], ny = zy[1];
+        const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz, ny);
+        const size_t P = (size_t)wino_points(nz, ny);
         const size_t eb = gemm_x3_env() ? 6 : 4;      // X3: V and U hold three bf16 planes
         const size_t wt = gemm_x3_env() ? al(sizeof(float) * 27 * (size_t)Cin * Cout) : 0;
         // U (eb bytes / element) then M (fp32), in either role order (fwd: U over
@@ -4649,9 +4677,9 @@ extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t 
 
 struct WinoWs { float *V, *U, *M, *WT; };
 // [WT: X3 only, the transposed kernel][V][U][M]
-static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, int nz = -1) {
+static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, int nz = -1, int ny = WNY) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t P = (size_t)wino_points(nz < 0 ? wino_nz() : nz);
+    const size_t P = (size_t)wino_points(nz < 0 ? wino_nz() : nz, ny);
     char* p = (char*)ws;
     WinoWs w;
     w.WT = (float*)p;
@@ -5056,8 +5084,7 @@ extern "C" int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int6
         return einval("conv3d winograd bwd-data (fused BN backward): Cin must divide 256 or be a multiple of it");
     if (wino_per_item(B, H, W, D, OD, Cin, Cout))
         return einval("conv3d winograd bwd-data (fused BN backward): batch past the 32-bit operand bound");
-    const int nz = wino_dgrad_nz();
-    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, wino_dgrad_nz(), wino_dgrad_ny());
     const int64_t rows = Cin % 256 == 0 ? g.T : (g.T * Cin + 255) / 256;
     Epi e{};
     int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
@@ -5071,21 +5098,51 @@ extern "C" int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int6
 // the data-gradient output transform: dx over the (halo-extended) grid, or,
 // for a depth slab with dx_halo, interior planes into dx (depth dl) and the
 // neighbours' planes into dx_halo [B][H][W][2][C]
+template <int NZ, int NY>
 static void wino_dgrad_out(const float* Mt, const WinoGeom& g, int C, float* dx, int accumulate,
-                           float* dx_halo, int hlo, int dl, int nz, hipStream_t hs, const Epi* fb = nullptr) {
+                           float* dx_halo, int hlo, int dl, hipStream_t hs, const Epi* fb) {
     Epi o{};
     if (fb) o = *fb;                 // the fused BN backward's fields
     o.y = dx; o.ldy = C; o.accumulate = accumulate;
+    const dim3 grid(grid_for(g.T * C, 256));
     if (fb) {
-        WINO_LAUNCH_NZ(nz, wino_output_bn_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+        hipLaunchKernelGGL((wino_output_bn_kernel<NZ, NY>), grid, dim3(256), 0, hs, Mt, g, C, o);
         return;
     }
     if (dx_halo) {
         o.yh = dx_halo; o.hlo = hlo; o.dl = dl;
-        WINO_LAUNCH_NZ(nz, wino_output_halo_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+        hipLaunchKernelGGL((wino_output_halo_kernel<NZ, NY>), grid, dim3(256), 0, hs, Mt, g, C, o);
         return;
     }
-    WINO_LAUNCH_NZ(nz, wino_output_kernel, dim3(grid_for(g.T * C, 256)), dim3(256), 0, hs, Mt, g, C, o);
+    hipLaunchKernelGGL((wino_output_kernel<NZ, NY>), grid, dim3(256), 0, hs, Mt, g, C, o);
+}
+
+// the data gradient's launches on F(NY x 2 x NZ) tiles (geometry g, workspace ws)
+template <int NZ, int NY>
+static void bwd_data_wino_launch(const float* dz, const float* w, const WinoGeom& g, const WinoWs& ws, int Cin,
+                                 int Cout, float* dx, int32_t accumulate, float* dx_halo, int hlo, int dl,
+                                 bool v_ready, const Epi* fb, hipStream_t hs) {
+    const int P = wino_points(NZ, NY);
+    const dim3 wgrid(grid_for((int64_t)Cin * Cout, 256)), igrid(grid_for(g.T * Cout, 256));
+    if (gemm_x3_env()) {
+        if (!v_ready)
+            hipLaunchKernelGGL((wino_weight_kernel<NZ, true, NY>), wgrid, dim3(256), 0, hs, w, Cin, Cout, 1, ws.V);
+        const bool af32 = x3_af32_env();
+        if (af32)
+            hipLaunchKernelGGL((wino_input_kernel<NZ, false, false, NY>), igrid, dim3(256), 0, hs, dz, g, Cout, ws.U);
+        else
+            hipLaunchKernelGGL((wino_input_kernel<NZ, true, false, NY>), igrid, dim3(256), 0, hs, dz, g, Cout, ws.U);
+        wino_gemm_x3(ws, g.T, Cout, Cin, P, hs, af32);
+    } else {
+        hipLaunchKernelGGL((wino_weight_kernel<NZ, false, NY>), wgrid, dim3(256), 0, hs, w, Cin, Cout, 1, ws.V);
+        hipLaunchKernelGGL((wino_input_kernel<NZ, false, false, NY>), igrid, dim3(256), 0, hs, dz, g, Cout, ws.U);
+        ConvP p = wino_gemm_p(ws.U, g.T, Cout, ws.V, Cin);
+        Epi e{};
+        e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
+        e.ysy = e.ysx = e.ysz = 1;
+        dispatch_gemm<false, true>(p, e, hs, P);
+    }
+    wino_dgrad_out<NZ, NY>(ws.M, g, Cin, dx, accumulate, dx_halo, hlo, dl, hs, fb);
 }
 
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
@@ -5106,35 +5163,19 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
         }
         return M3D_OK;
     }
-    const int nz = wino_dgrad_nz();
-    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz);
+    const int nz = wino_dgrad_nz(), ny = wino_dgrad_ny();
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz, ny);
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
-    WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz);
-    if (gemm_x3_env()) {
-        if (!v_ready)
-            WINO_LAUNCH_NZ_X3(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
-                              (int)Cin, (int)Cout, 1, ws.V);
-        const bool af32 = x3_af32_env();
-        if (af32)
-            WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
-                           (int)Cout, ws.U);
-        else
-            WINO_LAUNCH_NZ_X3(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
-                              (int)Cout, ws.U);
-        wino_gemm_x3(ws, g.T, (int)Cout, (int)Cin, wino_points(nz), hs, af32);
-        wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs, fb);
-        return check_launch("conv3d winograd bwd-data (x3)");
-    }
-    WINO_LAUNCH_NZ(nz, wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, hs, w,
-                       (int)Cin, (int)Cout, 1, ws.V);
-    WINO_LAUNCH_NZ(nz, wino_input_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, hs, dz, g,
-                       (int)Cout, ws.U);
-    ConvP p = wino_gemm_p(ws.U, g.T, (int)Cout, ws.V, (int)Cin);
-    Epi e{};
-    e.y = ws.M; e.ldy = Cin; e.simple = 1; e.YH = 1; e.YW = 1; e.YD = (int)g.T;
-    e.ysy = e.ysx = e.ysz = 1;
-    dispatch_gemm<false, true>(p, e, hs, wino_points(nz));
-    wino_dgrad_out(ws.M, g, (int)Cin, dx, accumulate, dx_halo, hlo, (int)OD, nz, hs, fb);
+    const WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz, ny);
+    const int ci = (int)Cin, co = (int)Cout, dl = (int)OD;
+    if (nz == 4 && ny == 4)
+        bwd_data_wino_launch<4, 4>(dz, w, g, ws, ci, co, dx, accumulate, dx_halo, hlo, dl, v_ready, fb, hs);
+    else if (nz == 4)
+        bwd_data_wino_launch<4, 2>(dz, w, g, ws, ci, co, dx, accumulate, dx_halo, hlo, dl, v_ready, fb, hs);
+    else if (ny == 4)
+        bwd_data_wino_launch<2, 4>(dz, w, g, ws, ci, co, dx, accumulate, dx_halo, hlo, dl, v_ready, fb, hs);
+    else
+        bwd_data_wino_launch<2, 2>(dz, w, g, ws, ci, co, dx, accumulate, dx_halo, hlo, dl, v_ready, fb, hs);
     return check_launch("conv3d winograd bwd-data");
 }
 

@@ -204,9 +204,11 @@ def _wgrad1_x3(geo, cin, cout, in_sp):
             and tuple(geo.out) == tuple(in_sp) and cin % 4 == 0 and cout >= 65)
 
 
-def _wino_exec(B, OH, OW, OD, cin, cout, nz):
-    """MFMA FLOPs of the Winograd point GEMMs, F(ny x 2 x nz): (ny+2)*4*(nz+2) points."""
-    ny = int(_L().m3d_conv3d_wino_tile_y())
+def _wino_exec(B, OH, OW, OD, cin, cout, nz, ny=None):
+    """MFMA FLOPs of the Winograd point GEMMs, F(ny x 2 x nz): (ny+2)*4*(nz+2)
+    points (ny: the forward's y tile unless given)."""
+    if ny is None:
+        ny = int(_L().m3d_conv3d_wino_tile_y())
     tiles = B * -(-OH // ny) * -(-OW // 2) * -(-OD // nz)
     return 2.0 * (ny + 2) * 4 * (nz + 2) * tiles * cin * cout
 
@@ -824,7 +826,8 @@ class _ConvBNAct(torch.autograd.Function):
                                                            stream()), "conv3d_bwd_data_wino")
                     _shared_wino_release(ctx.wshare)
                 if logging:
-                    _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_tile_z())),
+                    _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_dgrad_tile_z()),
+                                                          int(L.m3d_conv3d_wino_dgrad_tile_y())),
                          4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel), "bwd_data", ctx.name,
                          td, "x3")
                 dx = _link_park(ctx.link, dx, acc)

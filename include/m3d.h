@@ -359,6 +359,11 @@ int32_t m3d_conv3d_wino_tile_z(void);
  * transformed input the forward keeps -- m3d_conv3d_wino_u_bytes > 0; 2: F(2x2x2)). */
 int32_t m3d_conv3d_wino_wgrad_tile_z(void);
 int32_t m3d_conv3d_wino_tile_y(void);   /* output tile rows along y (2: F(2,3), 4: F(4,3)) */
+/* the data gradient's tile (m3d_conv3d_bwd_data_wino*): F(2,3) along y by
+ * default (F(2x2x4)) beside the forward's F(4x2x4) -- the accuracy of the
+ * gradients every earlier layer receives */
+int32_t m3d_conv3d_wino_dgrad_tile_y(void);
+int32_t m3d_conv3d_wino_dgrad_tile_z(void);
 size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin);
 int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
                              const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,

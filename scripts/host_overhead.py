@@ -43,3 +43,20 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f"host enqueue {(t1 - t0) / N * 1e3:.2f} ms/step, wall {(t2 - t0) / N * 1e3:.2f} ms/step")
+# where the host's enqueue time goes: cProfile over N more steps (the GPU queue
+# stays full, so the profile sees the host's own work, plus any blocking call)
+import cProfile  # noqa: E402
+import io  # noqa: E402
+import pstats  # noqa: E402
+
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(N):
+    model.train_step(image, targets)
+pr.disable()
+torch.cuda.synchronize()
+for key in ("tottime", "cumulative"):
+    buf = io.StringIO()
+    pstats.Stats(pr, stream=buf).sort_stats(key).print_stats(35)
+    print(f"--- cProfile over {N} steps, by {key} (seconds are for all {N} steps)")
+    print("\n".join(l for l in buf.getvalue().splitlines() if l.strip())[:9000])

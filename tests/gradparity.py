@@ -27,13 +27,17 @@ def ref_grads(model, image, match, bbox, dtype, relu_masks=None):
     return float(rlc), float(rlb), {k: (v.grad.clone() if v.grad is not None else None) for k, v in ref.p.items()}
 
 
+# the median tensor's bar (round 5: 1e-5 -> 3e-6 with the F(2x2x4) data gradients)
+MEDIAN_BAR = 3e-6
+
+
 def grad_parity(model, g64, g32, label):
     """Per weight tensor: GPU gradient vs the float64 restatement that took the
     GPU forward's ReLU branches.  Bars: every tensor within the north-star
     1e-4 of its scale -- or, where the CPU fp32 restatement on the same
     branches is itself further off (the stem conv's gradient: 3^3 max-pool
     ties fp32 and fp64 break differently), within 2x the CPU fp32 error --
-    and the median tensor below 1e-5."""
+    and the median tensor below MEDIAN_BAR."""
     rows = []
     for p in model.store.params:
         g_ref = g64[p.name]
@@ -43,8 +47,11 @@ def grad_parity(model, g64, g32, label):
                      p.name))
     rows.sort(reverse=True)
     med = float(np.median([r[0] for r in rows]))
-    print(f"{label} gradients: {len(rows)} tensors, GPU median {med:.2e}, worst {rows[:3]}", flush=True)
-    assert med < 1e-5, med
+    med32 = float(np.median([r[1] for r in rows]))
+    over10 = sum(r[0] > 10.0 * r[1] for r in rows)
+    print(f"{label} gradients: {len(rows)} tensors, GPU median {med:.2e} (CPU fp32 on the same branches "
+          f"{med32:.2e}), {over10} tensors above 10x their CPU fp32 error, worst {rows[:3]}", flush=True)
+    assert med < MEDIAN_BAR, med
     bad = [r for r in rows if r[0] > max(1e-4, 2.0 * r[1])]
     assert not bad, bad[:5]
 

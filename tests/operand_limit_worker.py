@@ -87,6 +87,16 @@ def main():
                                                  C, hdw.data_ptr(), wsh.data_ptr(), nbh, s), "wino bwd_weight halo")
     r.update(h_y=hy, h_dx=hdx, h_dhalo=hdh, h_dw=hdw)
     torch.cuda.synchronize()
+    # float64 weight gradients (the anchor of the dw comparisons)
+    def wgrad64(xin, dzz, pad):
+        xi = xin.cpu().double().permute(0, 4, 1, 2, 3)
+        gi = dzz.cpu().double().permute(0, 4, 1, 2, 3)
+        gw = torch.nn.grad.conv3d_weight(xi, (C, C, 3, 3, 3), gi, padding=pad)
+        return gw.permute(2, 3, 4, 1, 0).contiguous()
+    r["ref_d3_dw"] = wgrad64(x, dz, 1)
+    r["ref_w_dw"] = r["ref_d3_dw"]
+    x_ext = torch.cat([halo[:, :, :, 0:1], x, halo[:, :, :, 1:2]], dim=3)
+    r["ref_h_dw"] = wgrad64(x_ext, dz, (1, 1, 0))
     np.savez(out, ws_bytes=np.array([nb, nbh]), **{k: v.cpu().numpy() for k, v in r.items()})
 
 

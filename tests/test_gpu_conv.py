@@ -329,8 +329,10 @@ def test_batch_items_past_operand_bound(tmp_path):
     32-bit operand bound runs one batch item at a time (M3D_OPERAND_LIMIT
     lowers the 4 GiB bound to 500 KB so a 3 x 262 KB batch crosses it): the
     forward and data gradients are bit-identical to the whole-batch launch,
-    the weight gradients (summed per item) within fp32 reassociation, and the
-    Winograd workspace shrinks to one item's."""
+    the weight gradients (summed per item) both within 1e-5 of the float64
+    weight gradient (of its largest element; 2e-5 for the Winograd F(4x2x4)
+    weight gradients), and the Winograd workspace
+    shrinks to one item's."""
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(__file__), "operand_limit_worker.py")
@@ -347,14 +349,19 @@ def test_batch_items_past_operand_bound(tmp_path):
     a, b = res["whole"], res["items"]
     assert (b["ws_bytes"] < a["ws_bytes"]).all()
     for k in a.files:
-        if k == "ws_bytes":
+        if k == "ws_bytes" or k.startswith("ref_"):
             continue
         if k.endswith("dw"):
-            # fp32 reassociation of the per-item sums; the Winograd weight gradient's
-            # G^T rows (4, 8/3, ... for F(4,3) axes) amplify it: 4e-5 there
-            scale = float(np.abs(a[k]).max())
-            tol = 4e-5 if k.startswith("w") else 1e-5
-            assert float(np.abs(a[k] - b[k]).max()) <= tol * scale, k
+            # the per-item sums reassociate the fp32 tile sums: each form against
+            # float64.  The Winograd weight gradients (F(4x2x4) tiles, w_ / h_) pass
+            # the point GEMMs' fp32 tile sums through G^T, whose F(4,3) rows (4, 8/3)
+            # amplify their rounding: measured 1.35e-5 here (C = 32, 192 tiles)
+            ref = a["ref_" + k]
+            scale = float(np.abs(ref).max())
+            tol = 2e-5 if k[0] in "wh" else 1e-5
+            for tag, got in (("whole", a[k]), ("items", b[k])):
+                err = float(np.abs(got - ref).max()) / scale
+                assert err <= tol, (k, tag, err)
         else:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
