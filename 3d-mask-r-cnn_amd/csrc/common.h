@@ -169,6 +169,10 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3_ACC
 #define M3D_TUNE_X3_ACC 1
 #endif
+// 1x1x1 conv epilogue inside x3_gemm256_af_kernel (1) or as a second pass (0)
+#ifndef M3D_TUNE_CONV1_EPI
+#define M3D_TUNE_CONV1_EPI 1
+#endif
 #ifndef M3D_TUNE_WINO_NY
 #define M3D_TUNE_WINO_NY 4
 #endif

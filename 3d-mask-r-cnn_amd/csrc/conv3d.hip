@@ -228,7 +228,9 @@ __device__ __forceinline__ void x3_mac(floatx16& acc, const bf16x8& ah, const bf
 // tile q-1's VALU add, a scheduling barrier per tile keeps two step partials
 // live (without it the compiler runs every tile's chain first and holds all
 // their partials: spills in the 128x128 kernels).
-template <int TM, int TN, int X3ACC>
+// LAG false: each tile's partial added right behind its own chain (one partial
+// live; the add waits for the chain's last MFMA -- for kernels at the register limit)
+template <int TM, int TN, int X3ACC, bool LAG = true>
 __device__ __forceinline__ void x3_mac_tiles(floatx16 (&acc)[TM][TN], const bf16x8 (&af)[TM][3],
                                              const bf16x8 (&bf)[TN][3]) {
     if constexpr (X3ACC == 1) {
@@ -242,11 +244,15 @@ __device__ __forceinline__ void x3_mac_tiles(floatx16 (&acc)[TM][TN], const bf16
             t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bf[j][0], t, 0, 0, 0);
             t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][1], t, 0, 0, 0);
             t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][0], t, 0, 0, 0);
-            if (q > 0) acc[(q - 1) / TN][(q - 1) % TN] += pend;
-            pend = t;
+            if constexpr (LAG) {
+                if (q > 0) acc[(q - 1) / TN][(q - 1) % TN] += pend;
+                pend = t;
+            } else {
+                acc[i][j] += t;
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
-        acc[TM - 1][TN - 1] += pend;
+        if constexpr (LAG) acc[TM - 1][TN - 1] += pend;
     } else {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -431,7 +437,7 @@ __device__ __forceinline__ void epi_store4_pre(const ConvP& p, const Epi& e, int
 // spill at 3, and must not touch the register budget of the other forms)
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false,
           bool X3 = false, bool FBN = false>
-__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) void conv_gemm_kernel(ConvP p,
+__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && X3ACC_CONV) ? 3 : 2)) void conv_gemm_kernel(ConvP p,
                                                                                                   Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) vo
                     for (int pl = 0; pl < 3; ++pl)
                         bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * (BN * BK * 2) + off);
                 }
-                x3_mac_tiles<TM, TN, X3ACC_CONV>(acc, af, bfr);
+                x3_mac_tiles<TM, TN, X3ACC_CONV, false>(acc, af, bfr);
             }
         } else {
         const float* As = smem + buf * (A_SZ + B_SZ);
@@ -2536,6 +2542,20 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
 // chunks in flight in registers; 6 bf16 MFMAs per product (see split3).
 // PERSIST: a resident grid loops over all tiles of all batches (XCD-
 // contiguous order, as conv_gemm_kernel).
+// conv epilogue applied by x3_gemm256_af_kernel to its tile (a 1x1x1 conv's
+// GEMM, nbatch 1, rows = voxels, ld = N): epi_store4's operations per element
+// in its order -- + bias, z store, * scale + shift, + same-shape residual,
+// activation -- so the fused form is bit-identical to the GEMM + epilogue pass
+struct X3Epi {
+    const float* bias;
+    const float* scale;
+    const float* shift;
+    const float* res;          // [M][N] (res_mode 1) or nullptr
+    float* z;                  // pre-BN output or nullptr
+    int act;                   // act() code
+    int on;                    // 0: plain C store
+};
+
 struct X3G {
     const unsigned short* a;
     const float* af;           // AF32: A as fp32 [batch][M][K], split in the LDS store
@@ -2545,6 +2565,7 @@ struct X3G {
     int K, N, nbatch;
     int64_t psa, psb;          // plane strides (elements)
     int64_t bsa, bsb, bsc;     // batch strides (elements)
+    X3Epi ep;                  // x3_gemm256_af_kernel only
 };
 
 // byte offset of (row, chunk) in a 16-deep X3 plane: 32-B rows of two 16-B
@@ -3023,6 +3044,45 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
+    if (g.ep.on) {
+        // the fused conv epilogue (X3Epi): per accumulator tile its 16 residual
+        // values are loaded before its first store; rows past M read zeros and
+        // their stores are dropped (the descriptors' range)
+        const X3Epi& E = g.ep;
+        const uint64_t rbytes = (uint64_t)(g.M - m0) * g.N * 4;
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(E.res ? E.res + m0 * g.N : g.c, E.res ? rbytes : 0);
+        const __amdgpu_buffer_rsrc_t rz = make_rsrc(E.z ? E.z + m0 * g.N : g.c, E.z ? rbytes : 0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = (int)n0 + wn * 64 + j * 32 + l32;
+            const float bias = E.bias ? E.bias[col] : 0.0f;
+            const float sc = E.scale ? E.scale[col] : 1.0f, sh = E.scale ? E.shift[col] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float rv[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    rv[r] = E.res ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                        rr, (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u), 0, 0))
+                                  : 0.0f;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int off = (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u);
+                    float v = acc[i][j][r];
+                    if (E.bias) v += bias;
+                    if (E.z) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rz, off, 0, 0);
+                    if (E.scale) v = v * sc + sh;
+                    if (E.res) v += rv[r];
+                    if (E.act) v = act(E.act, v);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, off, 0, 0);
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -4893,9 +4953,17 @@ static int conv1_x3_launch(const float* a, const uint16_t* planes, int64_t M, in
     q.psb = K * N;
     const int64_t t256 = ((M + 255) / 256) * (N / 256);
     const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
+    // the epilogue in the GEMM's own stores when it is element-local (same-shape
+    // residual); the FPN's upsampled residual (res_mode 2) takes the second pass
+    const bool fuse = M3D_TUNE_CONV1_EPI && e && e->res_mode <= 1 && !e->accumulate && e->split <= 0 &&
+                      e->ldy == N && e->simple;
+    if (fuse) {
+        q.ep.bias = e->bias; q.ep.scale = e->scale; q.ep.shift = e->shift;
+        q.ep.res = e->res_mode == 1 ? e->res : nullptr; q.ep.z = e->z; q.ep.act = e->relu; q.ep.on = 1;
+    }
     hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
     int rc = check_launch("x3_gemm256_af_kernel(conv1)");
-    if (rc || !e) return rc;
+    if (rc || !e || fuse) return rc;
     ConvP p{};
     p.M = M; p.N = (int)N; p.K = (int)K; p.OH = (int)H; p.OW = (int)W; p.OD = (int)D;
     hipLaunchKernelGGL(splitk_epi_kernel, dim3(grid_for(M * N / 4, 256)), dim3(256), 0, s, out, 1, p, *e);

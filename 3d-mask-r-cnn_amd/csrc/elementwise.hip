@@ -959,6 +959,28 @@ __global__ void bn_affine_kernel(const float* __restrict__ gamma, const float* _
 }
 }  // namespace m3d
 
+namespace m3d {
+// one grid row per BN layer (bn_affine_kernel's expressions)
+__global__ void bn_affine_batched_kernel(const m3d_bn_affine_item_t* __restrict__ items) {
+    const m3d_bn_affine_item_t it = items[blockIdx.y];
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= it.C) return;
+    const float r = 1.0f / sqrtf(it.var[c] + it.eps);
+    const float sc = it.gamma[c] * r;
+    it.out[c] = r;
+    it.out[it.C + c] = sc;
+    it.out[2 * it.C + c] = it.beta[c] - it.mean[c] * sc;
+}
+}  // namespace m3d
+
+extern "C" int m3d_bn_affine_batched(const m3d_bn_affine_item_t* items, int32_t n, int64_t max_c,
+                                     m3d_stream_t s) {
+    if (n <= 0 || n > 65535 || max_c <= 0 || !items) return einval("bn_affine_batched: bad arguments");
+    hipLaunchKernelGGL(bn_affine_batched_kernel, dim3(grid_for(max_c, 256), (unsigned)n), dim3(256), 0, st(s),
+                       items);
+    return check_launch("bn_affine_batched_kernel");
+}
+
 extern "C" int m3d_bn_affine(const float* gamma, const float* beta, const float* mean,
                              const float* var, float eps, int64_t C, float* scale, float* shift,
                              float* rstd, m3d_stream_t s) {

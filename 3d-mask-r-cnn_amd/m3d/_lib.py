@@ -170,6 +170,7 @@ _SIGS = {
     "m3d_subsample221_fwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_subsample221_bwd": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_bn_affine": [c_p, c_p, c_p, c_p, c_f, c_i64, c_p, c_p, c_p, c_p],
+    "m3d_bn_affine_batched": [c_p, c_i32, c_i64, c_p],
     "m3d_bn_act_bwd_workspace_bytes": [c_i64, c_i64],
     "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
                        c_p, c_p, c_p, c_sz, c_p],
@@ -225,12 +226,23 @@ DET_ENTRY_POINTS = ("m3d_conv3d_bwd_weight", "m3d_conv3d_bwd_weight_halo", "m3d_
                     "m3d_sgd_keras", "m3d_adam_keras", "m3d_adadelta_keras")
 
 
+class BnAffineItem(ctypes.Structure):
+    """m3d_bn_affine_item_t (include/m3d.h)."""
+    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("mean", ctypes.c_void_p),
+                ("var", ctypes.c_void_p), ("out", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("C", ctypes.c_int32)]
+
+
 class _Lib:
     """The loaded CDLL; the DET_ENTRY_POINTS called without their det argument
     get det_arg() inserted before the stream."""
 
     def __init__(self, cdll):
         self._cdll = cdll
+        # every signed entry point bound on the instance: an attribute lookup per
+        # launch is then a dict hit, not a __getattr__ round trip (host enqueue)
+        for name in _SIGS:
+            setattr(self, name, getattr(cdll, name))
         for name in DET_ENTRY_POINTS:
             fn = getattr(cdll, name)
             n = len(fn.argtypes)
@@ -261,7 +273,17 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
+try:                   # the raw current stream without a torch.cuda.Stream object per call
+    _raw_stream = torch._C._cuda_getCurrentRawStream
+    _cur_device = torch._C._cuda_getDevice
+except AttributeError:  # pragma: no cover - other torch builds
+    _raw_stream = None
+
+
 def stream() -> int:
+    """The current HIP stream of the current device (an int handle)."""
+    if _raw_stream is not None:
+        return _raw_stream(_cur_device())
     return torch.cuda.current_stream().cuda_stream
 
 

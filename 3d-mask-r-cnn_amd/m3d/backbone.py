@@ -77,6 +77,7 @@ class ResNet3D:
         assert architecture in ("resnet50", "resnet101")
         if train_bn:
             raise NotImplementedError("TRAIN_BN=True (batch-statistics BN) is not on the hot path")
+        self.store = store
         self.stem = _Unit(store, "conv1", "bn_conv1", (7, 7, 7), 1, 64, (2, 2, 1), 3)
         s = (2, 2, 1)
         self.stages = []
@@ -98,6 +99,15 @@ class ResNet3D:
     def __call__(self, image):
         self.links = []                 # GradLinks of this forward (checked by check_links)
         self.fuses = []                 # BNFuse records of this forward (checked by check_fuses)
+        # every BN layer's affine in one launch for this forward (ParamStore.bn_affine_refresh)
+        self.store.bn_affine_refresh()
+        self.store.bn_aff_live = True
+        try:
+            return self._forward(image)
+        finally:
+            self.store.bn_aff_live = False
+
+    def _forward(self, image):
         x = self.stem(image, relu=True, need_dx=False)
         c1 = x = max_pool3d(x, (3, 3, 3), (2, 2, 1), "same")
         outs = [c1]

@@ -581,11 +581,13 @@ class _ConvBNAct(torch.autograd.Function):
         z = None
         scale = shift = None
         if bn is not None:
-            gamma, beta, mean, var, eps = bn
-            aff = torch.empty((3, Cout), device=x.device, dtype=torch.float32)
+            gamma, beta, mean, var, eps = bn[:5]
+            aff = bn[5] if len(bn) > 5 else None
+            if aff is None:
+                aff = torch.empty((3, Cout), device=x.device, dtype=torch.float32)
+                check(_L().m3d_bn_affine(ptr(gamma), ptr(beta), ptr(mean), ptr(var), float(eps), Cout,
+                                         ptr(aff[1]), ptr(aff[2]), ptr(aff[0]), stream()), "bn_affine")
             rstd, scale, shift = aff[0], aff[1], aff[2]
-            check(_L().m3d_bn_affine(ptr(gamma), ptr(beta), ptr(mean), ptr(var), float(eps), Cout,
-                                     ptr(scale), ptr(shift), ptr(rstd), stream()), "bn_affine")
             if grads is not None and grads.get("gamma") is not None:
                 z = torch.empty_like(y)
             ctx.bn = (mean, rstd, scale)
@@ -967,7 +969,10 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         grads = dict(grads, _hook=(GRAD_HOOK, key))
     bnt = None
     if bn is not None:
-        bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps)
+        # the model forward's batched affine (ParamStore.bn_affine_refresh) when current
+        st = getattr(bn, "store", None)
+        aff = bn.aff if st is not None and st.bn_aff_live else None
+        bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps, aff)
     if residual is not None:
         residual = residual.contiguous()
     halo = None

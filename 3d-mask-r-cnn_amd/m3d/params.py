@@ -46,6 +46,8 @@ class BNLayer:
 
     def __init__(self, store, name, c, eps=1e-3):
         self.name, self.c, self.eps = name, c, eps
+        self.store = store
+        self.aff = None            # [3, c] (rstd, scale, shift) of ParamStore.bn_affine_refresh
         self.gamma = store.add(f"{name}/gamma:0", (c,), "ones", False)
         self.beta = store.add(f"{name}/beta:0", (c,), "zeros", False)
         self.moving_mean = None
@@ -57,6 +59,10 @@ class ParamStore:
     def __init__(self):
         self.params: list[Param] = []
         self.bns: list[BNLayer] = []
+        # every BN layer's affine from one launch (bn_affine_refresh); the views
+        # bn.aff are current while bn_aff_live is set (a model forward's span)
+        self._bn_items = self._bn_key = None
+        self.bn_aff_live = False
         self.by_name = {}
         self.flat = self.grad_flat = self.moments = None
 
@@ -116,6 +122,36 @@ class ParamStore:
 
     def zero_grad(self):
         self.grad_flat.zero_()
+
+    def bn_affine_refresh(self):
+        """(rstd, scale, shift) of every BN layer into bn.aff by ONE launch of
+        m3d_bn_affine_batched on the current stream (was one m3d_bn_affine per
+        BN conv unit per forward).  The descriptor table is built once and
+        rebuilt if any parameter / statistics buffer moved."""
+        from . import _lib
+        if not self.bns:
+            return
+        key = tuple((bn.gamma.data.data_ptr(), bn.beta.data.data_ptr(), bn.moving_mean.data_ptr(),
+                     bn.moving_variance.data_ptr()) for bn in self.bns)
+        if self._bn_items is None or key != self._bn_key:
+            dev = self.bns[0].gamma.data.device
+            total = sum(3 * bn.c for bn in self.bns)
+            self._bn_out = torch.empty(total, dtype=torch.float32, device=dev)
+            items = (_lib.BnAffineItem * len(self.bns))()
+            off = 0
+            for i, bn in enumerate(self.bns):
+                bn.aff = self._bn_out[off:off + 3 * bn.c].view(3, bn.c)
+                items[i] = _lib.BnAffineItem(bn.gamma.data.data_ptr(), bn.beta.data.data_ptr(),
+                                             bn.moving_mean.data_ptr(), bn.moving_variance.data_ptr(),
+                                             bn.aff.data_ptr(), float(bn.eps), int(bn.c))
+                off += 3 * bn.c
+            host = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
+            self._bn_items = host.to(dev)
+            self._bn_key = key
+            self._bn_max_c = max(bn.c for bn in self.bns)
+        L = _lib.load()
+        _lib.check(L.m3d_bn_affine_batched(self._bn_items.data_ptr(), len(self.bns), self._bn_max_c,
+                                           _lib.stream()), "bn_affine_batched")
 
     def state_dict(self):
         d = {p.name: p.data.detach().cpu().clone() for p in self.params}

@@ -660,6 +660,22 @@ int m3d_subsample221_bwd(const float* dy, int64_t B, int64_t H, int64_t W, int64
  * mode): rstd = 1/sqrt(var+eps), scale = gamma*rstd, shift = beta - mean*scale. */
 int m3d_bn_affine(const float* gamma, const float* beta, const float* mean, const float* var,
                   float eps, int64_t C, float* scale, float* shift, float* rstd, m3d_stream_t s);
+/* Every frozen-BN affine of a model in one launch (the same expressions as
+ * m3d_bn_affine, bit-identical): items is a DEVICE array of n descriptors, one
+ * per BatchNorm layer; item i writes out[0..C) = rstd, out[C..2C) = scale,
+ * out[2C..3C) = shift.  max_c >= every item's C.  Replaces the per-layer
+ * affine of each BatchNorm call in the backbone's forward (core/models.py:
+ * 102-114: KL.BatchNormalization(training=False) after every Conv3D). */
+typedef struct m3d_bn_affine_item {
+    const float* gamma;
+    const float* beta;
+    const float* mean;
+    const float* var;
+    float* out;
+    float eps;
+    int32_t C;
+} m3d_bn_affine_item_t;
+int m3d_bn_affine_batched(const m3d_bn_affine_item_t* items, int32_t n, int64_t max_c, m3d_stream_t s);
 
 /* Backward of y = act(z*scale + shift [+ residual]) for frozen-statistics BN
  * (TRAIN_BN=False).  dpre = dy * (y > 0 if relu); dz = dpre*scale (or dpre;

@@ -577,3 +577,49 @@ def test_wino_weight_gradient_accuracy(cuda, cin, cout):
     err = float((dw.double().cpu() - ref).abs().max() / ref.abs().max())
     print(f"winograd weight gradient {cin}->{cout}: rel err {err:.2e}")
     assert err <= 2e-5
+
+
+def test_bn_affine_batched_matches_per_layer(cuda):
+    """ParamStore.bn_affine_refresh (one m3d_bn_affine_batched launch for every
+    BN layer) writes the same bits as m3d_bn_affine per layer, and a backbone
+    forward with the batched affines equals one with the per-call affines."""
+    from m3d import _lib
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, synthetic_volume
+    L = _lib.load()
+    model = RPN(synthetic_rpn_config(64), device=cuda, seed=3)
+    st = model.store
+    g = torch.Generator().manual_seed(5)
+    for bn in st.bns:                       # non-trivial statistics and affine parameters
+        bn.moving_mean.copy_(torch.randn(bn.c, generator=g))
+        bn.moving_variance.copy_(torch.rand(bn.c, generator=g) + 0.5)
+        bn.gamma.data.copy_(torch.randn(bn.c, generator=g))
+        bn.beta.data.copy_(torch.randn(bn.c, generator=g))
+    st.bn_affine_refresh()
+    torch.cuda.synchronize()
+    for bn in st.bns:
+        ref = torch.empty((3, bn.c), device=cuda)
+        _lib.check(L.m3d_bn_affine(bn.gamma.data.data_ptr(), bn.beta.data.data_ptr(), bn.moving_mean.data_ptr(),
+                                   bn.moving_variance.data_ptr(), float(bn.eps), bn.c, ref[1].data_ptr(),
+                                   ref[2].data_ptr(), ref[0].data_ptr(), _lib.stream()), "bn_affine")
+        assert torch.equal(ref, bn.aff), bn.name
+    image = synthetic_volume(64, seed=7).to(cuda)
+    with torch.no_grad():
+        a = model.backbone(image)
+        refresh = st.bn_affine_refresh
+        st.bn_affine_refresh = lambda: None          # per-call affines (bn_aff_live stays False)
+        st.bn_aff_live = False
+        try:
+            import m3d.backbone as mb
+            orig = mb.ResNet3D.__call__
+
+            def per_call(self, image):
+                return self._forward(image)
+            mb.ResNet3D.__call__ = per_call
+            b = model.backbone(image)
+        finally:
+            mb.ResNet3D.__call__ = orig
+            st.bn_affine_refresh = refresh
+    for x, y in zip(a, b):
+        if x is not None:
+            assert torch.equal(x, y)

@@ -46,3 +46,14 @@ def test_stream_fork_bad_mode(cuda):
     lib.check(lib.load().m3d_stream_fork(s, s, ev.value), "stream_fork")
     torch.cuda.synchronize()
     lib.check(lib.load().m3d_fork_event_destroy(ev.value), "fork_event_destroy")
+
+
+def test_stream_handle_is_torch_current_stream(cuda):
+    """m3d._lib.stream() (the raw-handle fast path) names the stream torch
+    considers current, on the default stream and inside a side-stream context."""
+    from m3d import _lib
+    assert _lib.stream() == torch.cuda.current_stream().cuda_stream
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        assert _lib.stream() == side.cuda_stream == torch.cuda.current_stream().cuda_stream
+    assert _lib.stream() == torch.cuda.current_stream().cuda_stream
