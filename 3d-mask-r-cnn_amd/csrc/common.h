@@ -173,6 +173,15 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_CONV1_EPI
 #define M3D_TUNE_CONV1_EPI 1
 #endif
+// conv_gemm epilogue: float4 rows per thread whose residual / destination loads
+// are issued together before their stores (4: round 4)
+#ifndef M3D_TUNE_EPI_PB
+#define M3D_TUNE_EPI_PB 4
+#endif
+// the implicit-GEMM convs on the bf16 split at 2 workgroups per CU instead of 3
+#ifndef M3D_TUNE_CONV_X3_OCC2
+#define M3D_TUNE_CONV_X3_OCC2 0
+#endif
 #ifndef M3D_TUNE_WINO_NY
 #define M3D_TUNE_WINO_NY 4
 #endif

@@ -437,7 +437,7 @@ __device__ __forceinline__ void epi_store4_pre(const ConvP& p, const Epi& e, int
 // spill at 3, and must not touch the register budget of the other forms)
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false,
           bool X3 = false, bool FBN = false>
-__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && X3ACC_CONV) ? 3 : 2)) void conv_gemm_kernel(ConvP p,
+__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (X3ACC_CONV || M3D_TUNE_CONV_X3_OCC2)) ? 3 : 2)) void conv_gemm_kernel(ConvP p,
                                                                                                   Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
@@ -704,7 +704,9 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && X
         if constexpr (X3) {
             const char* Ab = reinterpret_cast<const char*>(smem);
             const char* Bb = Ab + 3 * BM * BK * 2;
-#pragma unroll
+            // (fresh-accumulator form: one k step at a time -- unrolled, the two
+            // steps' fragments and partials exceed the register budget)
+#pragma unroll X3ACC_CONV ? 1 : 2
             for (int s16 = 0; s16 < BK / 16; ++s16) {
                 // lane (l32, h): row l32, k = 16 s16 + 8h .. +7 (one 16-B chunk)
                 bf16x8 af[TM][3], bfr[TN][3];
@@ -848,7 +850,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && X
         }
         // PB float4 per thread per batch: with pf, the batch's residual /
         // destination loads are all issued before its first store
-        constexpr int PB = QN < 4 ? QN : 4;
+        constexpr int PB = QN < M3D_TUNE_EPI_PB ? QN : M3D_TUNE_EPI_PB;
         static_assert(QN % PB == 0, "epilogue batches");
 #pragma unroll
         for (int q0 = 0; q0 < QN; q0 += PB) {
@@ -1459,7 +1461,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
     __syncthreads();
     for (int t = 0; t < nchunks; ++t) {
         if (t + 1 < nchunks) load(ms + (int64_t)(t + 1) * BKM);
-#pragma unroll
+#pragma unroll X3ACC_WG ? 1 : 2
         for (int s16 = 0; s16 < 2; ++s16) {
             bf16x8 af[TI][3], bfr[TJ][3];
 #pragma unroll
@@ -2565,7 +2567,7 @@ struct X3G {
     int K, N, nbatch;
     int64_t psa, psb;          // plane strides (elements)
     int64_t bsa, bsb, bsc;     // batch strides (elements)
-    X3Epi ep;                  // x3_gemm256_af_kernel only
+    X3Epi ep = {};             // x3_gemm256_af_kernel only (zero: the plain C store)
 };
 
 // byte offset of (row, chunk) in a 16-deep X3 plane: 32-B rows of two 16-B
@@ -2692,7 +2694,7 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
             if (kt + 1 < nk) load(kt + 1);
             const char* As = smem + (NBUF == 2 ? (kt & 1) : 0) * STAGE;
             const char* Bs = As + 3 * PLA;
-#pragma unroll
+#pragma unroll X3ACC_GEMM ? 1 : BK / 16
             for (int s16 = 0; s16 < BK / 16; ++s16) {
                 // lane (l32, h): row l32 of its 32-row blocks, k = 16 s16 + 8h .. +7
                 bf16x8 af[TM][3], bfr[TN][3];
@@ -4793,7 +4795,7 @@ static int x3_af32_env() { return (x3_mask() >> 4) & 1; }
 // af32: U is fp32 [P][T][K] (split in the GEMM's LDS store)
 static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipStream_t s,
                          bool af32 = false) {
-    X3G q;
+    X3G q{};                   // (value-initialised: q.ep.on = 0, the plain C store)
     q.a = reinterpret_cast<const unsigned short*>(ws.U);
     q.af = ws.U;
     q.b = reinterpret_cast<const unsigned short*>(ws.V);
@@ -4835,7 +4837,7 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     }
     const int64_t tiles = ((T + 127) / 128) * ((N + 127) / 128) * P;
     const bool bk16 = x3_bk_env() == 16;
-    const bool occ3 = !bk16 && x3_occ3_env();
+    const bool occ3 = !bk16 && x3_occ3_env() && !X3ACC_GEMM;   // (fresh accumulators: no room at 3/CU)
     const int64_t resident = (int64_t)num_cus() * (bk16 || occ3 ? 3 : 2);
     const bool persist = x3_persist_env() && tiles > 2 * resident;
     const dim3 grid(persist ? (unsigned)(resident / 8 * 8) : (unsigned)tiles);

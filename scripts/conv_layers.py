@@ -50,6 +50,7 @@ def main():
     print(f"{'x shape':>26} {'k':>7} {'Cin':>5} {'Cout':>5} {'n':>2} {'alg':>5} "
           f"{'fwd_ms':>7} {'TF/s':>6} {'GB/s':>6} {'bwd_ms':>7} {'TF/s':>6} {'tot_ms*n':>8}")
     tot = 0.0
+    tot_f = tot_f1 = 0.0
     rows = []
     for key, cs in groups.items():
         xs, layer, geo, relu, rs, rm, bn, nd = cs[0]
@@ -92,6 +93,8 @@ def main():
         nb = 4.0 * (x.numel() + layer.kernel.data.numel() + 2 * y.numel() + (r.numel() if r is not None else 0))
         n = len(cs)
         tot += n * (tf + tbm)
+        tot_f += n * tf
+        tot_f1 += n * tf if geo.k == (1, 1, 1) else 0.0
         rows.append((n * (tf + tbm), f"{str(xs):>26} {str(geo.k):>7} {Cin:>5} {Cout:>5} {n:>2} "
                      f"{'wino' if wino else 'dir':>5} {tf:7.3f} {fl / tf / 1e9:6.1f} {nb / tf / 1e6:6.0f} "
                      f"{tbm:7.3f} {2 * fl / tbm / 1e9:6.1f} {n * (tf + tbm):8.3f}"))
@@ -99,7 +102,7 @@ def main():
         torch.cuda.empty_cache()
     for _, line in sorted(rows, reverse=True):
         print(line, flush=True)
-    print(f"total fwd+bwd over layers: {tot:.2f} ms")
+    print(f"total fwd {tot_f:.2f} ms (1x1x1 {tot_f1:.2f}); total fwd+bwd over layers: {tot:.2f} ms")
 
 
 if __name__ == "__main__":

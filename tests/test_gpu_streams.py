@@ -57,3 +57,32 @@ def test_stream_handle_is_torch_current_stream(cuda):
     with torch.cuda.stream(side):
         assert _lib.stream() == side.cuda_stream == torch.cuda.current_stream().cuda_stream
     assert _lib.stream() == torch.cuda.current_stream().cuda_stream
+
+
+def test_fork_mode2_recycled_buffers(cuda):
+    """The weight-gradient fork's default event kind (mode 2: no system-scope
+    fence) with buffers the caching allocator recycles between the streams: a
+    block written on one stream, handed to the other by the fork, freed and
+    reused there, always reads back what its last writer stored (the
+    device-scope release of each kernel's end carries it across XCDs)."""
+    import m3d._lib as lib
+    from m3d.nn import fork_event
+    L = lib.load()
+    side, main = torch.cuda.Stream(cuda), torch.cuda.current_stream(cuda)
+    n = 1 << 20
+    for it in range(64):
+        with torch.cuda.stream(side):
+            x = torch.full((n,), float(it), device=cuda)
+            x.add_(0.5)
+        lib.check(L.m3d_stream_fork(side.cuda_stream, main.cuda_stream, fork_event(cuda.index or 0, 2)), "fork")
+        s = x.sum()                                   # main reads the side stream's block
+        x.record_stream(main)
+        del x                                         # the block returns to side's pool after main's use
+        lib.check(L.m3d_stream_fork(main.cuda_stream, side.cuda_stream, fork_event(cuda.index or 0, 2)), "fork")
+        with torch.cuda.stream(side):
+            y = torch.full((n,), -1.0, device=cuda)   # likely the recycled block, rewritten
+            t = y.sum()
+        lib.check(L.m3d_stream_fork(side.cuda_stream, main.cuda_stream, fork_event(cuda.index or 0, 2)), "fork")
+        assert float(s) == (it + 0.5) * n
+        assert float(t) == -float(n)
+        del y
