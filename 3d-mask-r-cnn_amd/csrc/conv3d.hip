@@ -2555,7 +2555,21 @@ struct X3Epi {
     const float* res;          // [M][N] (res_mode 1) or nullptr
     float* z;                  // pre-BN output or nullptr
     int act;                   // act() code
-    int on;                    // 0: plain C store
+    int on;                    // 0: plain C store, 1: the forward conv epilogue above, 2: the fused
+                               // BN-ReLU backward below (a 1x1x1 conv's data gradient)
+    // on == 2: epi_bnbwd4's maths per element of the data gradient g (accumulate 0):
+    // g masked by y > 0 (frelu), dz = g * fscale into C, g into fdres, and the channel
+    // sums (g, g * (fz - fmean) * frstd, dz) of each 128-row half tile into fpart row
+    // 2 * (m0 / 256) + (wave row)
+    const float* fy;
+    const float* fz;
+    const float* fscale;
+    const float* fmean;
+    const float* frstd;
+    float* fdres;
+    float* fpart;
+    int64_t fprows;
+    int frelu;
 };
 
 struct X3G {
@@ -2913,6 +2927,10 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
 template <int N_> struct IC { static constexpr int v = N_; };
 // M3D_TUNE_X3AF (A/B bits): 1 static s_setprio 1 for waves 4-7, 2 s_setprio
 // around each step's MFMA cluster, 8 all six stages in ONE __shared__ array
+// EPI (compile-time, one instantiation per epilogue so each gets its own
+// register allocation): 0 the plain C store, 1 the forward conv epilogue,
+// 2 the fused BN-ReLU backward (X3Epi.on)
+template <int EPI>
 __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #if M3D_TUNE_X3AF & 8
     __shared__ __attribute__((aligned(16))) char sAll[18 * G2_PL];
@@ -3046,7 +3064,70 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
-    if (g.ep.on) {
+    if constexpr (EPI == 2) {
+        // fused BN-ReLU backward (X3Epi on == 2): per accumulator tile its 16 y / z
+        // values loaded before its stores; rows past M load zeros (masked, summed
+        // as 0) and their stores are dropped
+        const X3Epi& E = g.ep;
+        const uint64_t rbytes = (uint64_t)(g.M - m0) * g.N * 4;
+        const __amdgpu_buffer_rsrc_t ry = make_rsrc(E.fy ? E.fy + m0 * g.N : g.c, E.frelu ? rbytes : 0);
+        const __amdgpu_buffer_rsrc_t rzz = make_rsrc(E.fz ? E.fz + m0 * g.N : g.c, E.fz ? rbytes : 0);
+        const __amdgpu_buffer_rsrc_t rd = make_rsrc(E.fdres ? E.fdres + m0 * g.N : g.c, E.fdres ? rbytes : 0);
+        float sums[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = (int)n0 + wn * 64 + j * 32 + l32;
+            const float sc = E.fscale ? E.fscale[col] : 1.0f;
+            const float mu = E.fz ? E.fmean[col] : 0.0f, rs = E.fz ? E.frstd[col] : 1.0f;
+            float sp = 0.f, sx = 0.f, sz = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float yv[16], zv[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int off = (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u);
+                    yv[r] = E.frelu ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, off, 0, 0)) : 1.0f;
+                    zv[r] = E.fz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rzz, off, 0, 0)) : 0.0f;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int off = (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u);
+                    float gv = acc[i][j][r];
+                    if (E.frelu && !(yv[r] > 0.f)) gv = 0.f;
+                    const float d = gv * sc;
+                    sp += gv;
+                    sx += gv * ((zv[r] - mu) * rs);
+                    sz += d;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d), rc, off, 0, 0);
+                    if (E.fdres) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rd, off, 0, 0);
+                }
+                // one tile's 32 loads in flight at a time (hoisting every tile's
+                // loads above the stores spilled hundreds of registers)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            sums[j][0] = sp; sums[j][1] = sx; sums[j][2] = sz;
+        }
+        if (!E.fpart) return;
+        // column sums of each 128-row half tile (wave row wm): the two lane halves
+        // (rows 4 apart) combined, one partial row per half tile (no block barrier)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) sums[j][a] += __shfl_xor(sums[j][a], 32);
+        if (h == 0) {
+            const int64_t prow = (m0 / 256) * 2 + wm;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = (int)n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) E.fpart[((int64_t)a * E.fprows + prow) * g.N + col] = sums[j][a];
+            }
+        }
+        return;
+    }
+    if constexpr (EPI == 1) {
         // the fused conv epilogue (X3Epi): per accumulator tile its 16 residual
         // values are loaded before its first store; rows past M read zeros and
         // their stores are dropped (the descriptors' range)
@@ -4817,7 +4898,7 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     if (af32 && x3_256_env() && N % 256 == 0 && T >= 256 && t256n >= M3D_TUNE_X3_256_MIN_TILES) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
-        hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
+        hipLaunchKernelGGL(x3_gemm256_af_kernel<0>, grid, dim3(512), 0, s, q);
         return;
     }
     if (!af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
@@ -4963,7 +5044,8 @@ static int conv1_x3_launch(const float* a, const uint16_t* planes, int64_t M, in
         q.ep.bias = e->bias; q.ep.scale = e->scale; q.ep.shift = e->shift;
         q.ep.res = e->res_mode == 1 ? e->res : nullptr; q.ep.z = e->z; q.ep.act = e->relu; q.ep.on = 1;
     }
-    hipLaunchKernelGGL(x3_gemm256_af_kernel, grid, dim3(512), 0, s, q);
+    if (fuse) hipLaunchKernelGGL(x3_gemm256_af_kernel<1>, grid, dim3(512), 0, s, q);
+    else hipLaunchKernelGGL(x3_gemm256_af_kernel<0>, grid, dim3(512), 0, s, q);
     int rc = check_launch("x3_gemm256_af_kernel(conv1)");
     if (rc || !e || fuse) return rc;
     ConvP p{};
@@ -4996,6 +5078,39 @@ extern "C" int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, i
                                       int64_t D, int64_t Cin, int64_t Cout, float* dx, m3d_stream_t s) {
     if (B <= 0 || H <= 0 || W <= 0 || D <= 0) return einval("conv3d x3: tensor dimensions must be positive");
     return conv1_x3_launch(dz, planes, B * H * W * D, Cout, Cin, H, W, D, dx, nullptr, st(s));
+}
+
+// m3d_conv3d_bwd_data_x3 with the fused BN-ReLU backward of the unit that made
+// x (m3d_conv3d_bwd_data_bn's contract, accumulate 0): the GEMM's epilogue
+// applies it to each element (dz into dx, dpre into bn->dres) and writes the
+// channel sums of each 128-row half tile; bn_sums_reduce folds them in row order.
+extern "C" int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W,
+                                         int64_t D, int64_t Cin, int64_t Cout, float* dx, const m3d_bn_bwd_t* bn,
+                                         void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s) {
+    if (B <= 0 || H <= 0 || W <= 0 || D <= 0) return einval("conv3d x3: tensor dimensions must be positive");
+    const int64_t M = B * H * W * D;
+    if (Cout % 32 || Cin % 256) return einval("conv1 x3: K must be a multiple of 32 and N of 256");
+    if (M > 0x7FFFFFFF || M * Cout >= op_lim() || M * Cin >= op_lim() || Cin * Cout * 2 >= 0xFFFFFFF0LL)
+        return einval("conv1 x3: operand larger than 4 GiB (32-bit buffer offsets)");
+    const int64_t rows = 2 * ((M + 255) / 256);           // one partial row per 128-row half tile
+    Epi e{};
+    int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
+    if (rc) return rc;
+    X3G q{};
+    q.af = dz;
+    q.b = reinterpret_cast<const unsigned short*>(planes);
+    q.c = dx;
+    q.M = M; q.K = (int)Cout; q.N = (int)Cin; q.nbatch = 1;
+    q.psb = Cout * Cin;
+    q.ep.on = 2;
+    q.ep.fy = e.fy; q.ep.fz = e.fz; q.ep.fscale = e.fscale; q.ep.fmean = e.fmean; q.ep.frstd = e.frstd;
+    q.ep.fdres = e.fdres; q.ep.fpart = e.fpart; q.ep.fprows = rows; q.ep.frelu = e.frelu;
+    const int64_t t256 = (rows / 2) * (Cin / 256);
+    const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
+    hipLaunchKernelGGL(x3_gemm256_af_kernel<2>, grid, dim3(512), 0, st(s), q);
+    rc = check_launch("x3_gemm256_af_kernel(conv1 bwd-data, fused BN backward)");
+    if (rc || !e.fpart) return rc;
+    return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, st(s));
 }
 
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {

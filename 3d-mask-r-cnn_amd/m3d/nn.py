@@ -876,7 +876,18 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
             dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin)
-            if dx_x3:
+            if dx_x3 and rec is not None and rec.armed and _fuse_final(link, x, acc):
+                # the producer's BN-ReLU backward in the split GEMM's epilogue
+                planes = _x3_planes(w, Cin, Cout, False)
+                dres_f = torch.empty_like(x) if rec.need_res else None
+                bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
+                d = rec.descriptor(dres_f)
+                check(L.m3d_conv3d_bwd_data_x3_bn(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx),
+                                                  ctypes.addressof(d), ptr(bws), bwsb, stream()),
+                      "conv3d_bwd_data_x3_bn")
+                rec.buf, rec.dres, rec.done = dx, dres_f, True
+                fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
+            elif dx_x3:
                 planes = _x3_planes(w, Cin, Cout, False)
                 check(L.m3d_conv3d_bwd_data_x3(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), stream()),
                       "conv3d_bwd_data_x3")

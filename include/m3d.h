@@ -445,6 +445,12 @@ int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int6
                                 int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                                 void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn,
                                 void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s);
+/* m3d_conv3d_bwd_data_x3 (a 1x1x1 stride-1 conv's data gradient on the
+ * bf16-split GEMM, accumulate 0) with m3d_conv3d_bwd_data_bn's fused BN-ReLU
+ * backward in the GEMM's epilogue; bn_ws: m3d_bn_bwd_fused_workspace_bytes. */
+int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
+                              int64_t Cin, int64_t Cout, float* dx, const m3d_bn_bwd_t* bn, void* bn_ws,
+                              size_t bn_ws_bytes, m3d_stream_t s);
 int m3d_conv3d_bwd_data_splitk_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                                   int64_t Cin, int64_t Cout, float* dx, int32_t accumulate, int32_t splits,
                                   void* workspace, size_t ws_bytes, const m3d_bn_bwd_t* bn, void* bn_ws,

@@ -70,6 +70,9 @@ CASES = [
     ("wino", 3, 128, 64, 2, 5, 7, 9, 0, False, True, True),         # ragged grid, batch 2
     ("splitk4", 1, 2048, 512, 1, 4, 4, 16, 1, True, True, True),    # res5 identity 2a: 4 K-slices, accumulated
     ("splitk2", 1, 1024, 256, 1, 4, 4, 8, 0, True, True, False),    # 2 K-slices
+    ("x3", 1, 512, 256, 1, 16, 16, 8, 0, True, True, False),         # rpn_conv_shared1 <- shared2 (bf16-split GEMM)
+    ("x3", 1, 256, 512, 1, 10, 6, 9, 0, True, True, True),           # ragged last 256-row tile, dres
+    ("x3", 1, 768, 1024, 2, 8, 8, 8, 0, False, False, True),         # no ReLU / gamma sum, 3 N-tiles
 ]
 
 
@@ -116,6 +119,19 @@ def test_fused_matches_unfused(cuda, alg, k, cin, cout, B, H, W, D, acc, relu, w
             _lib.check(L.m3d_conv3d_bwd_data_splitk_bn(dz_in.data_ptr(), w.data_ptr(), B, H, W, D, cin, cout,
                                                        dx.data_ptr(), a, sp, wsk.data_ptr(), wsk.numel() * 4, d, bws,
                                                        bwsb, st), "dgrad split-K bn")
+    elif alg == "x3":
+        planes = torch.empty(3 * cin * cout, device=cuda, dtype=torch.int16)
+        _lib.check(L.m3d_conv1_x3_planes(w.data_ptr(), cin, cout, 0, planes.data_ptr(), st), "planes")
+
+        def conv(dx, a):
+            assert a == 0
+            _lib.check(L.m3d_conv3d_bwd_data_x3(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
+                                                dx.data_ptr(), st), "dgrad x3")
+
+        def conv_bn(dx, a, d, bws, bwsb):
+            assert a == 0
+            _lib.check(L.m3d_conv3d_bwd_data_x3_bn(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
+                                                   dx.data_ptr(), d, bws, bwsb, st), "dgrad x3 bn")
     else:
         def conv(dx, a):
             _lib.check(L.m3d_conv3d_bwd_data(dz_in.data_ptr(), w.data_ptr(), B, H, W, D, cin, k, k, k, cout, H, W,
