@@ -163,11 +163,16 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
 // 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at
 // 128^3 (same box, r04ny4_ab), parity suite green (profiles/r04ny4_parity_tests.log)
-// x3 GEMM accumulation (conv3d.hip x3_mac): 1 = each 16-deep k step's six
-// bf16 MFMAs into a fresh accumulator, added to the running sum by one VALU
-// add (round 5: half the fp32 error); 0 = one MFMA accumulator chain
+// x3 GEMM accumulation (conv3d.hip x3_mac): 0 = one MFMA accumulator chain
+// (default); bits 0/1/2 = each 16-deep k step's six bf16 MFMAs into a fresh
+// accumulator added to the running sum by one VALU add, for the point GEMMs /
+// implicit-GEMM convs / weight gradients.  The host model predicted half the
+// error; measured on the MI355X the 128^3 gradient median got WORSE (3.29e-6
+// vs 2.28e-6 with bit 0, F(2x2x4) data gradients) and the step slower (27.2 vs
+// 26.6 ms, gpurun_out/r05safe): the MFMA accumulator does better than an
+// fp32 rounding per instruction.  Kept as an A/B switch.
 #ifndef M3D_TUNE_X3_ACC
-#define M3D_TUNE_X3_ACC 1
+#define M3D_TUNE_X3_ACC 0
 #endif
 // 1x1x1 conv epilogue inside x3_gemm256_af_kernel (1) or as a second pass (0)
 #ifndef M3D_TUNE_CONV1_EPI

@@ -70,6 +70,9 @@ class _Block:
         return self.c(y, relu=True, residual=short, fuse=fuse_out, fuse_in=fb)
 
 
+BN_AFFINE_BATCHED = True
+
+
 class ResNet3D:
     """resnet_graph(input_image, architecture, stage5, train_bn) -> [C1..C5]."""
 
@@ -99,7 +102,10 @@ class ResNet3D:
     def __call__(self, image):
         self.links = []                 # GradLinks of this forward (checked by check_links)
         self.fuses = []                 # BNFuse records of this forward (checked by check_fuses)
-        # every BN layer's affine in one launch for this forward (ParamStore.bn_affine_refresh)
+        # every BN layer's affine in one launch for this forward (ParamStore.bn_affine_refresh;
+        # BN_AFFINE_BATCHED False: one m3d_bn_affine per BN conv unit, A/B)
+        if not BN_AFFINE_BATCHED:
+            return self._forward(image)
         self.store.bn_affine_refresh()
         self.store.bn_aff_live = True
         try:

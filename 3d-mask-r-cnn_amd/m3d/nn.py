@@ -459,6 +459,9 @@ def _link_park(link, dx, acc):
 # read-modify-write pass over the activation gradient less per fused unit.
 # BN_FUSE = False runs bn_act_bwd everywhere (A/B; tests/test_gpu_bnfuse.py).
 BN_FUSE = True
+# ... and in the bf16-split 1x1x1 data gradient (m3d_conv3d_bwd_data_x3_bn;
+# False: that GEMM's plain store, then the producer's bn_act_bwd)
+X3_BN_FUSE = True
 
 
 class BNFuse:
@@ -876,7 +879,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
             dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin)
-            if dx_x3 and rec is not None and rec.armed and _fuse_final(link, x, acc):
+            if dx_x3 and X3_BN_FUSE and rec is not None and rec.armed and _fuse_final(link, x, acc):
                 # the producer's BN-ReLU backward in the split GEMM's epilogue
                 planes = _x3_planes(w, Cin, Cout, False)
                 dres_f = torch.empty_like(x) if rec.need_res else None

@@ -8,7 +8,7 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-AMD_SERIALIZE_KERNEL=3 timeout -k 10 300 python -u -m pytest tests/test_gpu_conv.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "split3 or gemm or conv1_x3 or bn_affine or wino or maxpool" tests/test_gpu_bnfuse.py > $OUT/stage1.log 2>&1 || { echo "stage1 failed"; tail -30 $OUT/stage1.log; exit 1; }
+AMD_SERIALIZE_KERNEL=3 timeout -k 10 300 python -u -m pytest tests/test_gpu_conv.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "split3 or gemm or conv1_x3 or bn_affine or wino or maxpool or fused" tests/test_gpu_bnfuse.py > $OUT/stage1.log 2>&1 || { echo "stage1 failed"; tail -30 $OUT/stage1.log; exit 1; }
 tail -n 1 $OUT/stage1.log
 for L in "$@"; do
   M3D_LIB_FILE=$L timeout -k 10 240 python -u scripts/grad_table.py --out $OUT/grad_$L.json --variants base > $OUT/grad_$L.log 2>&1 || { tail -20 $OUT/grad_$L.log; exit 1; }

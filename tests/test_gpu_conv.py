@@ -590,11 +590,12 @@ def test_bn_affine_batched_matches_per_layer(cuda):
     model = RPN(synthetic_rpn_config(64), device=cuda, seed=3)
     st = model.store
     g = torch.Generator().manual_seed(5)
-    for bn in st.bns:                       # non-trivial statistics and affine parameters
-        bn.moving_mean.copy_(torch.randn(bn.c, generator=g))
-        bn.moving_variance.copy_(torch.rand(bn.c, generator=g) + 0.5)
-        bn.gamma.data.copy_(torch.randn(bn.c, generator=g))
-        bn.beta.data.copy_(torch.randn(bn.c, generator=g))
+    with torch.no_grad():
+        for bn in st.bns:                   # non-trivial statistics and affine parameters
+            bn.moving_mean.copy_(torch.randn(bn.c, generator=g))
+            bn.moving_variance.copy_(torch.rand(bn.c, generator=g) + 0.5)
+            bn.gamma.data.copy_(torch.randn(bn.c, generator=g))
+            bn.beta.data.copy_(torch.randn(bn.c, generator=g))
     st.bn_affine_refresh()
     torch.cuda.synchronize()
     for bn in st.bns:
