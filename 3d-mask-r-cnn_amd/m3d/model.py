@@ -27,6 +27,11 @@ from .layers import ProposalLayer
 from .optim import KerasOptimizer
 from .params import ParamStore
 
+# Enqueue the ProposalLayer (side stream) after the loss instead of before it.
+# Same work and dependencies; in a HIP-graph capture the loss / backward then is
+# the forward's first successor (see nn.WGRAD_LAST).
+PROPOSALS_AFTER_LOSS = False
+
 
 # ---------------------------------------------------------------------------
 # losses
@@ -327,8 +332,10 @@ class RPN:
         store.grad_flat, the ProposalLayer overlapped on its side stream."""
         self.store.zero_grad()
         out = self.forward(image, proposals=False)
-        join = self.proposals_async(out)[1] if proposals else None
+        join = self.proposals_async(out)[1] if proposals and not PROPOSALS_AFTER_LOSS else None
         total, lc, lb = self.loss_total(out, targets)
+        if proposals and PROPOSALS_AFTER_LOSS:
+            join = self.proposals_async(out)[1]
         total.backward()
         self.rpn.finish_backward()
         return {"loss": total.detach(), "rpn_class_loss": lc.detach(), "rpn_bbox_loss": lb.detach(),
@@ -341,10 +348,11 @@ class RPN:
 
     def graphed_train_step(self, image, targets: RPNTargets, proposals=True, warmup=2):
         """The training step with its forward + backward (+ ProposalLayer on
-        the side stream) captured once into a HIP graph: ~870 launches replay
-        without the host's per-launch overhead (the stage-4/5 layers are
-        launch-bound eagerly; measured on the 128^3 step the replayed kernels
-        run longer than eager ones, so bench.py uses it only with --graph).
+        the side stream) captured once into a HIP graph: ~680 launches replay
+        without the host's per-launch overhead (host 6.6 ms per replay against
+        16.5 ms eager, step 26.04 vs 26.23 ms at 128^3; the replay runs each
+        stream's chain on its own queue once every fork is captured compute
+        path first, nn.WGRAD_LAST).
         The optimizer runs eagerly after each replay
         (its learning rate decays per iteration).  ``image`` and ``targets``
         are the graph's static inputs: copy new data into them in place.

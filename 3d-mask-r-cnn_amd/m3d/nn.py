@@ -54,6 +54,14 @@ GRAD_HOOK = None
 # before anything reads the gradients -- makes the compute stream wait for it.
 # False runs them in line (bench.py --wgrad-inline: serialized kernel traces).
 WGRAD_STREAM = True
+# Enqueue order inside a conv unit's backward: True launches the weight
+# gradient (side stream) after the data gradient (compute stream), False before
+# it.  The GPU work and its dependencies are the same either way (eager 128^3
+# step 26.23 vs 26.25 ms), but a HIP-graph replay puts a node's first-captured
+# successor on the node's own queue: with the weight gradient first, the
+# compute path hopped onto the weight-gradient queue behind its backlog and the
+# replay ran 28.7 ms; data gradient first, 26.04 ms (scripts/gpu_r05_graph3.sh).
+WGRAD_LAST = True
 _SIDE = {}
 _SIDE_USED = set()
 
@@ -757,7 +765,7 @@ class _ConvBNAct(torch.autograd.Function):
         if halo is not None and side is not None:
             halo[0].record_stream(side)
         if ctx.wino:
-            if grads.get("kernel") is not None:
+            def wgrad():
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                     tw = _span()
                     if min(Cin, Cout) < WINO_WGRAD_MIN_C and halo is not None:
@@ -795,6 +803,9 @@ class _ConvBNAct(torch.autograd.Function):
                         _log("wino_wgrad", direct, exe, 4.0 * (x.numel() + dz.numel() + w.numel()),
                              "bwd_weight", ctx.name, tw, "f32" if min(Cin, Cout) < WINO_WGRAD_MIN_C else "x3")
                 ctx.u = None
+            has_w = grads.get("kernel") is not None
+            if has_w and not WGRAD_LAST:
+                wgrad()
             td = _span()
             ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device)
             dx = None
@@ -836,6 +847,8 @@ class _ConvBNAct(torch.autograd.Function):
                          4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel), "bwd_data", ctx.name,
                          td, "x3")
                 dx = _link_park(ctx.link, dx, acc)
+            if has_w and WGRAD_LAST:
+                wgrad()
             _grad_done(grads, side)
             ctx.halo = None
             ctx.fuse_in = None
@@ -843,7 +856,7 @@ class _ConvBNAct(torch.autograd.Function):
                     None, None, None, None)
         if halo is not None and ctx.need_dx:
             raise ValueError("the stem's halo form has no data gradient (its input is the volume)")
-        if grads.get("kernel") is not None:
+        def wgrad_d():
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 tw = _span()
                 if halo is not None:        # the stem on a depth slab: halo planes beside the slab
@@ -859,6 +872,9 @@ class _ConvBNAct(torch.autograd.Function):
                     _log(f"conv{kh}_wgrad", direct, direct, 4.0 * (x.numel() + dz.numel() + w.numel()),
                          "bwd_weight", ctx.name, tw,
                          "x3" if halo is None and _wgrad1_x3(geo, Cin, Cout, (H, W, D)) else "f32")
+        has_w = grads.get("kernel") is not None
+        if has_w and not WGRAD_LAST:
+            wgrad_d()
         dx = None
         link = ctx.link
         acc = 0
@@ -929,6 +945,8 @@ class _ConvBNAct(torch.autograd.Function):
                      4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel),
                      "bwd_data", ctx.name, td, "x3" if dx_x3 else "f32")
             dx = _link_park(link, dx, acc)
+        if has_w and WGRAD_LAST:
+            wgrad_d()
         _grad_done(grads, side)
         dr = None
         if need_res:
@@ -1119,6 +1137,13 @@ def subsample221(x):
 RPN_OUT_SIDE = True
 
 
+def _rpn_out_wgrad(L, side, xb, dz, H, W, D, Cin, npad, grads):
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
+                                      W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
+                                      stream()), "rpn_out_wgrad")
+
+
 class _RPNOut(torch.autograd.Function):
     """The RPN class/bbox 1x1x1 heads (rpn_class_raw, rpn_bbox_pred;
     core/models.py:540-556) of all pyramid levels in one function.  Each level's
@@ -1201,6 +1226,7 @@ class _RPNOut(torch.autograd.Function):
                 if grads.get("bias") is not None:
                     bn_act_bwd(dz, None, None, r, npad, False, None, None, None, None, None, None,
                                None, grads["bias"])
+                side = None
                 if grads.get("kernel") is not None:
                     # on the weight-gradient stream like every conv unit's (joined before the
                     # update); the data gradients below do not wait for it
@@ -1208,10 +1234,8 @@ class _RPNOut(torch.autograd.Function):
                     if side is not None:
                         dz_all.record_stream(side)
                         s.record_stream(side)
-                    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                        check(L.m3d_conv3d_bwd_weight(ptr(xb), ptr(dz), 1, H, W, D, Cin, 1, 1, 1, npad, H,
-                                                      W, D, 1, 1, 1, 0, 0, 0, ptr(grads["kernel"]),
-                                                      stream()), "rpn_out_wgrad")
+                    if not WGRAD_LAST:
+                        _rpn_out_wgrad(L, side, xb, dz, H, W, D, Cin, npad, grads)
                 if fws[li] is not None:
                     # rpn_conv_shared2's ReLU backward (and bias sums) in this data gradient's epilogue
                     dres_f, bws, bwsb = fws[li]
@@ -1223,6 +1247,8 @@ class _RPNOut(torch.autograd.Function):
                     check(L.m3d_conv3d_bwd_data(ptr(dz), ptr(w_pad), 1, H, W, D, Cin, 1, 1, 1, npad, H,
                                                 W, D, 1, 1, 1, 0, 0, 0, dshared[li][b:b + 1].data_ptr(),
                                                 0, stream()), "rpn_out_dgrad")
+                if grads.get("kernel") is not None and WGRAD_LAST:
+                    _rpn_out_wgrad(L, side, xb, dz, H, W, D, Cin, npad, grads)
                 off += r
         for li, rec in enumerate(fuses):
             if fws[li] is not None:

@@ -1116,7 +1116,8 @@ def main():
     ap.add_argument("--roi-size", type=int, default=256, help="large-volume ROIAlign leg (0: off)")
     ap.add_argument("--infer-size", type=int, default=256, help="MaskRCNN inference leg size (0: off)")
     ap.add_argument("--cpu-slab", type=int, default=0, help="CPU-baseline depth slab (0: whole volume)")
-    ap.add_argument("--graph", action="store_true", help="HIP-graph capture of the N=1 step")
+    ap.add_argument("--graph", action="store_true", help="(default at N=1) HIP-graph replay of the step")
+    ap.add_argument("--eager", action="store_true", help="N=1: eager launches instead of the HIP-graph replay")
     ap.add_argument("--wgrad-inline", action="store_true",
                     help="weight gradients on the compute stream (serialized kernel traces)")
     args = ap.parse_args()
@@ -1141,18 +1142,25 @@ def main():
     targets = RPNTargets(match, bbox, dev)
     props = not args.no_proposals
 
-    if world == 1 and args.graph:
-        # the whole forward + backward as one HIP graph (m3d.model.RPN.graphed_train_step):
-        # measured slower (37.6 vs 35.4 ms/step at 128^3: the replayed kernels run
-        # longer, 37.2 vs 36.5 ms busy, while the ~1 ms of launch gaps it removes
-        # is less than that), so eager launches are the default
-        step = model.graphed_train_step(image, targets, proposals=props)
-    else:
-        def step():
-            return data_parallel_train_step(model, image, targets, world, proposals=props)
-
     def eager_step():
         return data_parallel_train_step(model, image, targets, world, proposals=props)
+
+    graph_error = None
+    use_graph = world == 1 and not args.eager
+    if use_graph:
+        # N=1: the forward + backward (+ ProposalLayer) captured once as a HIP graph
+        # (m3d.model.RPN.graphed_train_step) and replayed, the optimizer eager
+        # after it.  128^3: 26.04 vs 26.23 ms eager, host 6.6 vs 16.5 ms per step
+        # (DESIGN.md 5, round 5).  N>1 stays eager: the gradient buckets'
+        # all-reduces are enqueued as the backward produces them.
+        try:
+            step = model.graphed_train_step(image, targets, proposals=props)
+        except Exception as e:  # report, never hide: the line then says hip_graph false
+            graph_error = repr(e)
+            use_graph = False
+            torch.cuda.synchronize()
+    if not use_graph:
+        step = eager_step
 
     log(f"[bench] rank {rank}/{world} size {S}^3, warmup {args.warmup}")
     for _ in range(args.warmup):
@@ -1186,7 +1194,20 @@ def main():
                                   f"{S}^3 x1 volume per GPU",
                       "size": S, "batch_per_gpu": 1, "parallelism": f"dp{world}",
                       "anchors": int(model.anchors.shape[1]),
-                      "hip_graph": bool(world == 1 and args.graph)}}
+                      "hip_graph": use_graph}}
+    if graph_error is not None:
+        out["config"]["hip_graph_error"] = graph_error
+    if use_graph:
+        # the same step launched eagerly, timed the same way (for comparison only)
+        for _ in range(2):
+            eager_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eager_step()
+        torch.cuda.synchronize()
+        out["eager_ms_per_step"] = round((time.perf_counter() - t0) / args.steps * 1e3, 2)
+        model._graph = step = None              # release the replay's private pool before the legs
     if world == 1 and not args.no_extras:
         try:
             out["step_roofline"] = step_roofline(model, eager_step, ms, os.environ.get("M3D_STEP_ROOFLINE_TABLE"))

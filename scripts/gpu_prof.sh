@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 P="rocprofv3 -f csv"
 STEPS=5; WARM=2
-timeout -k 10 400 $P --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps $STEPS --warmup $WARM --no-extras --size $S > $OUT/prof_bench.log 2>&1 || { echo "rocprof bench failed"; tail -30 $OUT/prof_bench.log; exit 1; }
+timeout -k 10 400 $P --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --eager --steps $STEPS --warmup $WARM --no-extras --size $S > $OUT/prof_bench.log 2>&1 || { echo "rocprof bench failed"; tail -30 $OUT/prof_bench.log; exit 1; }
 python3 scripts/prof_summary.py $OUT/prof/run_kernel_stats.csv $((STEPS + WARM)) 40 > $OUT/bench_kernels.txt
 rm -f $OUT/prof/run_kernel_trace.csv
 NR=$([ "$S" = 128 ] && echo 128 || echo 512)

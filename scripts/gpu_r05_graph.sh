@@ -1,7 +1,9 @@
 #!/bin/bash
 # HIP-graph replay vs eager: the replayed step under the
-# runtime's graph-execution modes -- default (AQL packet capture), packet
-# capture off, and a forced count of parallel-branch streams.
+# runtime's graph-execution modes (r05graph: packet capture off and a forced
+# count of graph streams changed nothing) and with more hardware queues per
+# process (HWQ), so the replay's parallel branches stop sharing a queue with
+# the weight-gradient backlog.
 set -o pipefail
 OUT=gpurun_out/${1:-r05graph}
 mkdir -p $OUT
@@ -15,6 +17,8 @@ import json; d = json.loads(open('$OUT/b.json').read().strip().splitlines()[-1])
 for rep in 1 2; do
   run eager M3D_X=0
   run graph M3D_X=0 --graph
-  run graph_nopkt DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 --graph
-  run graph_q4 DEBUG_HIP_FORCE_GRAPH_QUEUES=4 --graph
+  for q in ${HWQ:-8 16}; do
+    run eager_hwq$q GPU_MAX_HW_QUEUES=$q
+    run graph_hwq$q GPU_MAX_HW_QUEUES=$q --graph
+  done
 done

@@ -14,6 +14,12 @@ import torch  # noqa: E402
 from m3d.config import synthetic_rpn_config  # noqa: E402
 from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume  # noqa: E402
 
+import m3d.nn as nn  # noqa: E402
+
+GRAPH = "--graph" in sys.argv             # also time the HIP-graph replay's host and GPU cost
+NO_PROFILE = "--no-profile" in sys.argv
+if "--wgrad-last" in sys.argv:
+    nn.WGRAD_LAST = True
 dev = torch.device("cuda:0")
 S = int(os.environ.get("S", "128"))
 cfg = synthetic_rpn_config(S)
@@ -43,6 +49,28 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f"host enqueue {(t1 - t0) / N * 1e3:.2f} ms/step, wall {(t2 - t0) / N * 1e3:.2f} ms/step")
+if GRAPH:
+    step = model.graphed_train_step(image, targets, proposals=True)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(N):
+        model._graph.replay()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"graph replay (WGRAD_LAST={nn.WGRAD_LAST}): host {(t1 - t0) / N * 1e3:.2f} ms/replay, "
+          f"wall {(t2 - t0) / N * 1e3:.2f} ms/replay")
+    t0 = time.perf_counter()
+    for _ in range(N):
+        step()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"graph step (replay + optimizer): host {(t1 - t0) / N * 1e3:.2f} ms/step, wall {(t2 - t0) / N * 1e3:.2f} ms/step")
+if NO_PROFILE:
+    sys.exit(0)
 # where the host's enqueue time goes: cProfile over N more steps (the GPU queue
 # stays full, so the profile sees the host's own work, plus any blocking call)
 import cProfile  # noqa: E402
