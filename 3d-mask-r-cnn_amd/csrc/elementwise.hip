@@ -512,20 +512,16 @@ __global__ __launch_bounds__(256) void bn_act_bwd_kernel(
 // 4 channel quads (float4) x 64 row groups, each with 4 independent
 // accumulators, folded by a fixed LDS tree (deterministic).  64 row groups keep
 // the serial chain short for the 2048-block partials of bn_act_bwd_kernel.
-__global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __restrict__ part, int gx,
-                                                             int C, float* __restrict__ s0,
-                                                             float* __restrict__ s1,
-                                                             float* __restrict__ s2) {
-    const int a = blockIdx.y;
-    float* dst = a == 0 ? s0 : (a == 1 ? s1 : s2);
-    if (!dst) return;
+// The fold of one [gx][C] partial array into dst (block blockIdx.x's 16
+// channels); every thread of the block calls it.
+__device__ __forceinline__ void bn_sums_fold(const float* __restrict__ part, int gx, int C, float* __restrict__ dst) {
     const int tq = threadIdx.x & 3, rg = threadIdx.x >> 2;
     const int c = blockIdx.x * 16 + tq * 4;
     float4 acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < C) {
-        const float* p = part + (int64_t)a * gx * C + c;
+        const float* p = part + c;
         int b = rg;
         for (; b + 192 < gx; b += 256) {
 #pragma unroll
@@ -558,6 +554,16 @@ __global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __rest
         const float4 r = red[0][tq];
         dst[c] += r.x; dst[c + 1] += r.y; dst[c + 2] += r.z; dst[c + 3] += r.w;
     }
+}
+
+__global__ __launch_bounds__(256) void bn_sums_reduce_kernel(const float* __restrict__ part, int gx,
+                                                             int C, float* __restrict__ s0,
+                                                             float* __restrict__ s1,
+                                                             float* __restrict__ s2) {
+    const int a = blockIdx.y;
+    float* dst = a == 0 ? s0 : (a == 1 ? s1 : s2);
+    if (!dst) return;
+    bn_sums_fold(part + (int64_t)a * gx * C, gx, C, dst);
 }
 
 // ---- Keras SGD over a flat parameter buffer split into segments padded to
@@ -1058,6 +1064,124 @@ extern "C" int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, i
     hipLaunchKernelGGL(bn_sums_reduce_kernel, dim3((unsigned)((C + 15) / 16), 3), dim3(256), 0, st(s),
                        (const float*)workspace, (int)gx, (int)C, sum_dpre, sum_dpre_xhat, sum_dz);
     return check_launch("bn_sums_reduce_kernel");
+}
+
+// ---- batched column sums (m3d_col_sums_batched): every item with
+// bn_act_bwd_kernel's block geometry (bn_grid) and summation order, one sum
+// instead of three, all items in one launch; then bn_sums_reduce_kernel's fold
+// per item, all items in a second launch.  The item table travels by value in
+// the kernel arguments (no device copy; capturable in a HIP graph).
+struct ColSumsBatch {
+    const float* x[M3D_COL_SUMS_MAX];
+    float* out[M3D_COL_SUMS_MAX];
+    int64_t M[M3D_COL_SUMS_MAX];
+    int64_t part[M3D_COL_SUMS_MAX];        // float offset of the item's [gx][C] partial rows
+    int C[M3D_COL_SUMS_MAX], T[M3D_COL_SUMS_MAX], gx[M3D_COL_SUMS_MAX];
+    int block0[M3D_COL_SUMS_MAX + 1];      // first block of each item in the flat grid
+    int n;
+};
+
+__global__ __launch_bounds__(256) void col_sums_batched_kernel(const ColSumsBatch b, float* __restrict__ ws) {
+    int i = 0;
+    while (i + 1 < b.n && (int)blockIdx.x >= b.block0[i + 1]) ++i;
+    const int local = (int)blockIdx.x - b.block0[i];
+    const int gx = b.gx[i], T = b.T[i], C = b.C[i];
+    const int bx = local % gx, by = local / gx;
+    const int R = 256 / T;
+    const int tx = threadIdx.x % T, ty = threadIdx.x / T;
+    const int c = (by * T + tx) * 4;
+    const float* __restrict__ x = b.x[i];
+    const int64_t M = b.M[i];
+    float s[4] = {0, 0, 0, 0};
+    if (c < C) {
+        const int64_t step = (int64_t)gx * R;
+        for (int64_t r = (int64_t)bx * R + ty; r < M; r += step) {
+            const float4 v = *(const float4*)(x + r * C + c);
+            s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+        }
+    }
+    __shared__ float red[256][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[threadIdx.x][q] = s[q];
+    __syncthreads();
+    for (int st_ = R / 2; st_ > 0; st_ >>= 1) {
+        if (ty < st_) {
+            const int o = threadIdx.x + st_ * T;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[threadIdx.x][q] += red[o][q];
+        }
+        __syncthreads();
+    }
+    if (ty == 0 && c < C)
+        *(float4*)(ws + b.part[i] + (int64_t)bx * C + c) =
+            make_float4(red[tx][0], red[tx][1], red[tx][2], red[tx][3]);
+}
+
+// grid (ceil(max C / 16), n): item blockIdx.y's partial rows folded into its out
+__global__ __launch_bounds__(256) void col_sums_reduce_kernel(const ColSumsBatch b, const float* __restrict__ ws) {
+    const int i = blockIdx.y;
+    const int C = b.C[i];
+    if ((int)blockIdx.x * 16 >= C) return;                 // block-uniform
+    bn_sums_fold(ws + b.part[i], b.gx[i], C, b.out[i]);
+}
+
+static int col_sums_plan(const m3d_col_sums_item_t* items, int32_t n, ColSumsBatch& b, size_t& ws_floats,
+                         int& max_c) {
+    if (n < 0 || n > M3D_COL_SUMS_MAX || (n > 0 && !items)) return einval("col_sums_batched: bad item count");
+    b = ColSumsBatch{};
+    b.n = n;
+    ws_floats = 0;
+    max_c = 0;
+    int blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const m3d_col_sums_item_t& it = items[i];
+        if (!it.x || !it.out || it.M <= 0 || it.C <= 0 || it.C % 4 || it.C > (1 << 20))
+            return einval("col_sums_batched: an item needs x, out, M > 0, C > 0 and C % 4 == 0");
+        for (int j = 0; j < i; ++j)
+            if (items[j].out == it.out) return einval("col_sums_batched: two items share out");
+        int T, groups;
+        int64_t gx;
+        bn_grid(it.M, it.C, T, groups, gx);
+        b.x[i] = it.x;
+        b.out[i] = it.out;
+        b.M[i] = it.M;
+        b.C[i] = (int)it.C;
+        b.T[i] = T;
+        b.gx[i] = (int)gx;
+        b.part[i] = (int64_t)ws_floats;
+        b.block0[i] = blocks;
+        blocks += (int)gx * groups;
+        ws_floats += (size_t)gx * (size_t)it.C;
+        if ((int)it.C > max_c) max_c = (int)it.C;
+    }
+    b.block0[n] = blocks;
+    return M3D_OK;
+}
+
+extern "C" size_t m3d_col_sums_batched_workspace_bytes(const m3d_col_sums_item_t* items, int32_t n) {
+    ColSumsBatch b;
+    size_t f;
+    int mc;
+    if (col_sums_plan(items, n, b, f, mc) != M3D_OK) return 0;
+    return sizeof(float) * f;
+}
+
+extern "C" int m3d_col_sums_batched(const m3d_col_sums_item_t* items, int32_t n, void* workspace, size_t ws_bytes,
+                                    m3d_stream_t s) {
+    ColSumsBatch b;
+    size_t f;
+    int max_c;
+    int rc = col_sums_plan(items, n, b, f, max_c);
+    if (rc) return rc;
+    if (n == 0) return M3D_OK;
+    if (!workspace || ws_bytes < sizeof(float) * f) return einval("col_sums_batched: workspace too small");
+    hipLaunchKernelGGL(col_sums_batched_kernel, dim3((unsigned)b.block0[n]), dim3(256), 0, st(s), b,
+                       (float*)workspace);
+    rc = check_launch("col_sums_batched_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(col_sums_reduce_kernel, dim3((unsigned)((max_c + 15) / 16), (unsigned)n), dim3(256), 0, st(s),
+                       b, (const float*)workspace);
+    return check_launch("col_sums_reduce_kernel");
 }
 
 // per-segment squared norms of (grad + l2 * w) for tf.clip_by_norm

@@ -175,6 +175,8 @@ _SIGS = {
     "m3d_bn_act_bwd_workspace_bytes": [c_i64, c_i64],
     "m3d_bn_act_bwd": [c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_i32, c_p,
                        c_p, c_p, c_p, c_sz, c_p],
+    "m3d_col_sums_batched_workspace_bytes": [c_p, c_i32],
+    "m3d_col_sums_batched": [c_p, c_i32, c_p, c_sz, c_p],
     "m3d_sgd_keras": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_p, c_p, c_p],
     "m3d_adam_keras": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_f, c_f, c_f, c_f, c_f, c_p,
                        c_p, c_p],
@@ -191,7 +193,7 @@ _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_s
              "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
              "m3d_conv3d_wino_tile_y": c_i32, "m3d_conv3d_wino_dgrad_tile_y": c_i32,
-             "m3d_conv3d_wino_dgrad_tile_z": c_i32}
+             "m3d_conv3d_wino_dgrad_tile_z": c_i32, "m3d_col_sums_batched_workspace_bytes": c_sz}
 
 EXPORTED = tuple(_SIGS)
 
@@ -232,6 +234,14 @@ class BnAffineItem(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("mean", ctypes.c_void_p),
                 ("var", ctypes.c_void_p), ("out", ctypes.c_void_p), ("eps", ctypes.c_float),
                 ("C", ctypes.c_int32)]
+
+
+class ColSumsItem(ctypes.Structure):
+    """m3d_col_sums_item_t (include/m3d.h)."""
+    _fields_ = [("x", ctypes.c_void_p), ("M", ctypes.c_int64), ("C", ctypes.c_int64), ("out", ctypes.c_void_p)]
+
+
+COL_SUMS_MAX = 16          # M3D_COL_SUMS_MAX
 
 
 class _Lib:

@@ -278,8 +278,16 @@ class RPN:
         return self.fpn(C2, C3, C4, C5)
 
     def forward(self, image, proposals=True):
-        fmaps = self.features(image)
-        logits, probs, bbox = self.rpn(fmaps)
+        from . import nn as _nn
+        batch = _nn.BiasSums() if torch.is_grad_enabled() else None
+        prev, _nn.BIAS_BATCH = _nn.BIAS_BATCH, batch
+        try:
+            fmaps = self.features(image)
+            logits, probs, bbox = self.rpn(fmaps)
+        finally:
+            _nn.BIAS_BATCH = prev
+        if batch is not None:
+            self.rpn.bias_batch = batch         # flushed by RPNHead.finish_backward
         rois = None
         if proposals:
             rois = self.proposal_layer([probs, bbox, self.anchors])

@@ -385,6 +385,60 @@ def bn_act_bwd(dy, y, z, M, C, relu, scale, mean, rstd, dz, dres, sum_dpre, sum_
                            ptr(sum_dz), ptr(ws), wsb, stream()), "bn_act_bwd")
 
 
+class BiasSums:
+    """The bias gradients of the bias-only units of one forward (the FPN's
+    fpn_c*p* / fpn_p* convs and the RPN class/bbox heads: out += column sums of
+    the output gradient, tf.nn.bias_add's gradient), collected during the
+    backward and reduced by two launches in ``flush`` (m3d_col_sums_batched,
+    bit-identical per item to the per-unit m3d_bn_act_bwd) instead of two per
+    unit.  Armed by RPN.forward for its training graph (BIAS_BATCH), flushed by
+    RPNHead.finish_backward, i.e. before the weight-gradient join and before
+    anything reads the gradients.  The output gradients stay referenced until
+    the flush (same stream: no record_stream needed)."""
+
+    def __init__(self):
+        self.items = []           # (x, M, C, out)
+
+    def add(self, x, M, C, out):
+        if any(o is out or o.data_ptr() == out.data_ptr() for _, _, _, o in self.items) \
+                or len(self.items) >= _lib.COL_SUMS_MAX:
+            self.flush()
+        self.items.append((x, M, C, out))
+
+    def flush(self):
+        items, self.items = self.items, []
+        if not items:
+            return
+        L = _L()
+        arr = (_lib.ColSumsItem * len(items))(*[_lib.ColSumsItem(ptr(x), M, C, ptr(o)) for x, M, C, o in items])
+        wsb = int(L.m3d_col_sums_batched_workspace_bytes(arr, len(items)))
+        if wsb <= 0:
+            raise ValueError("col_sums_batched: " + L.m3d_last_error().decode())
+        ws = torch.empty(wsb // 4 + 1, device=items[0][0].device, dtype=torch.float32)
+        t0 = _span()
+        check(L.m3d_col_sums_batched(arr, len(items), ptr(ws), wsb, stream()), "col_sums_batched")
+        if LAYER_LOG is not None:
+            _log("bias_sums", 0, 0, 4.0 * sum(x.numel() for x, _, _, _ in items), "bwd_bn",
+                 f"{len(items)} bias-only units", t0)
+
+
+# The BiasSums of the training forward being built (RPN.forward sets and
+# clears it); None: every bias-only unit reduces its own bias gradient inline.
+BIAS_BATCH = None
+# False: no batching (every bias-only unit launches its own reduction).
+BIAS_BATCHED = True
+
+
+def bias_grad(dy, M, C, out, grads=None, batch=None):
+    """out += column sums of dy [M, C]: batched when ``batch`` is armed and the
+    unit has no bucket hook (a DP all-reduce may start as soon as the unit's
+    gradients are signalled done), inline otherwise."""
+    if batch is not None and BIAS_BATCHED and not (grads and grads.get("_hook") is not None):
+        batch.add(dy, M, C, out)
+    else:
+        bn_act_bwd(dy, None, None, M, C, False, None, None, None, None, None, None, None, out)
+
+
 @dataclass
 class ConvGeom:
     k: tuple
@@ -687,6 +741,7 @@ class _ConvBNAct(torch.autograd.Function):
             # data-gradient calls still to come: the last one releases the held workspace
             wshare["pending_bwd"] = wshare.get("pending_bwd", 0) + 1
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
+        ctx.bias_batch = BIAS_BATCH if grads is not None else None
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
         # this unit's BN-ReLU backward handed to its consumer (BNFuse)
@@ -740,8 +795,7 @@ class _ConvBNAct(torch.autograd.Function):
             dz = dy
             dres = dy if need_res else None
             if grads.get("bias") is not None:
-                bn_act_bwd(dy, None, None, M, Cout, False, None, None, None, None, None, None, None,
-                           grads["bias"])
+                bias_grad(dy, M, Cout, grads["bias"], grads, ctx.bias_batch)
         else:
             if rec is not None:
                 rec.clear()
@@ -752,7 +806,8 @@ class _ConvBNAct(torch.autograd.Function):
                 mean, rstd, scale = ctx.bn
             bn_act_bwd(dy, y, z, M, Cout, ctx.relu, scale, mean, rstd, dz, dres, grads.get("beta"),
                        grads.get("gamma") if z is not None else None, grads.get("bias"))
-        if logging and not fused_bn:
+        if logging and not fused_bn and not (trivial and ctx.bias_batch is not None and BIAS_BATCHED
+                                             and grads.get("_hook") is None):
             nel = dy.numel() * (1 + (0 if trivial else 1 + (ctx.relu or ctx.bn is not None) +
                                      (z is not None) + (dres is not None and not trivial)))
             _log("bn_act_bwd", 0, 0, 4.0 * nel, "bwd_bn", ctx.name, t0)
@@ -1180,6 +1235,7 @@ class _RPNOut(torch.autograd.Function):
                  "fwd", "rpn_class_raw+rpn_bbox_pred", t0)
         ctx.save_for_backward(w24, *shared)
         ctx.grads, ctx.rows, ctx.apl = grads, rows, apl
+        ctx.bias_batch = BIAS_BATCH if grads is not None else None
         ctx.fuses = [f if (f is not None and f.armed and f.y is not None and f.y.data_ptr() == s.data_ptr()
                            and f.y.shape == s.shape) else None
                      for f, s in zip(fuses or [None] * len(shared), shared)]
@@ -1218,14 +1274,14 @@ class _RPNOut(torch.autograd.Function):
             dz_all = torch.nn.functional.pad(
                 torch.cat([dlogits[b].reshape(R, 2 * apl), dbbox[b].reshape(R, 6 * apl)], dim=1),
                 (0, npad - n_out))
+            if grads.get("bias") is not None:
+                # all levels' rows at once (one column sum of the level-concatenated matrix)
+                bias_grad(dz_all, R, npad, grads["bias"], grads, ctx.bias_batch)
             off = 0
             for li, (s, r) in enumerate(zip(shared, rows)):
                 xb = s[b:b + 1]
                 _, H, W, D, _ = xb.shape
                 dz = dz_all[off:off + r]
-                if grads.get("bias") is not None:
-                    bn_act_bwd(dz, None, None, r, npad, False, None, None, None, None, None, None,
-                               None, grads["bias"])
                 side = None
                 if grads.get("kernel") is not None:
                     # on the weight-gradient stream like every conv unit's (joined before the

@@ -699,6 +699,25 @@ int m3d_bn_act_bwd(const float* dy, const float* y, const float* z, int64_t M, i
                    float* dz, float* dres, int32_t accumulate_res, float* sum_dpre,
                    float* sum_dpre_xhat, float* sum_dz, void* workspace, size_t ws_bytes,
                    m3d_stream_t s);
+/* Column sums of up to M3D_COL_SUMS_MAX row-major [M, C] matrices in two
+ * launches: out[c] += sum_m x[m*C + c] per item -- the bias gradients of the
+ * bias-only conv units (tf.nn.bias_add's gradient; the FPN's fpn_c*p* /
+ * fpn_p* and the RPN class/bbox heads, core/models.py:3190-3214, 540-556),
+ * collected during the backward and reduced together.  Each item's sum is
+ * bit-identical to m3d_bn_act_bwd(x, ..., relu 0, scale NULL, sum_dz = out)
+ * (same block geometry and summation order).  No two items may share `out`.
+ * C % 4 == 0; items is a host array (copied into the launch); workspace:
+ * m3d_col_sums_batched_workspace_bytes of the same items. */
+#define M3D_COL_SUMS_MAX 16
+typedef struct {
+    const float* x;
+    int64_t M;
+    int64_t C;
+    float* out;
+} m3d_col_sums_item_t;
+size_t m3d_col_sums_batched_workspace_bytes(const m3d_col_sums_item_t* items, int32_t n);
+int m3d_col_sums_batched(const m3d_col_sums_item_t* items, int32_t n, void* workspace, size_t ws_bytes,
+                         m3d_stream_t s);
 /* Keras 2.3.1 SGD (momentum, per-tensor tf.clip_by_norm, decayed lr computed
  * by the caller) plus the RPN L2 term wd*0.5*||w||^2/size(w) whose gradient
  * l2_coef[seg]*w is added first (core/models.py:3340-3387).  params / grads /

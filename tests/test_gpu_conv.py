@@ -624,3 +624,76 @@ def test_bn_affine_batched_matches_per_layer(cuda):
     for x, y in zip(a, b):
         if x is not None:
             assert torch.equal(x, y)
+
+
+def test_col_sums_batched_matches_per_unit(cuda):
+    """m3d_col_sums_batched (the bias-only units' bias gradients, nn.BiasSums):
+    every item's column sums are bit-identical to the per-unit m3d_bn_act_bwd
+    (relu 0, no BN, sum_dz), added (+=) into out, across the shapes the model
+    feeds it (one-row to 32^3-row matrices, 4 to 256 channels); float64 within
+    1e-5 of scale; a shared out / bad C is rejected."""
+    import ctypes
+
+    from m3d import _lib, nn
+    L = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    shapes = [(32768, 256), (4096, 256), (1, 4), (333, 32), (513, 128), (12345, 64), (7, 256)]
+    xs = [torch.randn(m, c, generator=g).to(cuda) for m, c in shapes]
+    base = [torch.randn(c, generator=g).to(cuda) for _, c in shapes]
+    ref = [b.clone() for b in base]
+    for x, r, (m, c) in zip(xs, ref, shapes):
+        nn.bn_act_bwd(x, None, None, m, c, False, None, None, None, None, None, None, None, r)
+    out = [b.clone() for b in base]
+    arr = (_lib.ColSumsItem * len(shapes))(*[_lib.ColSumsItem(x.data_ptr(), m, c, o.data_ptr())
+                                             for x, o, (m, c) in zip(xs, out, shapes)])
+    wsb = int(L.m3d_col_sums_batched_workspace_bytes(arr, len(shapes)))
+    ws = torch.empty(wsb // 4 + 1, device=cuda)
+    _lib.check(L.m3d_col_sums_batched(arr, len(shapes), ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
+    torch.cuda.synchronize()
+    for x, o, r, b in zip(xs, out, ref, base):
+        assert torch.equal(o, r)
+        want = b.double() + x.double().sum(0)
+        assert float((o.double() - want).abs().max()) <= 1e-5 * max(1.0, float(want.abs().max()))
+    bad = (_lib.ColSumsItem * 2)(_lib.ColSumsItem(xs[0].data_ptr(), 4, 256, out[0].data_ptr()),
+                                 _lib.ColSumsItem(xs[1].data_ptr(), 4, 256, out[0].data_ptr()))
+    with pytest.raises(ValueError):
+        _lib.check(L.m3d_col_sums_batched(bad, 2, ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
+    bad1 = (_lib.ColSumsItem * 1)(_lib.ColSumsItem(xs[0].data_ptr(), 4, 6, out[0].data_ptr()))
+    with pytest.raises(ValueError):
+        _lib.check(L.m3d_col_sums_batched(bad1, 1, ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
+    assert ctypes.sizeof(_lib.ColSumsItem) == 32
+
+
+def test_bias_batch_model_step_matches_inline(cuda):
+    """The RPN training step with the bias-only units' gradients batched
+    (nn.BIAS_BATCHED, flushed in RPNHead.finish_backward) gives the same
+    gradients as inline per-unit reductions (the FPN units bit for bit; the RPN
+    heads' bias sums all levels at once instead of level by level)."""
+    from m3d import _lib, nn
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
+    _lib.set_deterministic(True)              # weight gradients without arrival-order atomics
+    cfg = synthetic_rpn_config(64, depth=32, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=500)
+    image = synthetic_volume(64, 32, seed=0).to(cuda)
+    grads = []
+    for batched in (True, False):
+        model = RPN(cfg, device=cuda, seed=5)
+        match, bbox = synthetic_rpn_targets(model.anchors.shape[1], 256, seed=2)
+        targets = RPNTargets(match, bbox, cuda)
+        old = nn.BIAS_BATCHED
+        nn.BIAS_BATCHED = batched
+        try:
+            model.forward_backward(image, targets, proposals=False)
+        finally:
+            nn.BIAS_BATCHED = old
+            torch.cuda.synchronize()
+        grads.append({p.name: p.grad.detach().clone() for p in model.store.params if p.grad is not None})
+    _lib.set_deterministic(False)
+    a, b = grads
+    assert a.keys() == b.keys()
+    for k in a:
+        if "rpn_class_raw/bias" in k or "rpn_bbox_pred/bias" in k:
+            s = float(b[k].abs().max())
+            assert float((a[k] - b[k]).abs().max()) <= 1e-5 * max(s, 1e-6), k
+        else:
+            assert torch.equal(a[k], b[k]), k
