@@ -425,8 +425,13 @@ class BiasSums:
 # The BiasSums of the training forward being built (RPN.forward sets and
 # clears it); None: every bias-only unit reduces its own bias gradient inline.
 BIAS_BATCH = None
-# False: no batching (every bias-only unit launches its own reduction).
-BIAS_BATCHED = True
+# Batch the bias-only units' reductions (True) or launch one per unit (False,
+# default).  Measured at 128^3 (scripts/gpu_r05_bias.sh, same box): eager
+# neutral (26.34 vs 26.32 ms, 655 vs 679 launches per step), but the HIP-graph
+# replay of the step slows from 26.0-26.2 to 30.6-30.7 ms with it on; under
+# rocprofv3 the batched replay shows no such loss (its queue assignment is the
+# clean one, r05gtrace2), so the cause is not found -- off until it is.
+BIAS_BATCHED = False
 
 
 def bias_grad(dy, M, C, out, grads=None, batch=None):
