@@ -284,22 +284,35 @@ def _splitk(xshape, geo, cin, cout, bwd_data):
     return int(_L().m3d_conv3d_splitk_count(B * OH * OW * OD, K, N))
 
 
-def _conv1_x3(xshape, geo, K, N):
+# Fewest 256x256 output tiles for which a 1x1x1 conv runs as one bf16-split
+# GEMM (m3d_conv3d_fwd_x3 / _bwd_data_x3) instead of the implicit GEMM or its
+# split-K form, per direction.  Round 5 (scripts/conv1_paths.py,
+# profiles/r05_conv1_paths.txt): at >= 128 tiles the split GEMM's forward wins
+# at every K (64 -> 256 at 256^3: 0.56 vs 0.82 ms; 128 -> 512: 0.36 vs 0.55;
+# 2048 -> 512 at 8x8x256: 0.27 vs 0.34), at 64 tiles it loses to split-K
+# (2048 -> 256 at 8x8x256: 0.24 vs 0.17 ms); the data gradient wins from 256
+# tiles (256 -> 64: 0.37 vs 0.49 ms) and is neutral at 128.  Both forms give
+# the same bits as the implicit GEMM on the split (no split-K).
+CONV1_X3_FWD_TILES = 128
+CONV1_X3_DGRAD_TILES = 256
+CONV1_X3_MIN_K = 32             # round 4: 256 (and 256 tiles both ways)
+
+
+def _conv1_x3(xshape, geo, K, N, bwd_data=False):
     """Run a 1x1x1 stride-1 conv (forward: K = Cin, N = Cout; data gradient:
     K = Cout, N = Cin) as one GEMM on the exact bf16 split (m3d_conv3d_fwd_x3 /
-    _bwd_data_x3)?  Only the big-K convs whose 256x256 tiles fill the chip
-    (rpn_conv_shared2 and the lateral at P2; the other 1x1x1 convs are bound by
-    their epilogue or a short K, where the split costs more than it saves).
-    The choice uses the whole volume's depth under depth-slab sharding, so
-    every slab runs the same kernel as the unsharded volume."""
+    _bwd_data_x3)?  When N is a multiple of 256 and its 256x256 tiles number
+    at least CONV1_X3_FWD_TILES / CONV1_X3_DGRAD_TILES.  The choice uses the
+    whole volume's depth under depth-slab sharding, so every slab runs the same
+    kernel as the unsharded volume."""
     if not CONV1_X3 or geo.k != (1, 1, 1) or geo.stride != (1, 1, 1) or geo.pad != (0, 0, 0):
         return False
     B, H, W, D = xshape[:4]
-    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < 256:
+    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < CONV1_X3_MIN_K:
         return False
     sg = slab.current()
     Dg = sg.D if sg is not None else D
-    return -(-B * H * W * Dg // 256) * (N // 256) >= 256
+    return -(-B * H * W * Dg // 256) * (N // 256) >= (CONV1_X3_DGRAD_TILES if bwd_data else CONV1_X3_FWD_TILES)
 
 
 def _x3_planes(w, cin, cout, transpose):
@@ -954,7 +967,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd = torch.zeros((B, OH, OW, OD, cpad), device=dz.device, dtype=torch.float32)
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
-            dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin)
+            dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True)
             if dx_x3 and X3_BN_FUSE and rec is not None and rec.armed and _fuse_final(link, x, acc):
                 # the producer's BN-ReLU backward in the split GEMM's epilogue
                 planes = _x3_planes(w, Cin, Cout, False)
