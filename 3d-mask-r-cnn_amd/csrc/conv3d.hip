@@ -5018,6 +5018,42 @@ extern "C" int m3d_conv1_x3_planes(const float* w, int64_t Cin, int64_t Cout, in
     return check_launch("x3_wplanes_kernel");
 }
 
+// Both orientations of every listed kernel in one launch (grid (ceil(max
+// Cin*Cout / 256), n)): each element split once, its three planes stored
+// transposed into fwd and in place into bwd (either may be NULL) -- the same
+// bits as x3_wplanes_kernel per orientation.
+__global__ __launch_bounds__(256) void x3_wplanes_batched_kernel(const m3d_x3_planes_item_t* __restrict__ items) {
+    const m3d_x3_planes_item_t it = items[blockIdx.y];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_el = (int64_t)it.cin * it.cout;
+    if (i >= n_el) return;
+    const int c = (int)(i / it.cout), o = (int)(i % it.cout);
+    uint32_t h, m, l;
+    split3(it.w[i], h, m, l);
+    if (it.fwd) {
+        unsigned short* pl = reinterpret_cast<unsigned short*>(it.fwd);
+        const int64_t at = (int64_t)o * it.cin + c;
+        pl[at] = (unsigned short)h;
+        pl[n_el + at] = (unsigned short)m;
+        pl[2 * n_el + at] = (unsigned short)l;
+    }
+    if (it.bwd) {
+        unsigned short* pl = reinterpret_cast<unsigned short*>(it.bwd);
+        pl[i] = (unsigned short)h;
+        pl[n_el + i] = (unsigned short)m;
+        pl[2 * n_el + i] = (unsigned short)l;
+    }
+}
+
+extern "C" int m3d_conv1_x3_planes_batched(const m3d_x3_planes_item_t* items, int32_t n, int64_t max_el,
+                                           m3d_stream_t s) {
+    if (n <= 0 || n > 65535 || max_el <= 0 || max_el > 0x7FFFFFFF || !items)
+        return einval("conv1_x3_planes_batched: bad arguments");
+    hipLaunchKernelGGL(x3_wplanes_batched_kernel, dim3(grid_for(max_el, 256), (unsigned)n), dim3(256), 0, st(s),
+                       items);
+    return check_launch("x3_wplanes_batched_kernel");
+}
+
 // the GEMM on x3_gemm256_af_kernel (plain C = out [M][N]), then -- when the
 // conv has an epilogue -- splitk_epi_kernel over `out` in place (one slice):
 // each element read once and rewritten through epi_store4.  (The epilogue

@@ -76,6 +76,7 @@ _SIGS = {
     "m3d_conv3d_bwd_data_splitk": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                    c_i32, c_i32, c_i32, c_p, c_i32, c_i32, c_p, c_sz, c_p],
     "m3d_conv1_x3_planes": [c_p, c_i64, c_i64, c_i32, c_p, c_p],
+    "m3d_conv1_x3_planes_batched": [c_p, c_i32, c_i64, c_p],
     "m3d_conv3d_fwd_x3": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_i32,
                           c_p, c_p, c_p],
     "m3d_conv3d_bwd_data_x3": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
@@ -234,6 +235,12 @@ class BnAffineItem(ctypes.Structure):
     _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("mean", ctypes.c_void_p),
                 ("var", ctypes.c_void_p), ("out", ctypes.c_void_p), ("eps", ctypes.c_float),
                 ("C", ctypes.c_int32)]
+
+
+class X3PlanesItem(ctypes.Structure):
+    """m3d_x3_planes_item_t (include/m3d.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("fwd", ctypes.c_void_p), ("bwd", ctypes.c_void_p),
+                ("cin", ctypes.c_int32), ("cout", ctypes.c_int32)]
 
 
 class ColSumsItem(ctypes.Structure):

@@ -281,11 +281,14 @@ class RPN:
         from . import nn as _nn
         batch = _nn.BiasSums() if torch.is_grad_enabled() else None
         prev, _nn.BIAS_BATCH = _nn.BIAS_BATCH, batch
+        if _nn.X3_PLANES_BATCHED:
+            _nn.X3_PLANES.refresh(self.device)   # live for this forward (nn.X3Planes)
         try:
             fmaps = self.features(image)
             logits, probs, bbox = self.rpn(fmaps)
         finally:
             _nn.BIAS_BATCH = prev
+            _nn.X3_PLANES.invalidate()          # the backward takes its planes through ctx
         if batch is not None:
             self.rpn.bias_batch = batch         # flushed by RPNHead.finish_backward
         rois = None

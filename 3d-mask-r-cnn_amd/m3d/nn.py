@@ -10,6 +10,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -315,11 +316,100 @@ def _conv1_x3(xshape, geo, K, N, bwd_data=False):
     return -(-B * H * W * Dg // 256) * (N // 256) >= (CONV1_X3_DGRAD_TILES if bwd_data else CONV1_X3_FWD_TILES)
 
 
+class X3Planes:
+    """The bf16-split planes of the 1x1x1 kernels that run on the split GEMM
+    (m3d_conv1_x3_planes), refreshed for all of them by ONE launch per model
+    forward (m3d_conv1_x3_planes_batched: both orientations, the data
+    gradient's too) instead of one launch per conv and per data gradient.
+
+    A kernel is registered the first time a conv asks for its planes (that call
+    splits it alone); each RPN.forward refreshes the registered kernels first
+    (``refresh``) and its convs take the cached planes while ``live``, i.e.
+    during that forward only (``invalidate`` at its end): a conv unit's forward
+    hands the data-gradient planes to its backward through ctx, so no cached
+    plane outlives the weights it was split from (optimizer steps, weight
+    loads and in-place edits all happen outside a forward).  Entries are keyed
+    by the kernel tensor's storage pointer and element count and hold a weak
+    reference to it (the model's persistent kernel view, kept by the
+    ParamStore: while it lives no other tensor can have its storage; a dead
+    entry is dropped at the next refresh)."""
+
+    def __init__(self):
+        self.entries = {}            # (ptr, numel) -> [weakref(w), cin, cout, fwd, bwd, valid]
+        self.tables = {}             # device -> (device item table, n, max_el, key)
+        self.live = False
+        self.hits = self.misses = 0  # refreshed planes taken / per-conv splits while live (tests)
+
+    @staticmethod
+    def _dev(dev):
+        dev = torch.device(dev)
+        return torch.device("cuda", torch.cuda.current_device() if dev.index is None else dev.index)
+
+    def _alive(self, dev):
+        for k in [k for k, e in self.entries.items() if e[0]() is None]:
+            del self.entries[k]
+        return [e for e in self.entries.values() if e[0]().device == dev]
+
+    def refresh(self, dev):
+        """Split every registered kernel on ``dev`` (current stream) and go live."""
+        dev = self._dev(dev)
+        es = self._alive(dev)
+        if es:
+            key = tuple((ptr(e[0]()), ptr(e[3]), ptr(e[4])) for e in es)
+            t = self.tables.get(dev)
+            if t is None or t[3] != key:
+                items = (_lib.X3PlanesItem * len(es))(*[_lib.X3PlanesItem(ptr(e[0]()), ptr(e[3]), ptr(e[4]), e[1], e[2])
+                                                        for e in es])
+                host = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
+                t = self.tables[dev] = (host.to(dev), len(es), max(e[1] * e[2] for e in es), key)
+            check(_L().m3d_conv1_x3_planes_batched(ptr(t[0]), t[1], t[2], stream()), "conv1_x3_planes_batched")
+            for e in es:
+                e[5] = True
+        self.live = True
+
+    def invalidate(self):
+        self.live = False
+
+    def cached(self, w, transpose):
+        """The refreshed planes of w (None when not live / not registered yet)."""
+        if not self.live:
+            return None
+        e = self.entries.get((w.data_ptr(), w.numel()))
+        if e is None or not e[5] or e[0]() is None:
+            return None
+        self.hits += 1
+        return e[3] if transpose else e[4]
+
+    def ensure(self, w, cin, cout):
+        """Register w (the caller's persistent kernel tensor) for the next refresh."""
+        key = (w.data_ptr(), w.numel())
+        e = self.entries.get(key)
+        if (X3_PLANES_BATCHED and (e is None or e[0]() is None)
+                and not torch.cuda.is_current_stream_capturing()):
+            self.entries[key] = [weakref.ref(w), cin, cout,
+                                 torch.empty(3 * cin * cout, device=w.device, dtype=torch.int16),
+                                 torch.empty(3 * cin * cout, device=w.device, dtype=torch.int16), False]
+
+    def get(self, w, cin, cout, transpose):
+        p = self.cached(w, transpose)
+        if p is not None:
+            return p
+        if self.live:
+            self.misses += 1         # a split GEMM's planes not covered by this forward's refresh
+        planes = torch.empty(3 * cin * cout, device=w.device, dtype=torch.int16)
+        check(_L().m3d_conv1_x3_planes(ptr(w), cin, cout, 1 if transpose else 0, ptr(planes), stream()),
+              "conv1_x3_planes")
+        return planes
+
+
+# one launch per model forward for every split-GEMM 1x1x1 kernel's planes
+# (False: one m3d_conv1_x3_planes per conv call and per data gradient)
+X3_PLANES_BATCHED = True
+X3_PLANES = X3Planes()
+
+
 def _x3_planes(w, cin, cout, transpose):
-    planes = torch.empty(3 * cin * cout, device=w.device, dtype=torch.int16)
-    check(_L().m3d_conv1_x3_planes(ptr(w), cin, cout, 1 if transpose else 0, ptr(planes), stream()),
-          "conv1_x3_planes")
-    return planes
+    return X3_PLANES.get(w, cin, cout, transpose)
 
 
 def _shared_wino_ws(wshare, role, ws, wsb, tag=None):
@@ -729,6 +819,7 @@ class _ConvBNAct(torch.autograd.Function):
                       "conv3d_fwd_wino")
         elif res_mode <= 2 and _conv1_x3(x.shape, geo, Cin, Cout):
             planes = _x3_planes(w, Cin, Cout, True)
+            X3_PLANES.ensure(w, Cin, Cout)
             check(_L().m3d_conv3d_fwd_x3(ptr(x), B, H, W, D, Cin, ptr(planes), Cout, ptr(b), ptr(scale),
                                          ptr(shift), ptr(residual), res_mode, 1 if relu else 0, ptr(z), ptr(y),
                                          stream()), "conv3d_fwd_x3")
@@ -759,6 +850,12 @@ class _ConvBNAct(torch.autograd.Function):
             # data-gradient calls still to come: the last one releases the held workspace
             wshare["pending_bwd"] = wshare.get("pending_bwd", 0) + 1
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
+        # the data gradient's split planes of this forward's refresh (X3Planes), if any
+        ctx.x3_bwd = None
+        if geo.k == (1, 1, 1) and need_dx and halo is None and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True):
+            ctx.x3_bwd = X3_PLANES.cached(w, False)
+            if ctx.x3_bwd is None:
+                X3_PLANES.ensure(w, Cin, Cout)
         ctx.bias_batch = BIAS_BATCH if grads is not None else None
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -970,7 +1067,7 @@ class _ConvBNAct(torch.autograd.Function):
             dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True)
             if dx_x3 and X3_BN_FUSE and rec is not None and rec.armed and _fuse_final(link, x, acc):
                 # the producer's BN-ReLU backward in the split GEMM's epilogue
-                planes = _x3_planes(w, Cin, Cout, False)
+                planes = ctx.x3_bwd if ctx.x3_bwd is not None else _x3_planes(w, Cin, Cout, False)
                 dres_f = torch.empty_like(x) if rec.need_res else None
                 bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
                 d = rec.descriptor(dres_f)
@@ -980,7 +1077,7 @@ class _ConvBNAct(torch.autograd.Function):
                 rec.buf, rec.dres, rec.done = dx, dres_f, True
                 fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
             elif dx_x3:
-                planes = _x3_planes(w, Cin, Cout, False)
+                planes = ctx.x3_bwd if ctx.x3_bwd is not None else _x3_planes(w, Cin, Cout, False)
                 check(L.m3d_conv3d_bwd_data_x3(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), stream()),
                       "conv3d_bwd_data_x3")
             elif (nsk > 1 and rec is not None and rec.armed and not strided and (OH, OW, OD) == (H, W, D)

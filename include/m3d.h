@@ -269,9 +269,9 @@ int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64_t B, int64
                                int64_t Cin, int64_t Cout, int64_t OH, int64_t OW, int64_t OD, int32_t sy,
                                int32_t sx, int32_t sz, float* dx, int32_t accumulate, int32_t splits,
                                void* workspace, size_t ws_bytes, m3d_stream_t s);
-/* 1x1x1 stride-1 convs as one GEMM on the exact bf16 split (the big-K convs
- * of the finest level: rpn_conv_shared2, the P2 lateral, their data
- * gradients).  m3d_conv1_x3_planes splits the Keras kernel w [Cin][Cout] into
+/* 1x1x1 stride-1 convs as one GEMM on the exact bf16 split (the 1x1x1 convs
+ * and data gradients with enough 256x256 output tiles to fill the chip,
+ * m3d.nn._conv1_x3).  m3d_conv1_x3_planes splits the Keras kernel w [Cin][Cout] into
  * planes uint16 [3][N][K] (transpose = 1: forward, N = Cout, K = Cin;
  * transpose = 0: data gradient, N = Cin, K = Cout).  Then the forward (epilogue
  * of m3d_conv3d_fwd: bias, z, BN, same-shape or (2,2,1)-upsampled residual,
@@ -281,6 +281,20 @@ int m3d_conv3d_bwd_data_splitk(const float* dz, const float* w, int64_t B, int64
  * product). */
 int m3d_conv1_x3_planes(const float* w, int64_t Cin, int64_t Cout, int32_t transpose, uint16_t* planes,
                         m3d_stream_t s);
+/* m3d_conv1_x3_planes of many kernels in one launch: items is a DEVICE array of
+ * n descriptors; each kernel w [cin][cout] is split once into its forward
+ * planes (fwd, transpose = 1 layout) and its data-gradient planes (bwd,
+ * transpose = 0 layout), either may be NULL; max_el = max cin*cout.  Same bits
+ * as the per-kernel call (the model's forward refreshes every 1x1x1 kernel that
+ * runs on the split GEMM at once, m3d.nn.X3Planes). */
+typedef struct {
+    const float* w;
+    uint16_t* fwd;
+    uint16_t* bwd;
+    int32_t cin;
+    int32_t cout;
+} m3d_x3_planes_item_t;
+int m3d_conv1_x3_planes_batched(const m3d_x3_planes_item_t* items, int32_t n, int64_t max_el, m3d_stream_t s);
 int m3d_conv3d_fwd_x3(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
                       const uint16_t* planes, int64_t Cout, const float* bias, const float* bn_scale,
                       const float* bn_shift, const float* residual, int32_t res_mode, int32_t relu,

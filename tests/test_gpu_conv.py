@@ -697,3 +697,62 @@ def test_bias_batch_model_step_matches_inline(cuda):
             assert float((a[k] - b[k]).abs().max()) <= 1e-5 * max(s, 1e-6), k
         else:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_x3_planes_batched_matches_per_kernel(cuda):
+    """m3d_conv1_x3_planes_batched (nn.X3Planes: one launch per model forward
+    for every split-GEMM 1x1x1 kernel) writes the same bits as
+    m3d_conv1_x3_planes per kernel and orientation; in a model's second
+    training pass every split-GEMM 1x1x1 conv takes the refreshed planes (no
+    per-conv split), and its gradients equal a pass with per-conv splits."""
+    import ctypes
+
+    from m3d import _lib, nn
+    L = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shapes = [(64, 256), (2048, 512), (32, 256), (256, 1024)]
+    ws = [torch.randn(ci, co, generator=g).to(cuda) for ci, co in shapes]
+    fw = [torch.empty(3 * ci * co, device=cuda, dtype=torch.int16) for ci, co in shapes]
+    bw = [torch.empty(3 * ci * co, device=cuda, dtype=torch.int16) for ci, co in shapes]
+    items = (_lib.X3PlanesItem * len(shapes))(*[_lib.X3PlanesItem(w.data_ptr(), f.data_ptr(), b.data_ptr(), ci, co)
+                                                for w, f, b, (ci, co) in zip(ws, fw, bw, shapes)])
+    tab = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8).to(cuda)
+    _lib.check(L.m3d_conv1_x3_planes_batched(tab.data_ptr(), len(shapes), max(a * b for a, b in shapes),
+                                             _lib.stream()), "planes_batched")
+    for w, f, b, (ci, co) in zip(ws, fw, bw, shapes):
+        for t, got in ((1, f), (0, b)):
+            ref = torch.empty_like(got)
+            _lib.check(L.m3d_conv1_x3_planes(w.data_ptr(), ci, co, t, ref.data_ptr(), _lib.stream()), "planes")
+            assert torch.equal(ref, got)
+    with pytest.raises(ValueError):
+        _lib.check(L.m3d_conv1_x3_planes_batched(tab.data_ptr(), 0, 16, _lib.stream()), "planes_batched")
+    assert ctypes.sizeof(_lib.X3PlanesItem) == 32
+
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
+    _lib.set_deterministic(True)
+    try:
+        cfg = synthetic_rpn_config(64, depth=32, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=500)
+        image = synthetic_volume(64, 32, seed=0).to(cuda)
+        grads = []
+        for batched in (True, False):
+            model = RPN(cfg, device=cuda, seed=5)
+            match, bbox = synthetic_rpn_targets(model.anchors.shape[1], 256, seed=2)
+            targets = RPNTargets(match, bbox, cuda)
+            old = nn.X3_PLANES_BATCHED, nn.CONV1_X3_FWD_TILES, nn.CONV1_X3_DGRAD_TILES
+            # every eligible 1x1x1 conv and data gradient on the split GEMM at this small size
+            nn.X3_PLANES_BATCHED, nn.CONV1_X3_FWD_TILES, nn.CONV1_X3_DGRAD_TILES = batched, 1, 1
+            try:
+                model.forward_backward(image, targets, proposals=False)        # registers the kernels
+                model.forward_backward(image, targets, proposals=False)        # zero_grad + the same pass again
+                if batched:
+                    h0, m0 = nn.X3_PLANES.hits, nn.X3_PLANES.misses
+                    model.forward_backward(image, targets, proposals=False)
+                    assert nn.X3_PLANES.hits > h0 and nn.X3_PLANES.misses == m0
+            finally:
+                nn.X3_PLANES_BATCHED, nn.CONV1_X3_FWD_TILES, nn.CONV1_X3_DGRAD_TILES = old
+                torch.cuda.synchronize()
+            grads.append(model.store.grad_flat.detach().clone())
+        assert torch.equal(grads[0], grads[1])
+    finally:
+        _lib.set_deterministic(False)
