@@ -291,12 +291,16 @@ def _splitk(xshape, geo, cin, cout, bwd_data):
 # profiles/r05_conv1_paths.txt): at >= 128 tiles the split GEMM's forward wins
 # at every K (64 -> 256 at 256^3: 0.56 vs 0.82 ms; 128 -> 512: 0.36 vs 0.55;
 # 2048 -> 512 at 8x8x256: 0.27 vs 0.34), at 64 tiles it loses to split-K
-# (2048 -> 256 at 8x8x256: 0.24 vs 0.17 ms); the data gradient wins from 256
-# tiles (256 -> 64: 0.37 vs 0.49 ms) and is neutral at 128.  Both forms give
-# the same bits as the implicit GEMM on the split (no split-K).
+# (2048 -> 256 at 8x8x256: 0.24 vs 0.17 ms).  Both forms give the same bits
+# as the implicit GEMM on the split (no split-K).  The data gradient alone is
+# faster from 256 tiles at short K too (256 -> 64: 0.37 vs 0.49 ms), but
+# inside the 256^3 step (fused BN-ReLU backward epilogues) it is not: slab step
+# 159.1 / 159.7 ms with the round-4 rule (K >= 256) for the data gradient vs
+# 160.2 / 167.8 with K >= 32 (scripts/gpu_r05_slab_ab.sh), so that rule stays.
 CONV1_X3_FWD_TILES = 128
 CONV1_X3_DGRAD_TILES = 256
-CONV1_X3_MIN_K = 32             # round 4: 256 (and 256 tiles both ways)
+CONV1_X3_MIN_K = 32             # forward; round 4: 256 (and 256 tiles)
+CONV1_X3_DGRAD_MIN_K = 256
 
 
 def _conv1_x3(xshape, geo, K, N, bwd_data=False):
@@ -309,7 +313,7 @@ def _conv1_x3(xshape, geo, K, N, bwd_data=False):
     if not CONV1_X3 or geo.k != (1, 1, 1) or geo.stride != (1, 1, 1) or geo.pad != (0, 0, 0):
         return False
     B, H, W, D = xshape[:4]
-    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < CONV1_X3_MIN_K:
+    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < (CONV1_X3_DGRAD_MIN_K if bwd_data else CONV1_X3_MIN_K):
         return False
     sg = slab.current()
     Dg = sg.D if sg is not None else D
