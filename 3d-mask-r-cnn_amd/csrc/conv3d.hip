@@ -5266,7 +5266,7 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t s, float* dx_halo = nullptr,
-                         int hlo = 0, bool v_ready = false, const Epi* fb = nullptr);
+                         int hlo = 0, bool v_ready = false, const Epi* fb = nullptr, int ny = 0);
 
 // The same two entry points for convs that share one kernel across calls (the
 // RPN head's rpn_conv_shared1 on P2..P6, core/models.py:512-557): with
@@ -5289,6 +5289,26 @@ extern "C" int m3d_conv3d_bwd_data_wino_v(const float* dz, const float* w, int64
                          0, v_ready != 0);
 }
 
+// tile_y: the data gradient's y tile for this call (2: F(2x2xNZ), 4: F(4x2xNZ);
+// 0: the library's, m3d_conv3d_wino_dgrad_tile_y).  The V region a v_ready
+// call reuses must have been transformed with the same tile_y.
+static int dgrad_tile_arg(int32_t tile_y, int& ny) {
+    if (tile_y != 0 && tile_y != 2 && tile_y != 4) return einval("conv3d winograd bwd-data: tile_y must be 0, 2 or 4");
+    ny = tile_y ? tile_y : wino_dgrad_ny();
+    return M3D_OK;
+}
+
+extern "C" int m3d_conv3d_bwd_data_wino_vy(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                           int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
+                                           int32_t accumulate, void* workspace, size_t ws_bytes, int32_t v_ready,
+                                           int32_t tile_y, m3d_stream_t s) {
+    int ny;
+    int rc = dgrad_tile_arg(tile_y, ny);
+    if (rc) return rc;
+    return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s), nullptr,
+                         0, v_ready != 0, nullptr, ny);
+}
+
 extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H,
                                         int64_t W, int64_t D, int64_t Cin, int64_t Cout,
                                         int64_t OD, int32_t pz, float* dx, int32_t accumulate,
@@ -5296,24 +5316,44 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
     return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s));
 }
 
+static int bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                            int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                            void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn, void* bn_ws,
+                            size_t bn_ws_bytes, int ny, hipStream_t hs) {
+    if (Cin % 256 != 0 && 256 % Cin != 0)
+        return einval("conv3d winograd bwd-data (fused BN backward): Cin must divide 256 or be a multiple of it");
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout))
+        return einval("conv3d winograd bwd-data (fused BN backward): batch past the 32-bit operand bound");
+    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, wino_dgrad_nz(), ny);
+    const int64_t rows = Cin % 256 == 0 ? g.T : (g.T * Cin + 255) / 256;
+    Epi e{};
+    int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
+    if (rc) return rc;
+    rc = bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, hs, nullptr, 0,
+                       v_ready != 0, &e, ny);
+    if (rc) return rc;
+    return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, hs);
+}
+
 extern "C" int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
                                            int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
                                            int32_t accumulate, void* workspace, size_t ws_bytes, int32_t v_ready,
                                            const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes,
                                            m3d_stream_t s) {
-    if (Cin % 256 != 0 && 256 % Cin != 0)
-        return einval("conv3d winograd bwd-data (fused BN backward): Cin must divide 256 or be a multiple of it");
-    if (wino_per_item(B, H, W, D, OD, Cin, Cout))
-        return einval("conv3d winograd bwd-data (fused BN backward): batch past the 32-bit operand bound");
-    const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, wino_dgrad_nz(), wino_dgrad_ny());
-    const int64_t rows = Cin % 256 == 0 ? g.T : (g.T * Cin + 255) / 256;
-    Epi e{};
-    int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
+    return bwd_data_wino_bn(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, v_ready, bn,
+                            bn_ws, bn_ws_bytes, wino_dgrad_ny(), st(s));
+}
+
+extern "C" int m3d_conv3d_bwd_data_wino_bny(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                            int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
+                                            int32_t accumulate, void* workspace, size_t ws_bytes, int32_t v_ready,
+                                            const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes, int32_t tile_y,
+                                            m3d_stream_t s) {
+    int ny;
+    int rc = dgrad_tile_arg(tile_y, ny);
     if (rc) return rc;
-    rc = bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s), nullptr, 0,
-                       v_ready != 0, &e);
-    if (rc) return rc;
-    return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, st(s));
+    return bwd_data_wino_bn(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, v_ready, bn,
+                            bn_ws, bn_ws_bytes, ny, st(s));
 }
 
 // the data-gradient output transform: dx over the (halo-extended) grid, or,
@@ -5369,7 +5409,7 @@ static void bwd_data_wino_launch(const float* dz, const float* w, const WinoGeom
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo, bool v_ready,
-                         const Epi* fb) {
+                         const Epi* fb, int ny_arg) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -5379,12 +5419,13 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
         for (int64_t b = 0; b < B; ++b) {
             rc = bwd_data_wino(dz + b * H * W * OD * Cout, w, 1, H, W, D, Cin, Cout, OD, pz, dx + b * H * W * dxd * Cin,
                                accumulate, workspace, ws_bytes, hs,
-                               dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo, v_ready || b > 0);
+                               dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo, v_ready || b > 0, nullptr,
+                               ny_arg);
             if (rc) return rc;
         }
         return M3D_OK;
     }
-    const int nz = wino_dgrad_nz(), ny = wino_dgrad_ny();
+    const int nz = wino_dgrad_nz(), ny = ny_arg ? ny_arg : wino_dgrad_ny();
     const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz, ny);
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
     const WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz, ny);

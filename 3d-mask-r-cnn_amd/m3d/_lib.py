@@ -85,6 +85,10 @@ _SIGS = {
                               c_i32, c_p, c_p, c_p, c_sz, c_i32, c_p],
     "m3d_conv3d_bwd_data_wino_v": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p,
                                    c_sz, c_i32, c_p],
+    "m3d_conv3d_bwd_data_wino_vy": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32,
+                                    c_p, c_sz, c_i32, c_i32, c_p],
+    "m3d_conv3d_bwd_data_wino_bny": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32,
+                                     c_p, c_sz, c_i32, c_p, c_p, c_sz, c_i32, c_p],
     "m3d_bn_bwd_fused_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "m3d_conv3d_bwd_data_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32,
                                c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,

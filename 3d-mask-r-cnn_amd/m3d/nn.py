@@ -260,6 +260,18 @@ WINO_MIN_C = 64
 WINO_WGRAD_MIN_C = 64
 
 
+# Layers whose Winograd data gradient runs on F(4x2x4) tiles instead of the
+# library's F(2x2x4) ('+'-separated layer names, "*" = all; round 5 moved every
+# data gradient to F(2x2x4) for gradient accuracy).
+WINO_DGRAD_Y4 = ""
+
+
+def _dgrad_tile_y(name):
+    if not WINO_DGRAD_Y4:
+        return 0
+    return 4 if WINO_DGRAD_Y4 == "*" or name in WINO_DGRAD_Y4.split("+") else 0
+
+
 def use_winograd(geo, cin, cout, in_sp):
     """'same' 3x3x3 stride-1 convs, or their z-halo-extended depth-slab form
     (z pad 0/1, input depth = output depth + halo planes)."""
@@ -988,6 +1000,7 @@ class _ConvBNAct(torch.autograd.Function):
                 dx, acc = _link_take(ctx.link, x)
                 if dx is None:
                     dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+                ty = 0 if halo is not None else _dgrad_tile_y(ctx.name)
                 if halo is not None:
                     dh = torch.empty_like(halo[0])
                     check(L.m3d_conv3d_bwd_data_wino_halo(ptr(dz), ptr(w), halo[1], halo[2], B, H, W, D, Cin,
@@ -997,7 +1010,7 @@ class _ConvBNAct(torch.autograd.Function):
                 else:
                     if ctx.wshare is not None:      # may be held across calls: not the arena
                         ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
-                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout))
+                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout, ty))
                     rec = ctx.fuse_in
                     if (rec is not None and rec.armed and (Cin % 256 == 0 or 256 % Cin == 0)
                             and not _per_item(B, H * W * max(D, OD), max(Cin, Cout), 0, 0)
@@ -1005,19 +1018,19 @@ class _ConvBNAct(torch.autograd.Function):
                         dres_f = torch.empty_like(x) if rec.need_res else None
                         bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
                         d = rec.descriptor(dres_f)
-                        check(L.m3d_conv3d_bwd_data_wino_bn(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD, geo.pad[2],
-                                                            ptr(dx), acc, ptr(ws), wsb, v_ready, ctypes.addressof(d),
-                                                            ptr(bws), bwsb, stream()), "conv3d_bwd_data_wino_bn")
+                        check(L.m3d_conv3d_bwd_data_wino_bny(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD, geo.pad[2],
+                                                             ptr(dx), acc, ptr(ws), wsb, v_ready, ctypes.addressof(d),
+                                                             ptr(bws), bwsb, ty, stream()), "conv3d_bwd_data_wino_bn")
                         rec.buf, rec.dres, rec.done = dx, dres_f, True
                         fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
                     else:
-                        check(L.m3d_conv3d_bwd_data_wino_v(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
-                                                           geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready,
-                                                           stream()), "conv3d_bwd_data_wino")
+                        check(L.m3d_conv3d_bwd_data_wino_vy(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                            geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, ty,
+                                                            stream()), "conv3d_bwd_data_wino")
                     _shared_wino_release(ctx.wshare)
                 if logging:
                     _log("wino_dgrad", direct, _wino_exec(B, OH, OW, OD, Cin, Cout, int(L.m3d_conv3d_wino_dgrad_tile_z()),
-                                                          int(L.m3d_conv3d_wino_dgrad_tile_y())),
+                                                          ty or int(L.m3d_conv3d_wino_dgrad_tile_y())),
                          4.0 * (dz.numel() + w.numel() + x.numel() * (1 + acc) + fused_nel), "bwd_data", ctx.name,
                          td, "x3")
                 dx = _link_park(ctx.link, dx, acc)

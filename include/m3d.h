@@ -459,6 +459,18 @@ int m3d_conv3d_bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int6
                                 int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                                 void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn,
                                 void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s);
+/* The two data-gradient forms above with the y tile chosen per call: tile_y 2
+ * (F(2x2xNZ), the library default: m3d_conv3d_wino_dgrad_tile_y) or 4
+ * (F(4x2xNZ): 4.5 instead of 6 points per output, ~4x the point GEMMs'
+ * rounding carried into dx), 0 = the default.  A v_ready call must reuse a V
+ * transformed with the same tile_y. */
+int m3d_conv3d_bwd_data_wino_vy(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                                void* workspace, size_t ws_bytes, int32_t v_ready, int32_t tile_y, m3d_stream_t s);
+int m3d_conv3d_bwd_data_wino_bny(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                 int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                                 void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn, void* bn_ws,
+                                 size_t bn_ws_bytes, int32_t tile_y, m3d_stream_t s);
 /* m3d_conv3d_bwd_data_x3 (a 1x1x1 stride-1 conv's data gradient on the
  * bf16-split GEMM, accumulate 0) with m3d_conv3d_bwd_data_bn's fused BN-ReLU
  * backward in the GEMM's epilogue; bn_ws: m3d_bn_bwd_fused_workspace_bytes. */

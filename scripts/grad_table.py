@@ -25,6 +25,11 @@ VARIANTS = {
     "wino_min128": {"WINO_MIN_C": 128},          # the 64-channel res2 2b convs direct
     "wino_min256": {"WINO_MIN_C": 256},          # res2 + res3 2b direct
     "no_wino": {"WINOGRAD": False},              # every 3^3 conv direct (accuracy floor of the kernels)
+    # round 5: the data gradient's y tile per layer (nn.WINO_DGRAD_Y4; F(2x2x4) default)
+    "y4_all": {"WINO_DGRAD_Y4": "*"},
+    "y4_shared1": {"WINO_DGRAD_Y4": "rpn_conv_shared1"},
+    "y4_p2": {"WINO_DGRAD_Y4": "rpn_conv_shared1+fpn_p2"},
+    "y4_fpn": {"WINO_DGRAD_Y4": "rpn_conv_shared1+fpn_p2+fpn_p3+fpn_p4+fpn_p5"},
 }
 
 
