@@ -369,10 +369,16 @@ class X3Planes:
     def refresh(self, dev):
         """Split every registered kernel on ``dev`` (current stream) and go live."""
         dev = self._dev(dev)
+        capturing = torch.cuda.is_current_stream_capturing()
         es = self._alive(dev)
         if es:
             key = tuple((ptr(e[0]()), ptr(e[3]), ptr(e[4])) for e in es)
             t = self.tables.get(dev)
+            if capturing and (t is None or t[3] != key):
+                # the table would need a host-to-device copy, illegal under graph
+                # capture: this pass splits per conv instead (correct, unbatched)
+                self.live = False
+                return
             if t is None or t[3] != key:
                 items = (_lib.X3PlanesItem * len(es))(*[_lib.X3PlanesItem(ptr(e[0]()), ptr(e[3]), ptr(e[4]), e[1], e[2])
                                                         for e in es])
