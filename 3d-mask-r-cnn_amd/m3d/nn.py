@@ -526,7 +526,7 @@ class BiasSums:
 
     def add(self, x, M, C, out):
         if any(o is out or o.data_ptr() == out.data_ptr() for _, _, _, o in self.items) \
-                or len(self.items) >= _lib.COL_SUMS_MAX:
+                or len(self.items) >= min(_lib.COL_SUMS_MAX, BIAS_BATCH_MAX):
             self.flush()
         self.items.append((x, M, C, out))
 
@@ -555,8 +555,13 @@ BIAS_BATCH = None
 # neutral (26.34 vs 26.32 ms, 655 vs 679 launches per step), but the HIP-graph
 # replay of the step slows from 26.0-26.2 to 30.6-30.7 ms with it on; under
 # rocprofv3 the batched replay shows no such loss (its queue assignment is the
-# clean one, r05gtrace2), so the cause is not found -- off until it is.
+# clean one, r05gtrace2), so the cause is not found -- off until it is.  Ruled
+# out (scripts/gpu_r05_bias2.sh / _bias3.sh): where the flushes land (batches of
+# 2 / 4 / 16: all 30.1-30.2 ms) and the item table's kernel-argument size (a
+# 4-item build: 30.1 ms).
 BIAS_BATCHED = False
+# most items per batched launch (flushed when full; A/B of where the flushes land)
+BIAS_BATCH_MAX = 16
 
 
 def bias_grad(dy, M, C, out, grads=None, batch=None):

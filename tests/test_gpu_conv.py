@@ -644,12 +644,19 @@ def test_col_sums_batched_matches_per_unit(cuda):
     for x, r, (m, c) in zip(xs, ref, shapes):
         nn.bn_act_bwd(x, None, None, m, c, False, None, None, None, None, None, None, None, r)
     out = [b.clone() for b in base]
-    arr = (_lib.ColSumsItem * len(shapes))(*[_lib.ColSumsItem(x.data_ptr(), m, c, o.data_ptr())
-                                             for x, o, (m, c) in zip(xs, out, shapes)])
-    wsb = int(L.m3d_col_sums_batched_workspace_bytes(arr, len(shapes)))
-    ws = torch.empty(wsb // 4 + 1, device=cuda)
-    _lib.check(L.m3d_col_sums_batched(arr, len(shapes), ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
+    n_max = _lib.COL_SUMS_MAX
+    for i0 in range(0, len(shapes), n_max):                 # batches of at most M3D_COL_SUMS_MAX items
+        sl = slice(i0, i0 + n_max)
+        arr = (_lib.ColSumsItem * len(shapes[sl]))(*[_lib.ColSumsItem(x.data_ptr(), m, c, o.data_ptr())
+                                                     for x, o, (m, c) in zip(xs[sl], out[sl], shapes[sl])])
+        wsb = int(L.m3d_col_sums_batched_workspace_bytes(arr, len(arr)))
+        ws = torch.empty(wsb // 4 + 1, device=cuda)
+        _lib.check(L.m3d_col_sums_batched(arr, len(arr), ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
     torch.cuda.synchronize()
+    over = (_lib.ColSumsItem * (n_max + 1))(*[_lib.ColSumsItem(xs[1].data_ptr(), 4, 256, o.data_ptr())
+                                             for o in [torch.empty(256, device=cuda) for _ in range(n_max + 1)]])
+    with pytest.raises(ValueError):
+        _lib.check(L.m3d_col_sums_batched(over, n_max + 1, ws.data_ptr(), wsb, _lib.stream()), "col_sums_batched")
     for x, o, r, b in zip(xs, out, ref, base):
         assert torch.equal(o, r)
         want = b.double() + x.double().sum(0)
