@@ -557,11 +557,16 @@ BIAS_BATCH = None
 # rocprofv3 the batched replay shows no such loss (its queue assignment is the
 # clean one, r05gtrace2), so the cause is not found -- off until it is.  Ruled
 # out (scripts/gpu_r05_bias2.sh / _bias3.sh): where the flushes land (batches of
-# 2 / 4 / 16: all 30.1-30.2 ms) and the item table's kernel-argument size (a
-# 4-item build: 30.1 ms).
+# 2 / 4 / 16: all 30.1-30.2 ms), the item table's kernel-argument size (a
+# 4-item build: 30.1 ms) and which units are deferred (the FPN's alone, or the
+# RPN heads' one sum alone: 29.9-30.0 ms) -- one reduction moved from the
+# backward to finish_backward is enough.
 BIAS_BATCHED = False
 # most items per batched launch (flushed when full; A/B of where the flushes land)
 BIAS_BATCH_MAX = 16
+# which bias-only units join the batch: the FPN convs ("fpn") and / or the RPN
+# class / bbox heads ("rpn")
+BIAS_BATCH_UNITS = "fpn+rpn"
 
 
 def bias_grad(dy, M, C, out, grads=None, batch=None):
@@ -940,7 +945,8 @@ class _ConvBNAct(torch.autograd.Function):
             dz = dy
             dres = dy if need_res else None
             if grads.get("bias") is not None:
-                bias_grad(dy, M, Cout, grads["bias"], grads, ctx.bias_batch)
+                bias_grad(dy, M, Cout, grads["bias"], grads,
+                          ctx.bias_batch if "fpn" in BIAS_BATCH_UNITS.split("+") else None)
         else:
             if rec is not None:
                 rec.clear()
@@ -1422,7 +1428,8 @@ class _RPNOut(torch.autograd.Function):
                 (0, npad - n_out))
             if grads.get("bias") is not None:
                 # all levels' rows at once (one column sum of the level-concatenated matrix)
-                bias_grad(dz_all, R, npad, grads["bias"], grads, ctx.bias_batch)
+                bias_grad(dz_all, R, npad, grads["bias"], grads,
+                          ctx.bias_batch if "rpn" in BIAS_BATCH_UNITS.split("+") else None)
             off = 0
             for li, (s, r) in enumerate(zip(shared, rows)):
                 xb = s[b:b + 1]
