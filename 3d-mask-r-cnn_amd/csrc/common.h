@@ -153,6 +153,11 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3W_OCC
 #define M3D_TUNE_X3W_OCC 2
 #endif
+// the x3 GEMMs' two accumulator tiles per A fragment issued interleaved
+// (x3_mac_pair; 0: one tile's six-MFMA chain after the other)
+#ifndef M3D_TUNE_X3_PAIR
+#define M3D_TUNE_X3_PAIR 1
+#endif
 #ifndef M3D_TUNE_X3_AF128
 #define M3D_TUNE_X3_AF128 0
 #endif

@@ -223,6 +223,34 @@ __device__ __forceinline__ void x3_mac(floatx16& acc, const bf16x8& ah, const bf
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
     }
 }
+// x3_mac of two accumulator tiles sharing the A fragment, their two six-MFMA
+// chains interleaved (M3D_TUNE_X3_PAIR): each accumulator sees its products in
+// x3_mac's order (bit-identical results), but consecutive MFMAs are independent,
+// so an MFMA does not wait for its predecessor's result.
+template <int X3ACC>
+__device__ __forceinline__ void x3_mac_pair(floatx16& acc0, floatx16& acc1, const bf16x8& ah, const bf16x8& am,
+                                            const bf16x8& al, const bf16x8& b0h, const bf16x8& b0m,
+                                            const bf16x8& b0l, const bf16x8& b1h, const bf16x8& b1m,
+                                            const bf16x8& b1l) {
+    if constexpr (X3ACC == 1 || !M3D_TUNE_X3_PAIR) {
+        x3_mac<X3ACC>(acc0, ah, am, al, b0h, b0m, b0l);
+        x3_mac<X3ACC>(acc1, ah, am, al, b1h, b1m, b1l);
+    } else {
+        floatx16 c0 = acc0, c1 = acc1;
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b0h, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b1h, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0m, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1m, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0l, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1l, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0h, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1h, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0m, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1m, c1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0h, c0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1h, c1, 0, 0, 0);
+    }
+}
 // x3_mac over a wave's TM x TN accumulator tiles with fragments af[i][plane],
 // bf[j][plane].  X3ACC 1: a lag-1 pipeline -- tile q's six MFMAs issue beside
 // tile q-1's VALU add, a scheduling barrier per tile keeps two step partials
@@ -1642,14 +1670,14 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
             bf16x8 af[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) af[pl] = w2_frag(S + pl * W2_PL + i * 64, abase, abase + 4 * W2_PITCH);
+            if (DBG == 2 || DBG == 5) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (DBG == 2 || DBG == 5) {
+                for (int j = 0; j < 2; ++j)
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
-                    continue;
-                }
-                x3_mac<X3ACC_WG>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
+                continue;
             }
+            x3_mac_pair<X3ACC_WG>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+                                  bfr[1][0], bfr[1][1], bfr[1][2]);
         }
     };
     // two named register sets (static indexing): X carries step kt+1 (loaded
@@ -2866,14 +2894,14 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(S + pl * G2_PL + off);
             // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
+            if (DBG == 2 || DBG == 4) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (DBG == 2 || DBG == 4) {
+                for (int j = 0; j < 2; ++j)
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
-                    continue;
-                }
-                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
+                continue;
             }
+            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+                                    bfr[1][0], bfr[1][1], bfr[1][2]);
         }
     }
     if (DBG == 1 || DBG == 4) {   // keep the accumulators live, store nothing
@@ -3044,10 +3072,8 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
             bf16x8 af[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
-            }
+            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+                                    bfr[1][0], bfr[1][1], bfr[1][2]);
         }
 #if M3D_TUNE_X3AF & 2
         __builtin_amdgcn_s_setprio(0);
@@ -3295,10 +3321,8 @@ __global__ __launch_bounds__(256, 2) void x3_gemm_af128_kernel(X3G g) {
             bf16x8 af[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G3_PLA + off);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                x3_mac<X3ACC_GEMM>(acc[i][j], af[0], af[1], af[2], bfr[j][0], bfr[j][1], bfr[j][2]);
-            }
+            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+                                    bfr[1][0], bfr[1][1], bfr[1][2]);
         }
     };
     for (int kt = 0;;) {
