@@ -37,8 +37,11 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6
 X3_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
 # the step's largest kernel by time in the rocprof table of this tree
 # (profiles/dominant_kernel_table.txt, line 1): the headline `roofline` prices
-# its largest launch
-DOMINANT_KERNEL = "x3_wgrad_tr_kernel"
+# its largest launch.  Round 5's interleaved MFMA chains (x3_mac_pair) took the
+# weight-gradient GEMM below the Winograd point GEMM (profiles/r05prof2_*:
+# x3_gemm256_af_kernel 6.92, x3_wgrad_tr_kernel 6.43 ms per step); the other is
+# reported beside it (roofline.wgrad_gemm)
+DOMINANT_KERNEL = "x3_gemm256_af_kernel"
 
 
 class LegWatchdog:
