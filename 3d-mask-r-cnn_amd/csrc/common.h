@@ -155,6 +155,10 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #endif
 // the x3 GEMMs' two accumulator tiles per A fragment issued interleaved
 // (x3_mac_pair; 0: one tile's six-MFMA chain after the other)
+// x3_gemm256_af_kernel: two A rows' fragments per step, four chains interleaved (A/B)
+#ifndef M3D_TUNE_X3_QUAD
+#define M3D_TUNE_X3_QUAD 0
+#endif
 #ifndef M3D_TUNE_X3_PAIR
 #define M3D_TUNE_X3_PAIR 1
 #endif

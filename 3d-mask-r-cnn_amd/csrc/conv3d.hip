@@ -3066,6 +3066,30 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #if M3D_TUNE_X3AF & 2
         __builtin_amdgcn_s_setprio(1);
 #endif
+#if M3D_TUNE_X3_QUAD
+        // two A rows' fragments at once: four independent six-MFMA chains interleaved
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            bf16x8 af[2][3];
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii) {
+                const int off = x3_off16(wm * 128 + (i + ii) * 32 + l32, h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) af[ii][pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
+            }
+            floatx16 c00 = acc[i][0], c01 = acc[i][1], c10 = acc[i + 1][0], c11 = acc[i + 1][1];
+            // per accumulator x3_mac's order: (l,h) (m,m) (h,l) (m,h) (h,m) (h,h)
+            const int pa[6] = {2, 1, 0, 1, 0, 0}, pb[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][pa[t]], bfr[0][pb[t]], c00, 0, 0, 0);
+                c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][pa[t]], bfr[1][pb[t]], c01, 0, 0, 0);
+                c10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][pa[t]], bfr[0][pb[t]], c10, 0, 0, 0);
+                c11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][pa[t]], bfr[1][pb[t]], c11, 0, 0, 0);
+            }
+            acc[i][0] = c00; acc[i][1] = c01; acc[i + 1][0] = c10; acc[i + 1][1] = c11;
+        }
+#else
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int off = x3_off16(wm * 128 + i * 32 + l32, h);
@@ -3075,6 +3099,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
             x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
                                     bfr[1][0], bfr[1][1], bfr[1][2]);
         }
+#endif
 #if M3D_TUNE_X3AF & 2
         __builtin_amdgcn_s_setprio(0);
 #endif
