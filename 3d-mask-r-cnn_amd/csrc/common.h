@@ -156,6 +156,13 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // the x3 GEMMs' two accumulator tiles per A fragment issued interleaved
 // (x3_mac_pair; 0: one tile's six-MFMA chain after the other)
 // x3_gemm256_af_kernel: two A rows' fragments per step, four chains interleaved (A/B)
+// x3_mac_tiles (the 128x128 x3 GEMMs: small-channel Winograd point GEMMs and
+// weight gradients): tile pairs' chains interleaved -- 128^3 step 25.61-25.66
+// vs 25.76-25.85 ms (graph), 25.63-25.64 vs 25.76-25.82 eager, same box
+// (scripts/gpu_r05_pt.sh); bit-identical per accumulator
+#ifndef M3D_TUNE_X3_PAIR_TILES
+#define M3D_TUNE_X3_PAIR_TILES 1
+#endif
 #ifndef M3D_TUNE_X3_QUAD
 #define M3D_TUNE_X3_QUAD 0
 #endif

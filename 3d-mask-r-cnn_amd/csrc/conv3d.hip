@@ -281,6 +281,13 @@ __device__ __forceinline__ void x3_mac_tiles(floatx16 (&acc)[TM][TN], const bf16
             __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (LAG) acc[TM - 1][TN - 1] += pend;
+    } else if constexpr (TN % 2 == 0 && M3D_TUNE_X3_PAIR_TILES) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; j += 2)
+                x3_mac_pair<0>(acc[i][j], acc[i][j + 1], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2],
+                               bf[j + 1][0], bf[j + 1][1], bf[j + 1][2]);
     } else {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
