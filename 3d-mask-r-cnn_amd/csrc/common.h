@@ -68,8 +68,13 @@ inline unsigned grid_for(int64_t n, int per_block, int64_t cap = 1 << 30) {
 // kernel that loads the next step's global operands before a barrier pays a
 // full memory round trip per step with it.  Use only where the barrier orders
 // LDS traffic alone (global results are not read by other waves after it).
+// A workgroup barrier with release / acquire fences limited to LDS ("local"
+// MMRA): the compiler knows it as a convergent barrier and orders LDS accesses
+// around it, and it emits only lgkmcnt(0) + s_barrier (no vmcnt wait).
 __device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }

@@ -3015,17 +3015,40 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         else if constexpr (decltype(st)::v == 1) return sB1;
         else return sB2;
     };
+#ifndef M3D_X3AF_KB
+#define M3D_X3AF_KB 0
+#endif
+#if M3D_X3AF_KB   // timing probe: k-blocked addressing (wrong values)
+    const __amdgpu_buffer_rsrc_t rak = make_rsrc(g.af + bz * g.bsa, (uint64_t)g.M * g.K * 4);
+    __amdgpu_buffer_rsrc_t rbk[3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) rbk[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb, (uint64_t)g.N * g.K * 2);
+#endif
     auto load_a = [&](int kt, float4 (&v)[2]) {
         const bool in = kt < nk;
+#if M3D_X3AF_KB & 2
+        const uint32_t o = ((uint32_t)(kt * g.M + m0 + arow) * 16u + (uint32_t)ach * 8u) * 4u;
+        v[0] = bload4(rak, in ? o : M3D_OOB);
+        v[1] = bload4(rak, in ? o + 16u : M3D_OOB);
+#else
         const uint32_t o = aoff0 + (uint32_t)kt * (G2_BK * 4);
         v[0] = bload4(ra, in ? o : M3D_OOB);
         v[1] = bload4(ra, in ? o + 16u : M3D_OOB);
+#endif
     };
     auto dma_b = [&](auto st, int kt) {
         char* S = stB(st) + wave * 1024;
+#if M3D_X3AF_KB & 1
+        const uint32_t off = kt < nk ? ((uint32_t)(kt * g.N + n0 + lrow) * 16u) * 2u +
+                                           (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4)
+                                     : M3D_OOB;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) g2_dma(rbk[pl], S + pl * G2_PL, off);
+#else
         const uint32_t off = kt < nk ? lsrc + (uint32_t)kt * (G2_BK * 2) : M3D_OOB;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G2_PL, off);
+#endif
     };
     auto split_a = [&](auto st, const float4 (&v)[2]) {
         char* S = stA(st) + awr;
@@ -4857,7 +4880,8 @@ extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t 
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     if (wino_per_item(B, H, W, D, OD, Cin, Cout)) B = 1;     // run one batch item at a time
     size_t best = 0;
-    const int tiles[3][2] = {{wino_nz(), WNY}, {wino_wgrad_nz(), WNY}, {wino_dgrad_nz(), wino_dgrad_ny()}};
+    // the data gradient's y tile is a per-call argument (m3d_conv3d_bwd_data_wino_vy / _bny): both sizes
+    const int tiles[4][2] = {{wino_nz(), WNY}, {wino_wgrad_nz(), WNY}, {wino_dgrad_nz(), 2}, {wino_dgrad_nz(), 4}};
     for (const auto& zy : tiles) {
         const int nz = zy[0], ny = zy[1];
         const WinoGeom g = wino_geom(B, H, W, D > OD ? D : OD, D, 1, nz, ny);
@@ -4875,6 +4899,23 @@ extern "C" size_t m3d_conv3d_wino_workspace_bytes(int64_t B, int64_t H, int64_t 
 }
 
 struct WinoWs { float *V, *U, *M, *WT; };
+// bytes wino_ws lays out for geometry g, operand widths C1 (U) / C2 (M) and the tile (nz, ny)
+static size_t wino_ws_need(const WinoGeom& g, int64_t C1, int64_t C2, int nz, int ny) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t P = (size_t)wino_points(nz, ny);
+    const size_t eb = gemm_x3_env() ? 6 : 4;
+    const size_t wt = gemm_x3_env() ? al(sizeof(float) * 27 * (size_t)C1 * C2) : 0;
+    return wt + al(eb * P * (size_t)C1 * C2) + al(eb * P * (size_t)g.T * C1) + al(4 * P * (size_t)g.T * C2);
+}
+// the data gradient's own workspace at tile_y (0: the library default): the
+// layout bwd_data_wino checks (dz transformed over Cout, dx's points over Cin)
+extern "C" size_t m3d_conv3d_wino_dgrad_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD,
+                                                        int64_t Cin, int64_t Cout, int32_t tile_y) {
+    if (tile_y != 0 && tile_y != 2 && tile_y != 4) return 0;
+    if (wino_per_item(B, H, W, D, OD, Cin, Cout)) B = 1;
+    const int nz = wino_dgrad_nz(), ny = tile_y ? tile_y : wino_dgrad_ny();
+    return wino_ws_need(wino_geom(B, H, W, D, OD, 1, nz, ny), Cout, Cin, nz, ny);
+}
 // [WT: X3 only, the transposed kernel][V][U][M]
 static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, int nz = -1, int ny = WNY) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -5468,8 +5509,6 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
                          const Epi* fb, int ny_arg) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
-    if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
-        return einval("conv3d winograd: workspace too small");
     if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {
         const int64_t dxd = dx_halo ? OD : D;          // dx depth: the slab's interior, or the full grid
         for (int64_t b = 0; b < B; ++b) {
@@ -5483,6 +5522,9 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
     }
     const int nz = wino_dgrad_nz(), ny = ny_arg ? ny_arg : wino_dgrad_ny();
     const WinoGeom g = wino_geom(B, H, W, D, OD, 2 - pz, nz, ny);
+    // the layout this call uses (its tile_y may differ from the library's default)
+    if (ws_bytes < wino_ws_need(g, Cout, Cin, nz, ny))
+        return einval("conv3d winograd: workspace too small");
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
     const WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz, ny);
     const int ci = (int)Cin, co = (int)Cout, dl = (int)OD;

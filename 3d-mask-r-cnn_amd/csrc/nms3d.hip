@@ -296,7 +296,7 @@ __global__ __launch_bounds__(1024) void nms_reduce_pf_kernel(const uint64_t* __r
                 if (nk >= max_out || vmask != ~0ull) stop_sh = 1;
             }
         }
-        lds_barrier();              // (the prefetched rows stay in flight)
+        lds_barrier();              // orders LDS only (kept_sh / stop_sh); the prefetched rows stay in flight
         if (stop_sh) return false;
         const uint64_t kept = kept_sh;
         uint64_t acc = 0;
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(1024) void nms_reduce_pf_kernel(const uint64_t* __r
             if (r < 64 && ((kept >> r) & 1ull)) acc |= cur[k];
         }
         if (own && acc) atomicOr((unsigned long long*)&removed[w], (unsigned long long)acc);
-        lds_barrier();
+        lds_barrier();              // orders LDS only (removed[])
         return true;
     };
     for (int64_t blk = 0; blk < cb; blk += 2) {

@@ -127,6 +127,7 @@ _SIGS = {
     "m3d_conv3d_wino_tile_z": [],
     "m3d_conv3d_wino_wgrad_tile_z": [],
     "m3d_conv3d_wino_tile_y": [],
+    "m3d_conv3d_wino_dgrad_workspace_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32],
     "m3d_conv3d_wino_dgrad_tile_y": [],
     "m3d_conv3d_wino_dgrad_tile_z": [],
     "m3d_conv3d_fwd_wino_keep": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
@@ -195,7 +196,7 @@ _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_s
              "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_rpn_loss_workspace_bytes": c_sz,
-             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz,
+             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz, "m3d_conv3d_wino_dgrad_workspace_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
              "m3d_conv3d_wino_tile_y": c_i32, "m3d_conv3d_wino_dgrad_tile_y": c_i32,
              "m3d_conv3d_wino_dgrad_tile_z": c_i32, "m3d_col_sums_batched_workspace_bytes": c_sz}

@@ -106,8 +106,7 @@ class ResNet3D:
         # BN_AFFINE_BATCHED False: one m3d_bn_affine per BN conv unit, A/B)
         if not BN_AFFINE_BATCHED:
             return self._forward(image)
-        self.store.bn_affine_refresh()
-        self.store.bn_aff_live = True
+        self.store.bn_aff_live = self.store.bn_affine_refresh()
         try:
             return self._forward(image)
         finally:

@@ -332,6 +332,22 @@ def _conv1_x3(xshape, geo, K, N, bwd_data=False):
     return -(-B * H * W * Dg // 256) * (N // 256) >= (CONV1_X3_DGRAD_TILES if bwd_data else CONV1_X3_FWD_TILES)
 
 
+def _check_generations(ctx):
+    """Ordering contract of the batched per-forward buffers (ParamStore's BN
+    affine, X3Planes): a conv unit's backward reads the affine / split planes
+    its forward used, which live in buffers the NEXT model forward refreshes in
+    place.  A backward that runs after another forward (retain_graph double
+    backward, accumulation across an update) would silently use the newer
+    values, so it raises instead."""
+    g = ctx.aff_gen
+    if g is not None and g[0].bn_gen != g[1]:
+        raise RuntimeError("conv backward after another model forward: the batched BN affine this unit's "
+                           "forward used was refreshed (run each backward before the next forward)")
+    if ctx.x3_gen is not None and X3_PLANES.gen != ctx.x3_gen:
+        raise RuntimeError("conv backward after another model forward: the split planes this unit's "
+                           "forward used were refreshed (run each backward before the next forward)")
+
+
 class X3Planes:
     """The bf16-split planes of the 1x1x1 kernels that run on the split GEMM
     (m3d_conv1_x3_planes), refreshed for all of them by ONE launch per model
@@ -354,6 +370,7 @@ class X3Planes:
         self.entries = {}            # (ptr, numel) -> [weakref(w), cin, cout, fwd, bwd, valid]
         self.tables = {}             # device -> (device item table, n, max_el, key)
         self.live = False
+        self.gen = 0                 # refreshes that rewrote the planes (_check_generations)
         self.hits = self.misses = 0  # refreshed planes taken / per-conv splits while live (tests)
 
     @staticmethod
@@ -385,6 +402,7 @@ class X3Planes:
                 host = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
                 t = self.tables[dev] = (host.to(dev), len(es), max(e[1] * e[2] for e in es), key)
             check(_L().m3d_conv1_x3_planes_batched(ptr(t[0]), t[1], t[2], stream()), "conv1_x3_planes_batched")
+            self.gen += 1
             for e in es:
                 e[5] = True
         self.live = True
@@ -791,6 +809,9 @@ class _ConvBNAct(torch.autograd.Function):
         if bn is not None:
             gamma, beta, mean, var, eps = bn[:5]
             aff = bn[5] if len(bn) > 5 else None
+            # the batched affine is a view into the store's shared buffer: the next
+            # refresh overwrites it (checked in backward, _check_generations)
+            ctx.aff_gen = bn[6] if len(bn) > 6 else None
             if aff is None:
                 aff = torch.empty((3, Cout), device=x.device, dtype=torch.float32)
                 check(_L().m3d_bn_affine(ptr(gamma), ptr(beta), ptr(mean), ptr(var), float(eps), Cout,
@@ -801,6 +822,7 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.bn = (mean, rstd, scale)
         else:
             ctx.bn = None
+            ctx.aff_gen = None
         ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
         if halo is not None and not ctx.wino and not _stem_halo(geo, Cin, Cout, res_mode):
             raise ValueError("halo planes are read by the Winograd kernels and the stem only")
@@ -891,6 +913,7 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.x3_bwd = X3_PLANES.cached(w, False)
             if ctx.x3_bwd is None:
                 X3_PLANES.ensure(w, Cin, Cout)
+        ctx.x3_gen = X3_PLANES.gen if ctx.x3_bwd is not None else None
         ctx.bias_batch = BIAS_BATCH if grads is not None else None
         ctx.link = link
         ctx.res_shape = None if residual is None else tuple(residual.shape)
@@ -912,6 +935,7 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _check_generations(ctx)
         x, w, y, z = ctx.saved_tensors
         dy = dy.contiguous()
         geo, grads = ctx.geo, ctx.grads or {}
@@ -1211,7 +1235,8 @@ def conv_bn_act(x, layer, geo, relu, residual=None, res_mode=0, bn=None, need_dx
         # the model forward's batched affine (ParamStore.bn_affine_refresh) when current
         st = getattr(bn, "store", None)
         aff = bn.aff if st is not None and st.bn_aff_live else None
-        bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps, aff)
+        bnt = (bn.gamma.data, bn.beta.data, bn.moving_mean, bn.moving_variance, bn.eps, aff,
+               (st, st.bn_gen) if aff is not None else None)
     if residual is not None:
         residual = residual.contiguous()
     halo = None

@@ -63,6 +63,7 @@ class ParamStore:
         # bn.aff are current while bn_aff_live is set (a model forward's span)
         self._bn_items = self._bn_key = None
         self.bn_aff_live = False
+        self.bn_gen = 0            # refreshes of the shared affine buffer (nn._check_generations)
         self.by_name = {}
         self.flat = self.grad_flat = self.moments = None
 
@@ -127,12 +128,18 @@ class ParamStore:
         """(rstd, scale, shift) of every BN layer into bn.aff by ONE launch of
         m3d_bn_affine_batched on the current stream (was one m3d_bn_affine per
         BN conv unit per forward).  The descriptor table is built once and
-        rebuilt if any parameter / statistics buffer moved."""
+        rebuilt if any parameter / statistics buffer moved.  Returns whether
+        bn.aff is current: under HIP-graph capture a missing / stale table
+        cannot be rebuilt (a pageable host-to-device copy), so the forward then
+        runs each unit's own m3d_bn_affine instead (as X3Planes.refresh)."""
         from . import _lib
+        import torch
         if not self.bns:
-            return
+            return False
         key = tuple((bn.gamma.data.data_ptr(), bn.beta.data.data_ptr(), bn.moving_mean.data_ptr(),
                      bn.moving_variance.data_ptr()) for bn in self.bns)
+        if (self._bn_items is None or key != self._bn_key) and torch.cuda.is_current_stream_capturing():
+            return False
         if self._bn_items is None or key != self._bn_key:
             dev = self.bns[0].gamma.data.device
             total = sum(3 * bn.c for bn in self.bns)
@@ -152,6 +159,8 @@ class ParamStore:
         L = _lib.load()
         _lib.check(L.m3d_bn_affine_batched(self._bn_items.data_ptr(), len(self.bns), self._bn_max_c,
                                            _lib.stream()), "bn_affine_batched")
+        self.bn_gen += 1
+        return True
 
     def state_dict(self):
         d = {p.name: p.data.detach().cpu().clone() for p in self.params}

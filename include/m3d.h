@@ -378,6 +378,12 @@ int32_t m3d_conv3d_wino_tile_y(void);   /* output tile rows along y (2: F(2,3), 
  * gradients every earlier layer receives */
 int32_t m3d_conv3d_wino_dgrad_tile_y(void);
 int32_t m3d_conv3d_wino_dgrad_tile_z(void);
+/* Workspace of one data-gradient call at tile_y (0, 2, 4; 0 = the default):
+ * the layout m3d_conv3d_bwd_data_wino(_v, _vy, _bn, _bny) check against
+ * (m3d_conv3d_wino_workspace_bytes covers every tile; this is the exact need).
+ * 0 for an invalid tile_y. */
+size_t m3d_conv3d_wino_dgrad_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t D, int64_t OD,
+                                             int64_t Cin, int64_t Cout, int32_t tile_y);
 size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin);
 int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
                              const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,

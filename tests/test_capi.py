@@ -168,3 +168,26 @@ def test_det_argument_is_validated():
     for d in (lib.Det(1, None, 1 << 20), lib.Det(1, 1 << 20, 64), lib.Det(1, (1 << 20) + 4, 1 << 20)):
         rc = L.m3d_gemm_wgrad_f32(None, None, None, 1, 4, 4, 4, ctypes.addressof(d), None)
         assert rc == -1 and b"det->scratch" in L.m3d_last_error()
+
+
+def test_wino_dgrad_workspace_follows_the_call_tile():
+    """a data-gradient call's tile_y sets its U / M layout, so its
+    workspace check must use that tile, not the library default.  The
+    workspace function covers both tiles; a tile_y = 2 call with a workspace
+    sized for tile_y = 4 (fewer tiles x points) is rejected before any launch."""
+    import m3d._lib as lib
+    L = lib.load()
+    for (B, H, W, D, C1, C2) in ((1, 32, 32, 128, 256, 512), (1, 8, 8, 8, 64, 64), (2, 16, 16, 32, 128, 128)):
+        nb = L.m3d_conv3d_wino_workspace_bytes(B, H, W, D, D, C1, C2)
+        n2 = L.m3d_conv3d_wino_dgrad_workspace_bytes(B, H, W, D, D, C1, C2, 2)
+        n4 = L.m3d_conv3d_wino_dgrad_workspace_bytes(B, H, W, D, D, C1, C2, 4)
+        assert n2 > 0 and n4 > 0 and nb >= max(n2, n4)
+        assert L.m3d_conv3d_wino_dgrad_workspace_bytes(B, H, W, D, D, C1, C2, 3) == 0
+        small, big = sorted((n2, n4))
+        ty_big = 2 if n2 > n4 else 4
+        fake = ctypes.c_void_p(0x1000)
+        rc = L.m3d_conv3d_bwd_data_wino_vy(fake, fake, B, H, W, D, C1, C2, D, 1, fake, 0, fake, small, 0,
+                                           ty_big, None)
+        assert rc == -1 and b"workspace too small" in L.m3d_last_error()
+        rc = L.m3d_conv3d_bwd_data_wino_vy(fake, fake, B, H, W, D, C1, C2, D, 1, fake, 0, fake, big, 0, 3, None)
+        assert rc == -1 and b"tile_y" in L.m3d_last_error()

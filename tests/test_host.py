@@ -295,3 +295,28 @@ def test_check_fuses_flags_an_unconsumed_fused_backward():
         mnn.check_fuses(reg)
     b.clear()                             # the producer's backward consumed it
     mnn.check_fuses(reg)
+
+
+def test_backward_after_a_refresh_raises():
+    """the batched BN affine and split planes are per-forward buffers
+    refreshed in place; a unit's backward after another model forward raises
+    instead of reading the newer values (nn._check_generations)."""
+    import types
+
+    import pytest
+
+    from m3d import nn
+    store = types.SimpleNamespace(bn_gen=3)
+    ctx = types.SimpleNamespace(aff_gen=(store, 3), x3_gen=None)
+    nn._check_generations(ctx)                       # same forward: fine
+    store.bn_gen = 4
+    with pytest.raises(RuntimeError, match="BN affine"):
+        nn._check_generations(ctx)
+    ctx = types.SimpleNamespace(aff_gen=None, x3_gen=nn.X3_PLANES.gen)
+    nn._check_generations(ctx)
+    nn.X3_PLANES.gen += 1
+    try:
+        with pytest.raises(RuntimeError, match="split planes"):
+            nn._check_generations(ctx)
+    finally:
+        nn.X3_PLANES.gen -= 1
