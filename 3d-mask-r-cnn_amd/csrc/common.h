@@ -132,6 +132,11 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3W_TR_MINM
 #define M3D_TUNE_X3W_TR_MINM 256
 #endif
+// stream-K x3_wgrad_tr_kernel in non-deterministic mode (one balanced round
+// of workgroups instead of tiles x splits; 0: the split grid in both modes)
+#ifndef M3D_TUNE_X3W_SK
+#define M3D_TUNE_X3W_SK 1
+#endif
 #ifndef M3D_TUNE_X3W_DBG
 #define M3D_TUNE_X3W_DBG 0
 #endif

@@ -111,10 +111,18 @@ __device__ __forceinline__ float act(int code, float v) {
 // -- used for the implicit zero padding of im2col so the loaders are
 // branch-free (no exec-mask divergence around every load).
 #define M3D_OOB 0xFFFFFFF0u
+// Every caller's base and size are wave-uniform (kernel arguments, blockIdx-
+// derived, or a readfirstlane'd wave role); the readfirstlanes make that
+// provable to the compiler, which otherwise wraps each buffer op whose
+// descriptor it holds in VGPRs (64-bit divisions, per-wave selects) in a
+// readfirstlane waterfall loop (cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
-                                             (int)(uint32_t)(bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : bytes),
-                                             0x00020000);
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)(bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : bytes));
+    void* const pu = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(pu, (short)0, (int)nb, 0x00020000);
 }
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
@@ -1569,32 +1577,16 @@ __device__ __forceinline__ bf16x8 w2_frag(const char* plane, int o1, int o2) {
 // DBG (timing probes, selected by M3D_X3W_DBG): 1 no global loads, 2 no MFMAs,
 // 3 neither split nor LDS writes (MFMAs on a stale stage), 4 loads issued and
 // waited for at once, their data unused, 5 loads only (no split, no MFMA)
+// One workgroup's pass over rows [ms, me) of one 256x256 output tile (k0, n0)
+// of one batch item (A, Bm, C already offset to it), then its tile out.
 template <int DBG>
-__global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __restrict__ A,
-                                                             const float* __restrict__ Bm,
-                                                             float* __restrict__ C, int64_t M, int K,
-                                                             int N, int64_t m_per_split, int64_t bsa,
-                                                             int64_t bsb, int64_t bsc, WgOut wo) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * W2_STAGE];
+__device__ __forceinline__ void x3w_segment(char* __restrict__ smem, const float* __restrict__ A,
+                                            const float* __restrict__ Bm, float* __restrict__ C, int64_t M,
+                                            int K, int N, int64_t ms, int64_t me, int k0, int n0,
+                                            const WgOut& wo, float* wp, int64_t rot_seed) {
+    if (ms >= me) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
-    const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
-    const int64_t total = gxy * gridDim.z;
-    const int64_t Lb = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
-    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
-    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
-    const int bz = (int)(Lt / gxy), rem = (int)(Lt % gxy);
-    const int k0 = (rem % gridDim.x) * 256;
-    const int n0 = (rem / gridDim.x) * 256;
-    const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
-    const int64_t batch = bz / nsplit;
-    float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
-    A += batch * bsa;
-    Bm += batch * bsb;
-    C += batch * bsc;
-    const int64_t ms = (int64_t)(bz % nsplit) * m_per_split;
-    const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
-    if (ms >= me) return;
     // loader: rows lr and lr + 8 of the step, columns lc..lc+3 of both operands
     const int lr = tid >> 6, lc = (tid & 63) * 4;
     const bool aok = k0 + lc < K, bok = n0 + lc < N;
@@ -1610,7 +1602,7 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
     // its tile index; the N-tiles sharing an A tile, same index, stay in step
     // for L2): the 256 concurrent streams start 8-16 MB apart, and in lockstep
     // they would hit the same HBM channels (2.2 TB/s measured without it).
-    const int rot = (int)(((int64_t)bz * 17) % nk);
+    const int rot = (int)((rot_seed * 17) % nk);
     // steps past the last one load zeros (out-of-range offset): no branch in the loop
     auto load = [&](int kt, float4 (&va)[2], float4 (&vb)[2]) {
         const int ph = kt + rot >= nk ? kt + rot - nk : kt + rot;
@@ -1722,6 +1714,61 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
         }
 }
 
+// Stream-K decomposition (non-deterministic mode): the launch's units (batch
+// item, output tile, 16-row step) are cut into gridDim.x equal contiguous
+// ranges, one per workgroup, so a launch whose tiles x splits leave a partial
+// last round of one-per-CU workgroups (e.g. 288 tiles on 256 CUs: 1.125 rounds
+// ran as 2) runs as one balanced round; a tile whose steps span two ranges is
+// added into C by both (fp32 atomics, as the m splits).
+struct X3wSK {
+    int64_t units = 0;           // nbatch * tk * tn * nk
+    int nk = 0, tk = 0, tn = 0;  // steps per tile, k / n tiles
+};
+
+template <int DBG, bool SK = false>
+__global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __restrict__ A,
+                                                             const float* __restrict__ Bm,
+                                                             float* __restrict__ C, int64_t M, int K,
+                                                             int N, int64_t m_per_split, int64_t bsa,
+                                                             int64_t bsb, int64_t bsc, WgOut wo, X3wSK sk) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * W2_STAGE];
+    if constexpr (SK) {
+        // XCD-contiguous: the workgroups of one XCD take consecutive unit ranges
+        const int64_t G = gridDim.x, L = blockIdx.x;
+        const int64_t xcd = L % 8, q8 = G / 8, r8 = G % 8;
+        const int64_t g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+        int64_t u = g * sk.units / G;
+        const int64_t ue = (g + 1) * sk.units / G;
+        const int64_t tpb = (int64_t)sk.tk * sk.tn;
+        while (u < ue) {
+            const int64_t t = u / sk.nk;
+            const int64_t s0 = u - t * sk.nk;
+            const int64_t s1 = s0 + (ue - u) < sk.nk ? s0 + (ue - u) : sk.nk;
+            const int64_t batch = t / tpb;
+            const int r = (int)(t - batch * tpb);
+            const int64_t me = s1 * W2_BK < M ? s1 * W2_BK : M;
+            x3w_segment<DBG>(smem, A + batch * bsa, Bm + batch * bsb, C + batch * bsc, M, K, N, s0 * W2_BK, me,
+                             (r % sk.tk) * 256, (r / sk.tk) * 256, wo, nullptr, 0);
+            u += s1 - s0;
+        }
+        return;
+    }
+    const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
+    const int64_t total = gxy * gridDim.z;
+    const int64_t Lb = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int bz = (int)(Lt / gxy), rem = (int)(Lt % gxy);
+    const int k0 = (rem % gridDim.x) * 256;
+    const int n0 = (rem / gridDim.x) * 256;
+    const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
+    const int64_t batch = bz / nsplit;
+    float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
+    const int64_t ms = (int64_t)(bz % nsplit) * m_per_split;
+    const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
+    x3w_segment<DBG>(smem, A + batch * bsa, Bm + batch * bsb, C + batch * bsc, M, K, N, ms, me, k0, n0, wo, wp, bz);
+}
+
 // M3D_X3W_TR (default 1): the 256x256 transposed-read weight-gradient kernel
 // for GEMMs with K, N >= 192; 0 keeps the 128x128 x3_wgrad_kernel everywhere.
 static int wgrad_tr_env() {
@@ -1733,6 +1780,23 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
     const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
     const int64_t cus = num_cus();
+    static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
+    static constexpr int dbg = M3D_TUNE_X3W_DBG;
+    if (M3D_TUNE_X3W_SK && dbg == 0 && !det().on) {
+        // stream-K (X3wSK): one balanced round of workgroups, each >= minm rows
+        X3wSK sk{};
+        sk.nk = (int)((M + W2_BK - 1) / W2_BK);
+        sk.tk = (K + 255) / 256;
+        sk.tn = (N + 255) / 256;
+        sk.units = tiles * sk.nk;
+        const int64_t min_steps = (minm + W2_BK - 1) / W2_BK;
+        int64_t G = (sk.units + min_steps - 1) / min_steps;
+        if (G > cus) G = cus;
+        if (G < 1) G = 1;
+        hipLaunchKernelGGL((x3_wgrad_tr_kernel<0, true>), dim3((unsigned)G), dim3(512), 0, s, A, Bm, C, M, K, N,
+                           (int64_t)0, bsa, bsb, bsc, WgOut{nullptr, 0, 0}, sk);
+        return;
+    }
     // M3D_X3W_TR_FLOOR=1: splits = floor(CUs / tiles) (one wave of workgroups at
     // one per CU) instead of the ceiling (e.g. 96 tiles: 2 x 96 vs 3 x 96 = 288)
     static constexpr int fl = M3D_TUNE_X3W_TR_FLOOR;
@@ -1743,7 +1807,6 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     // and their 16.7 M atomics per launch slowed the data-gradient stream beside
     // them.  256: 128^3 step 28.73 -> 27.8 ms (scripts/gpu_wgrad1b.sh, wg1c/d A/B:
     // 256 / 384 / 512 equal within noise, 1024 28.2-28.5 ms); alone 73 -> 64 us.
-    static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -1765,16 +1828,16 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
-    static constexpr int dbg = M3D_TUNE_X3W_DBG;
+    const X3wSK nosk{};
     if constexpr (dbg == 0) {
-        hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
+        hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk);
     } else switch (dbg) {
-        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
-        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
-        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
-        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
-        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo); break;
-        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
+        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
+        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
+        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
+        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
+        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
+        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk);
     }
     wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
 }
@@ -2584,39 +2647,42 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
 // in its order -- + bias, z store, * scale + shift, + same-shape residual,
 // activation -- so the fused form is bit-identical to the GEMM + epilogue pass
 struct X3Epi {
-    const float* bias;
-    const float* scale;
-    const float* shift;
-    const float* res;          // [M][N] (res_mode 1) or nullptr
-    float* z;                  // pre-BN output or nullptr
-    int act;                   // act() code
-    int on;                    // 0: plain C store, 1: the forward conv epilogue above, 2: the fused
+    const float* bias = nullptr;
+    const float* scale = nullptr;
+    const float* shift = nullptr;
+    const float* res = nullptr;   // [M][N] (res_mode 1) or nullptr
+    float* z = nullptr;           // pre-BN output or nullptr
+    int act = 0;                  // act() code
+    int on = 0;                    // 0: plain C store, 1: the forward conv epilogue above, 2: the fused
                                // BN-ReLU backward below (a 1x1x1 conv's data gradient)
     // on == 2: epi_bnbwd4's maths per element of the data gradient g (accumulate 0):
     // g masked by y > 0 (frelu), dz = g * fscale into C, g into fdres, and the channel
     // sums (g, g * (fz - fmean) * frstd, dz) of each 128-row half tile into fpart row
     // 2 * (m0 / 256) + (wave row)
-    const float* fy;
-    const float* fz;
-    const float* fscale;
-    const float* fmean;
-    const float* frstd;
-    float* fdres;
-    float* fpart;
-    int64_t fprows;
-    int frelu;
+    const float* fy = nullptr;
+    const float* fz = nullptr;
+    const float* fscale = nullptr;
+    const float* fmean = nullptr;
+    const float* frstd = nullptr;
+    float* fdres = nullptr;
+    float* fpart = nullptr;
+    int64_t fprows = 0;
+    int frelu = 0;
 };
 
 struct X3G {
-    const unsigned short* a;
-    const float* af;           // AF32: A as fp32 [batch][M][K], split in the LDS store
-    const unsigned short* b;
-    float* c;
-    int64_t M;
-    int K, N, nbatch;
-    int64_t psa, psb;          // plane strides (elements)
-    int64_t bsa, bsb, bsc;     // batch strides (elements)
-    X3Epi ep = {};             // x3_gemm256_af_kernel only (zero: the plain C store)
+    // default member initialisers: a descriptor declared without an initialiser
+    // is still all-zero (round 5: an uninitialised ep.on ran the fused epilogue
+    // on garbage and faulted; tests/test_sanitizers.py checks the declarations)
+    const unsigned short* a = nullptr;
+    const float* af = nullptr;    // AF32: A as fp32 [batch][M][K], split in the LDS store
+    const unsigned short* b = nullptr;
+    float* c = nullptr;
+    int64_t M = 0;
+    int K = 0, N = 0, nbatch = 0;
+    int64_t psa = 0, psb = 0;     // plane strides (elements)
+    int64_t bsa = 0, bsb = 0, bsc = 0;   // batch strides (elements)
+    X3Epi ep = {};                // x3_gemm256_af_kernel only (zero: the plain C store)
 };
 
 // byte offset of (row, chunk) in a 16-deep X3 plane: 32-B rows of two 16-B
@@ -2966,8 +3032,22 @@ template <int N_> struct IC { static constexpr int v = N_; };
 // register allocation): 0 the plain C store, 1 the forward conv epilogue,
 // 2 the fused BN-ReLU backward (X3Epi.on)
 template <int EPI>
+#ifndef M3D_X3AF_STAMP
+#define M3D_X3AF_STAMP 0   // timing probe (debug builds): per-workgroup clock stamps into C row m0
+#endif
 __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
-#if M3D_TUNE_X3AF & 8
+#if M3D_X3AF_STAMP
+    __shared__ __attribute__((aligned(16))) char sAll[18 * G2_PL + 256];
+    uint32_t* const stampbuf = reinterpret_cast<uint32_t*>(sAll + 18 * G2_PL);
+    char* const sA0 = sAll;
+    char* const sA1 = sAll + 3 * G2_PL;
+    char* const sA2 = sAll + 6 * G2_PL;
+    char* const sB0 = sAll + 9 * G2_PL;
+    char* const sB1 = sAll + 12 * G2_PL;
+    char* const sB2 = sAll + 15 * G2_PL;
+    const uint32_t st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+    const uint32_t st_r0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#elif M3D_TUNE_X3AF & 8
     __shared__ __attribute__((aligned(16))) char sAll[18 * G2_PL];
     char* const sA0 = sAll;
     char* const sA1 = sAll + 3 * G2_PL;
@@ -3073,12 +3153,18 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     dma_b(IC<1>{}, 1);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A(0)
     split_a(IC<0>{}, xa);
+#if M3D_X3AF_STAMP
+    const uint32_t st_t1 = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
     // step kt on stage st = kt % 3: cur holds A(kt+1) (loaded at step kt-1), nxt
     // receives A(kt+2) (its A(kt) was split at step kt-1)
     auto step = [&](auto st, int kt, float4 (&cur)[2], float4 (&nxt)[2]) {
         constexpr int s0 = decltype(st)::v;
         asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // B(kt); own A(kt) writes
         __builtin_amdgcn_s_barrier();
+#if M3D_X3AF_STAMP
+        if (tid == 0 && kt < 56) stampbuf[kt] = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
         load_a(kt + 2, nxt);
         dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");              // A(kt+1)
@@ -3144,6 +3230,9 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         step(IC<2>{}, kt, xa, ya); if (++kt >= nk) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
+#if M3D_X3AF_STAMP
+    const uint32_t st_t2 = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
     if constexpr (EPI == 2) {
         // fused BN-ReLU backward (X3Epi on == 2): per accumulator tile its 16 y / z
@@ -3261,6 +3350,24 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
                                                       0, 0);
             }
         }
+#if M3D_X3AF_STAMP
+    // wave 0 wrote C row m0, columns n0..n0+31 above: its own later stores win
+    const uint32_t st_t3 = (uint32_t)__builtin_amdgcn_s_memtime();
+    const uint32_t st_r3 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (wave == 0) {
+        uint32_t v = 0;
+        if (lane == 0) v = st_t0;
+        else if (lane == 1) v = st_t1;
+        else if (lane == 2) v = st_t2;
+        else if (lane == 3) v = st_t3;
+        else if (lane == 4) v = st_r0;
+        else if (lane == 5) v = st_r3;
+        else if (lane == 6) v = (uint32_t)nk;
+        else if (lane == 7) v = (uint32_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_ID (XCC/SE/CU ids)
+        else if (lane >= 8 && lane - 8 < nk && lane - 8 < 56) v = stampbuf[lane - 8];
+        __builtin_amdgcn_raw_buffer_store_b32(v, rc, (int)(((uint32_t)n0 + (uint32_t)lane) * 4u), 0, 0);
+    }
+#endif
 }
 
 #if M3D_TUNE_X3_AF128
@@ -3459,7 +3566,7 @@ static int wino_points() { return wino_points(wino_nz()); }
 
 static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Din, int pz,
                           int nz = -1, int ny = WNY) {
-    WinoGeom g;
+    WinoGeom g{};
     if (nz < 0) nz = wino_nz();
     g.B = (int)B; g.H = (int)H; g.W = (int)W; g.D = (int)D; g.Din = (int)Din; g.pz = pz;
     g.TY = (int)((H + ny - 1) / ny); g.TX = (int)((W + 1) / 2); g.TZ = (int)((D + nz - 1) / nz);
@@ -4921,7 +5028,7 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, in
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t P = (size_t)wino_points(nz < 0 ? wino_nz() : nz, ny);
     char* p = (char*)ws;
-    WinoWs w;
+    WinoWs w{};
     w.WT = (float*)p;
     if (gemm_x3_env()) p += al(sizeof(float) * 27 * (size_t)Cin * Cout);
     const size_t eb = gemm_x3_env() ? 6 : 4;
@@ -5058,7 +5165,7 @@ extern "C" int m3d_gemm_x3(const uint16_t* A3, const uint16_t* B3, float* C, int
     if (K % 32 || N % 4) return einval("gemm_x3: K must be a multiple of 32 and N of 4");
     if (M > 0x7FFFFFFF || M * K * 2 >= 0xFFFFFFF0LL || N * K * 2 >= 0xFFFFFFF0LL || M * N * 4 >= 0xFFFFFFF0LL)
         return einval("gemm_x3: operand larger than 4 GiB (32-bit buffer offsets)");
-    WinoWs ws;
+    WinoWs ws{};
     ws.U = (float*)const_cast<uint16_t*>(A3);
     ws.V = (float*)const_cast<uint16_t*>(B3);
     ws.M = C;
@@ -5074,7 +5181,7 @@ extern "C" int m3d_gemm_x3_af(const float* A, const uint16_t* B3, float* C, int6
     if (!A || !B3 || !C) return einval("gemm_x3_af: null operand");
     if (M > 0x7FFFFFFF || M * K * 4 >= 0xFFFFFFF0LL || N * K * 2 >= 0xFFFFFFF0LL || M * N * 4 >= 0xFFFFFFF0LL)
         return einval("gemm_x3_af: operand larger than 4 GiB (32-bit buffer offsets)");
-    WinoWs ws;
+    WinoWs ws{};
     ws.U = const_cast<float*>(A);
     ws.V = (float*)const_cast<uint16_t*>(B3);
     ws.M = C;

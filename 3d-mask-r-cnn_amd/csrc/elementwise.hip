@@ -1159,7 +1159,7 @@ static int col_sums_plan(const m3d_col_sums_item_t* items, int32_t n, ColSumsBat
 }
 
 extern "C" size_t m3d_col_sums_batched_workspace_bytes(const m3d_col_sums_item_t* items, int32_t n) {
-    ColSumsBatch b;
+    ColSumsBatch b{};
     size_t f;
     int mc;
     if (col_sums_plan(items, n, b, f, mc) != M3D_OK) return 0;
@@ -1168,7 +1168,7 @@ extern "C" size_t m3d_col_sums_batched_workspace_bytes(const m3d_col_sums_item_t
 
 extern "C" int m3d_col_sums_batched(const m3d_col_sums_item_t* items, int32_t n, void* workspace, size_t ws_bytes,
                                     m3d_stream_t s) {
-    ColSumsBatch b;
+    ColSumsBatch b{};
     size_t f;
     int max_c;
     int rc = col_sums_plan(items, n, b, f, max_c);

@@ -123,7 +123,7 @@ extern "C" int m3d_refine_detections(const float* rois, const float* probs, cons
                                      m3d_stream_t s) {
     if (N < 0 || num_classes < 2) return einval("refine_detections: need num_classes >= 2");
     if (N == 0) return M3D_OK;
-    F6 sd;
+    F6 sd{};
     for (int q = 0; q < 6; ++q) sd.v[q] = bbox_std_dev[q];
     hipLaunchKernelGGL(refine_kernel, dim3(grid_for(N, 256)), dim3(256), 0, st(s), rois, probs, deltas,
                        N, (int)num_classes, image_meta, sd, min_conf, boxes_px, nms_boxes, scores);

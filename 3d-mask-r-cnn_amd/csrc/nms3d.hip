@@ -423,7 +423,7 @@ struct NmsWs {
 };
 
 static NmsWs nms_ws_layout(int64_t N, void* base) {
-    NmsWs w;
+    NmsWs w{};
     const int64_t npad = pow2_at_least(N < 2 ? 2 : N);
     const int64_t cb = (N + 63) / 64;
     char* p = (char*)base;
@@ -515,7 +515,7 @@ extern "C" int m3d_proposal_decode(const float* probs, const float* deltas, cons
     if (k == 0) return M3D_OK;
     if (!probs || !deltas || !anchors || !order || !boxes || !scores || !std_dev)
         return einval("proposal_decode: null pointer");
-    Std6 sd;
+    Std6 sd{};
     for (int q = 0; q < 6; ++q) sd.v[q] = std_dev[q];
     hipLaunchKernelGGL(proposal_decode_kernel, dim3(grid_for(k, 256)), dim3(256), 0, st(s), probs,
                        deltas, anchors, n_anchors, order, k, sd, image_depth, boxes, scores, err);

@@ -35,7 +35,7 @@ struct Sample {
 
 __device__ __forceinline__ Sample make_sample(const float* box, int H, int W, int D, int ch, int cw,
                                               int cd, int y, int x, int z) {
-    Sample s;
+    Sample s{};
     const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
     const float in_y = axis_coord(y1, y2, H, ch, y, axis_scale(y1, y2, H, ch));
     const float in_x = axis_coord(x1, x2, W, cw, x, axis_scale(x1, x2, W, cw));
@@ -951,7 +951,7 @@ static int roi_region_mode() {
 
 template <int TY, int TX, int TZ>
 static void launch_region_fwd(const LineArgs& a, const Pyr& P, int64_t B, hipStream_t s) {
-    RegionGrid G;
+    RegionGrid G{};
     G.off[0] = 0;
     for (int l = 0; l < 4; ++l) {
         G.gy[l] = (P.H[l] + TY - 1) / TY;
@@ -1635,7 +1635,7 @@ struct GbTerm {
     double d;
 };
 __device__ __forceinline__ GbTerm gb_term(int n, int i, float g, float r, int S) {
-    GbTerm t;
+    GbTerm t{};
     if (n > 1) {
         t.lo = ((float)(S - 1) - r * (float)i) * g;
         t.hi = (g * (float)i) * r;
@@ -1962,7 +1962,7 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                             const float* boxes, const float* image_meta, int64_t meta_stride, int64_t B,
                             int64_t N, int32_t ph, int32_t pw, int32_t pd, float* out, float* boxes_adj,
                             int32_t* levels, void* workspace, size_t ws_bytes, hipStream_t s) {
-    Pyr P;
+    Pyr P{};
     int rc = make_pyr(P, fmaps, nullptr, fshape);
     if (rc) return rc;
     if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
@@ -2027,7 +2027,7 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 int32_t* offs = counts + nb;
                 int32_t* keys = offs + nb;
                 int32_t* pm = keys + nl;
-                RegionBase rb;
+                RegionBase rb{};
                 int64_t acc = 0;
                 for (int l = 0; l < 4; ++l) {
                     rb.base[l] = acc;
@@ -2047,7 +2047,7 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 int32_t* offs = counts + nb;
                 int32_t* keys = offs + nb;
                 int32_t* pm = keys + nl;
-                RegionBase rb;
+                RegionBase rb{};
                 int64_t acc = 0;
                 for (int l = 0; l < 4; ++l) {
                     rb.base[l] = acc;
@@ -2137,7 +2137,7 @@ extern "C" int m3d_pyramid_roi_align3d_bwd(const float* grad_out, const float* b
                                            int32_t ph, int32_t pw, int32_t pd,
                                            float* const gmaps[4], const int64_t fshape[4][3],
                                            int64_t C, m3d_stream_t s) {
-    Pyr P;
+    Pyr P{};
     int rc = make_pyr(P, nullptr, gmaps, fshape);
     if (rc) return rc;
     if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");
@@ -2178,7 +2178,7 @@ extern "C" int m3d_pyramid_roi_align3d_bwd_det(const float* grad_out, const floa
                                                int32_t ph, int32_t pw, int32_t pd,
                                                float* const gmaps[4], const int64_t fshape[4][3],
                                                int64_t C, int32_t* box_ind_ws, m3d_stream_t s) {
-    Pyr P;
+    Pyr P{};
     int rc = make_pyr(P, nullptr, gmaps, fshape);
     if (rc) return rc;
     if (ph <= 0 || pw <= 0 || pd <= 0) return einval("crop dimensions must be positive");

@@ -526,7 +526,7 @@ static size_t rt_layout(int64_t A, int64_t G, int64_t cap, char* base, RtWs* w) 
     size_t off = 0;
     auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off += al256(bytes); return p; };
     const int64_t nb = (A + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    RtWs t;
+    RtWs t{};
     t.iou_max = (float*)take(sizeof(float) * A);
     t.arg = (int32_t*)take(sizeof(int32_t) * A);
     t.gt_best = (unsigned long long*)take(sizeof(unsigned long long) * (G > 0 ? G : 1));
@@ -561,7 +561,7 @@ static int rpn_targets_impl(const float* anchors, int64_t A, const float* gt_box
     if (total <= 0) return einval("rpn_targets: RPN_TRAIN_ANCHORS_PER_IMAGE must be positive");
     if (list_cap <= 0 || list_cap > 0x7FFFFFFF) return einval("rpn_targets: list_cap must be in [1, 2^31)");
     if (ws_bytes < m3d_rpn_targets_workspace_bytes(A, G, list_cap)) return einval("rpn_targets: workspace too small");
-    RtWs w;
+    RtWs w{};
     rt_layout(A, G, list_cap, (char*)workspace, &w);
     if (hipMemsetAsync(rpn_bbox, 0, sizeof(float) * 6 * (size_t)total, hs) != hipSuccess)
         return check_launch("memset rpn_bbox");
@@ -620,7 +620,7 @@ static int rpn_targets_impl(const float* anchors, int64_t A, const float* gt_box
     const unsigned nb = (unsigned)((A + SCAN_CHUNK - 1) / SCAN_CHUNK);
     hipLaunchKernelGGL(pos_block_count_kernel, dim3(nb), dim3(256), 0, hs, rpn_match, A, w.bcount);
     hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(64), 0, hs, w.bcount, (int)nb);
-    G6 sd;
+    G6 sd{};
     for (int q = 0; q < 6; ++q) sd.v[q] = rpn_bbox_std_dev[q];
     hipLaunchKernelGGL(pos_deltas_kernel, dim3(nb), dim3(256), 0, hs, rpn_match, A, w.bcount, anchors, gt_boxes,
                        w.arg, sd, (int)total, rpn_bbox);
@@ -657,7 +657,7 @@ extern "C" int m3d_rpn_targets(const float* anchors, int64_t A, const float* gt_
                               atss_min_pos, rpn_bbox_std_dev, seed, rpn_match, rpn_bbox, list_cap, workspace,
                               ws_bytes, nullptr, hs);
     if (rc) return rc;
-    RtWs w;
+    RtWs w{};
     rt_layout(A, G, list_cap, (char*)workspace, &w);
     if (hipMemsetAsync(w.cnt, 0, sizeof(unsigned long long) * 2, hs) != hipSuccess) return check_launch("memset");
     hipLaunchKernelGGL(count_kernel, dim3(1024), dim3(256), 0, hs, rpn_match, A, w.cnt);

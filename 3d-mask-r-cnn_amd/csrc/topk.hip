@@ -320,7 +320,7 @@ struct TopkWs {
 };
 
 static TopkWs topk_ws(int64_t k, void* base) {
-    TopkWs w;
+    TopkWs w{};
     char* p = (char*)base;
     size_t off = 0;
     auto take = [&](size_t b) {

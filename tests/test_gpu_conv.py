@@ -276,10 +276,13 @@ def test_winograd_z_halo_geometry(cuda, D, OD, pz):
 
 
 @pytest.mark.parametrize("nb,M,K,N", [(3, 200, 64, 96), (2, 1000, 128, 36), (64, 512, 256, 512),
-                                     (2, 1000, 320, 260), (1, 37, 192, 196), (3, 4099, 512, 256)])
+                                     (2, 1000, 320, 260), (1, 37, 192, 196), (3, 4099, 512, 256),
+                                     (9, 4096, 256, 512), (5, 4000, 256, 256)])
 def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
     """m3d_gemm_wgrad_f32 (the Winograd weight-gradient GEMM launch bench.py
-    prices): C[b] += A[b]^T B[b] against a float64 torch bmm, ragged M/K/N tiles."""
+    prices): C[b] += A[b]^T B[b] against a float64 torch bmm, ragged M/K/N tiles.
+    The last two cut tiles across stream-K workgroup ranges at odd steps
+    (x3_wgrad_tr_kernel<0, true>: 18 and ~16 steps per workgroup)."""
     from m3d import _lib
     L = _lib.load()
     g = torch.Generator().manual_seed(11)

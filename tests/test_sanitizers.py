@@ -45,3 +45,29 @@ def test_oracle_under_asan_ubsan(sanitized_builds):
                        cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and _clean(out), out[-4000:]
+
+
+def test_launch_descriptors_value_initialised():
+    """VERDICT r5 weak #9 (fault e23973a: `X3G q;` left q.ep.on uninitialised
+    and x3_gemm256_af_kernel ran its fused epilogue on garbage).  Every
+    kernel-argument descriptor declared in csrc/ is value-initialised: no
+    declaration without an initialiser, and every member of the X3 GEMM
+    descriptors carries a default initialiser (so even `X3G q;` is zero)."""
+    import re
+    csrc = os.path.join(ROOT, "3d-mask-r-cnn_amd", "csrc")
+    srcs = {f: open(os.path.join(csrc, f)).read() for f in sorted(os.listdir(csrc))
+            if f.endswith((".hip", ".h", ".cpp"))}
+    types = sorted({m for s in srcs.values() for m in re.findall(r"^struct\s+(\w+)\s*\{", s, re.M)})
+    assert {"X3G", "X3Epi", "ConvP", "Epi", "WinoGeom", "X3wSK"} <= set(types)
+    bare = re.compile(r"^\s*(?:const\s+)?(" + "|".join(types) + r")\s+\w+(?:\s*\[[^\]]*\])?\s*;", re.M)
+    bad = [(f, s[:m.start()].count("\n") + 1, m.group(0).strip()) for f, s in srcs.items() for m in bare.finditer(s)]
+    # struct members (inside a struct body) are not declarations of a launch descriptor
+    bad = [b for b in bad if not re.search(r"^\s*(X3Epi)\s+ep", b[2])]
+    assert not bad, bad
+    conv = srcs["conv3d.hip"]
+    for name in ("X3G", "X3Epi", "X3wSK"):
+        body = conv[conv.index(f"struct {name} {{"):]
+        body = body[:body.index("\n};")]
+        members = [ln.split("//")[0].strip() for ln in body.split("\n")[1:]]
+        members = [m for m in members if m.endswith(";")]
+        assert members and all("=" in m for m in members), (name, [m for m in members if "=" not in m])
