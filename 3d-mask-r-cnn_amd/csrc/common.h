@@ -298,6 +298,14 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_ROI_ROW_CG
 #define M3D_TUNE_ROI_ROW_CG 1
 #endif
+// x3_gemm256_af_kernel: A loaded three steps ahead (no wait inside a step).
+// Round 6 (profiles/r06_x3af_stamps_128.txt, per-step clock stamps): with A two
+// steps ahead the six unrolled step copies ran 3.9K-7.2K cycles (the compiler's
+// waits differed per copy, one drained the prefetch); three ahead, three copies,
+// 3.7K-4.6K; priced launch 0.998 -> 0.959 ms, 128^3 step 25.33 -> 24.96 ms (same box)
+#ifndef M3D_TUNE_X3AF_A3
+#define M3D_TUNE_X3AF_A3 1
+#endif
 #ifndef M3D_TUNE_X3AF
 #define M3D_TUNE_X3AF 0
 #endif

@@ -3104,6 +3104,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) rbk[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb, (uint64_t)g.N * g.K * 2);
 #endif
+    using AReg = float4;
     auto load_a = [&](int kt, float4 (&v)[2]) {
         const bool in = kt < nk;
 #if M3D_X3AF_KB & 2
@@ -3130,11 +3131,11 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G2_PL, off);
 #endif
     };
-    auto split_a = [&](auto st, const float4 (&v)[2]) {
+    auto split_a = [&](auto st, const AReg (&v)[2]) {
         char* S = stA(st) + awr;
         uint2 lo4[3], hi4[3];
-        split3x4(v[0], lo4);
-        split3x4(v[1], hi4);
+        split3x4(make_float4(v[0][0], v[0][1], v[0][2], v[0][3]), lo4);
+        split3x4(make_float4(v[1][0], v[1][1], v[1][2], v[1][3]), hi4);
 #pragma unroll
         for (int q = 0; q < 3; ++q)
             *reinterpret_cast<uint4*>(S + q * G2_PL) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
@@ -3146,6 +3147,19 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+#if M3D_TUNE_X3AF_A3
+    // A three steps ahead (three register sets): per step A(kt+3) then B(kt+2)
+    // are issued, so A(kt+1) (issued at step kt-2, before B(kt)) is retired by
+    // the top-of-step wait for B(kt) and no wait sits inside the step
+    AReg xa[2], ya[2], za[2];
+    load_a(0, xa);
+    load_a(1, ya);
+    dma_b(IC<0>{}, 0);
+    load_a(2, za);
+    dma_b(IC<1>{}, 1);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A(0)
+    split_a(IC<0>{}, xa);
+#else
     float4 xa[2], ya[2];            // A rows of the even / odd steps
     load_a(0, xa);
     dma_b(IC<0>{}, 0);
@@ -3153,21 +3167,27 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     dma_b(IC<1>{}, 1);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A(0)
     split_a(IC<0>{}, xa);
+#endif
 #if M3D_X3AF_STAMP
     const uint32_t st_t1 = (uint32_t)__builtin_amdgcn_s_memtime();
 #endif
     // step kt on stage st = kt % 3: cur holds A(kt+1) (loaded at step kt-1), nxt
     // receives A(kt+2) (its A(kt) was split at step kt-1)
-    auto step = [&](auto st, int kt, float4 (&cur)[2], float4 (&nxt)[2]) {
+    auto step = [&](auto st, int kt, AReg (&cur)[2], AReg (&nxt)[2]) {
         constexpr int s0 = decltype(st)::v;
         asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // B(kt); own A(kt) writes
         __builtin_amdgcn_s_barrier();
 #if M3D_X3AF_STAMP
         if (tid == 0 && kt < 56) stampbuf[kt] = (uint32_t)__builtin_amdgcn_s_memtime();
 #endif
+#if M3D_TUNE_X3AF_A3
+        load_a(kt + 3, nxt);
+        dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
+#else
         load_a(kt + 2, nxt);
         dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");              // A(kt+1)
+#endif
         split_a(IC<(s0 + 1) % 3>{}, cur);        // stage last read at step kt-2
         const char* SA = stA(st);
         const char* SB = stB(st);
@@ -3221,6 +3241,14 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #endif
     };
     // stage kt % 3 and register set kt % 2 static: six steps per trip
+#if M3D_TUNE_X3AF_A3
+    // step kt: cur = set (kt+1) % 3 holds A(kt+1), nxt = set kt % 3 (A(kt) split at step kt-1)
+    for (int kt = 0;;) {
+        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
+        step(IC<1>{}, kt, za, ya); if (++kt >= nk) break;
+        step(IC<2>{}, kt, xa, za); if (++kt >= nk) break;
+    }
+#else
     for (int kt = 0;;) {
         step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
         step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
@@ -3229,6 +3257,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         step(IC<1>{}, kt, ya, xa); if (++kt >= nk) break;
         step(IC<2>{}, kt, xa, ya); if (++kt >= nk) break;
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
 #if M3D_X3AF_STAMP
     const uint32_t st_t2 = (uint32_t)__builtin_amdgcn_s_memtime();
