@@ -262,8 +262,11 @@ WINO_WGRAD_MIN_C = 64
 
 # Layers whose Winograd data gradient runs on F(4x2x4) tiles instead of the
 # library's F(2x2x4) ('+'-separated layer names, "*" = all; round 5 moved every
-# data gradient to F(2x2x4) for gradient accuracy).
-WINO_DGRAD_Y4 = ""
+# data gradient to F(2x2x4) for gradient accuracy).  Round 6: the
+# three 64-channel res2 branch2b convs, the last data gradients of the backward
+# chain (their rounding reaches only res2a / the stem): 256^3 step 151.6 ->
+# 150.2 ms, configs[1] gradient median 2.05e-6 unchanged (profiles/r06_res2_dgrad_y4.txt)
+WINO_DGRAD_Y4 = "res2a_branch2b+res2b_branch2b+res2c_branch2b"
 
 
 def _dgrad_tile_y(name):
