@@ -144,6 +144,40 @@ def test_train_steps_bitwise_repeatable(det, cuda):
     assert float((a[2] - d[2]).abs().max()) <= 1e-5 * float(a[2].abs().max())
 
 
+def test_graphed_step_with_in_step_targets_bitwise(det, cuda):
+    """The configs[0]-style step with its RPN targets built on the GPU every
+    step (RPNTargetBuilder, a new seed each step): eager steps and the
+    HIP-graph replay of the step captured over the builder's persistent
+    target buffers (the builder launched before each replay, bench.py) give
+    the same losses and weights bit for bit (deterministic mode)."""
+    from m3d.config import synthetic_rpn_config
+    from m3d.model import RPN, synthetic_volume
+    from m3d.targets import RPNTargetBuilder
+    _lib = det
+    _lib.set_deterministic(True)
+    cfg = synthetic_rpn_config(64, depth=16, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=500)
+    image = synthetic_volume(64, 16, seed=0).to(cuda)
+    gt = torch.tensor([[0.2, 0.2, 0.2, 0.5, 0.45, 0.6], [0.55, 0.5, 0.3, 0.8, 0.9, 0.8]], device=cuda)
+    runs = []
+    for graphed in (False, True):
+        model = RPN(cfg, device=cuda, seed=5)
+        builder = RPNTargetBuilder(model.anchors.reshape(-1, 6), cfg, max_gt=4)
+        if graphed:
+            step = model.graphed_train_step(image, builder(gt, seed=0), warmup=2)   # 2 steps on seed 0
+            for i in range(3):
+                builder(gt, seed=12 + i)
+                r = step()
+        else:
+            t = builder(gt, seed=0)
+            for _ in range(2):
+                model.train_step(image, t)
+            for i in range(3):
+                r = model.train_step(image, builder(gt, seed=12 + i))
+        torch.cuda.synchronize()
+        runs.append((float(r["loss"]), model.store.flat.detach().clone()))
+    assert runs[0][0] == runs[1][0] and torch.equal(runs[0][1], runs[1][1])
+
+
 def test_rpn_head_shared_wino_policy_bit_identical(det, cuda, monkeypatch):
     """The RPN head's shared Winograd weight transform as the model drives it
     (m3d.nn._shared_wino_ws): forward + backward of the whole RPN with sharing
