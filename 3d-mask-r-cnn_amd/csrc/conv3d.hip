@@ -1782,8 +1782,10 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t cus = num_cus();
     static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
     static constexpr int dbg = M3D_TUNE_X3W_DBG;
-    if (M3D_TUNE_X3W_SK && dbg == 0 && !det().on) {
+    if (M3D_TUNE_X3W_SK && dbg == 0 && !det().on && M >= 32 * W2_BK) {
         // stream-K (X3wSK): one balanced round of workgroups, each >= minm rows
+        // (only for tiles of >= 32 steps: with short tiles the minm floor would
+        // give one workgroup a run of tiles, each with its own atomic epilogue)
         X3wSK sk{};
         sk.nk = (int)((M + W2_BK - 1) / W2_BK);
         sk.tk = (K + 255) / 256;

@@ -296,6 +296,28 @@ def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
     close(Cd, ref)
 
 
+@pytest.mark.parametrize("nb,M,K,N", [(144, 4096, 256, 512), (40, 4096, 256, 512), (72, 2050, 256, 768),
+                                     (300, 512, 256, 256)])
+def test_wgrad_gemm_stream_k_shapes(cuda, nb, M, K, N):
+    """x3_wgrad_tr_kernel's stream-K form (non-deterministic mode): whole tiles
+    per workgroup with a plain add, the remainder tiles' step ranges added
+    atomically -- 288 tiles on 256 CUs (one whole tile each + 1/8 of a
+    remainder tile: the priced launch), 80 and 216 tiles (ranges only, a ragged
+    last step), and 300 short tiles (the split grid with plain adds).  C += A^T
+    B against float64 on the GPU, 1e-5 of the scale."""
+    from m3d import _lib
+    L = _lib.load()
+    g = torch.Generator(device=cuda).manual_seed(13)
+    A = torch.randn((nb, M, K), device=cuda, generator=g)
+    Bm = torch.randn((nb, M, N), device=cuda, generator=g)
+    C = torch.randn((nb, K, N), device=cuda, generator=g)
+    ref = torch.baddbmm(C.double(), A.double().transpose(1, 2), Bm.double())
+    _lib.check(L.m3d_gemm_wgrad_f32(A.data_ptr(), Bm.data_ptr(), C.data_ptr(), nb, M, K, N, _lib.stream()),
+               "gemm_wgrad")
+    err = float((C.double() - ref).abs().max()) / float(ref.abs().max())
+    assert err < 1e-5, err
+
+
 @pytest.mark.parametrize("nb,M,K,N", [(3, 300, 96, 160), (2, 300, 64, 256), (3, 1000, 256, 512),
                                      (1, 256, 128, 256), (2, 257, 512, 768), (96, 520, 256, 512)])
 def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
