@@ -102,32 +102,17 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // only in such builds (if constexpr on these values).  The one runtime switch
 // left is M3D_OPERAND_LIMIT (conv3d.hip: lowers the 32-bit operand bound so the
 // per-batch-item path runs at test sizes; tests/test_gpu_conv.py).
-#ifndef M3D_TUNE_GEMM_NBUF
-#define M3D_TUNE_GEMM_NBUF 1
-#endif
-#ifndef M3D_TUNE_GEMM_PERSIST
-#define M3D_TUNE_GEMM_PERSIST 1
-#endif
 // GEMM forms on the exact bf16 split (bit mask, conv3d.hip x3_mask); 31 = all,
 // the implicit-GEMM convs included since round 4 (same-box step A/B with the
 // fused BN backward: 27.33 -> 27.08 ms, profiles/r04v_cx3_step_ab.txt)
 #ifndef M3D_TUNE_GEMM_X3
 #define M3D_TUNE_GEMM_X3 31
 #endif
-#ifndef M3D_TUNE_GEMM_BK
-#define M3D_TUNE_GEMM_BK 32
-#endif
 #ifndef M3D_TUNE_WGRAD_MINM
 #define M3D_TUNE_WGRAD_MINM 512
 #endif
-#ifndef M3D_TUNE_WGRAD_K64
-#define M3D_TUNE_WGRAD_K64 1
-#endif
 #ifndef M3D_TUNE_X3W_TR
 #define M3D_TUNE_X3W_TR 1
-#endif
-#ifndef M3D_TUNE_X3W_TR_FLOOR
-#define M3D_TUNE_X3W_TR_FLOOR 0
 #endif
 #ifndef M3D_TUNE_X3W_TR_MINM
 #define M3D_TUNE_X3W_TR_MINM 256
@@ -137,9 +122,6 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3W_SK
 #define M3D_TUNE_X3W_SK 1
 #endif
-#ifndef M3D_TUNE_X3W_DBG
-#define M3D_TUNE_X3W_DBG 0
-#endif
 // wave-quantised m-splits for the 256x256 weight-gradient kernel (A/B only):
 // Q = 8 / 16 measured 25.5 / 25.45 vs 25.2-25.4 ms at 128^3 and 149.2-149.6 vs
 // 148.3-148.5 ms at 256^3 (profiles/r04q_wgrad_quant_ab.txt): the kernel runs on
@@ -148,21 +130,6 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // (A/B only): 128^3 25.19 vs 25.18 ms with the RPN heads' gradient on the side
 // stream, 25.19 vs 25.31-25.38 ms without (profiles/r04s_rpn_wgrad_ab.txt) --
 // the side stream alone removes the same cost from the critical path.
-#ifndef M3D_TUNE_WGRAD_FILL
-#define M3D_TUNE_WGRAD_FILL 0
-#endif
-#ifndef M3D_TUNE_X3W_TR_QUANT
-#define M3D_TUNE_X3W_TR_QUANT 0
-#endif
-#ifndef M3D_TUNE_X3W_TR_MIN_M
-#define M3D_TUNE_X3W_TR_MIN_M 0
-#endif
-#ifndef M3D_TUNE_X3W_MINM
-#define M3D_TUNE_X3W_MINM 0
-#endif
-#ifndef M3D_TUNE_X3W_OCC
-#define M3D_TUNE_X3W_OCC 2
-#endif
 // the x3 GEMMs' two accumulator tiles per A fragment issued interleaved
 // (x3_mac_pair; 0: one tile's six-MFMA chain after the other)
 // x3_gemm256_af_kernel: two A rows' fragments per step, four chains interleaved (A/B)
@@ -170,21 +137,6 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // weight gradients): tile pairs' chains interleaved -- 128^3 step 25.61-25.66
 // vs 25.76-25.85 ms (graph), 25.63-25.64 vs 25.76-25.82 eager, same box
 // (scripts/gpu_r05_pt.sh); bit-identical per accumulator
-#ifndef M3D_TUNE_X3_PAIR_TILES
-#define M3D_TUNE_X3_PAIR_TILES 1
-#endif
-#ifndef M3D_TUNE_X3_QUAD
-#define M3D_TUNE_X3_QUAD 0
-#endif
-#ifndef M3D_TUNE_X3_PAIR
-#define M3D_TUNE_X3_PAIR 1
-#endif
-#ifndef M3D_TUNE_X3_AF128
-#define M3D_TUNE_X3_AF128 0
-#endif
-#ifndef M3D_TUNE_X3_256
-#define M3D_TUNE_X3_256 1
-#endif
 // Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z.
 // 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
 // 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at
@@ -197,22 +149,10 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // vs 2.28e-6 with bit 0, F(2x2x4) data gradients) and the step slower (27.2 vs
 // 26.6 ms, gpurun_out/r05safe): the MFMA accumulator does better than an
 // fp32 rounding per instruction.  Kept as an A/B switch.
-#ifndef M3D_TUNE_X3_ACC
-#define M3D_TUNE_X3_ACC 0
-#endif
 // 1x1x1 conv epilogue inside x3_gemm256_af_kernel (1) or as a second pass (0)
-#ifndef M3D_TUNE_CONV1_EPI
-#define M3D_TUNE_CONV1_EPI 1
-#endif
 // conv_gemm epilogue: float4 rows per thread whose residual / destination loads
 // are issued together before their stores (4: round 4)
-#ifndef M3D_TUNE_EPI_PB
-#define M3D_TUNE_EPI_PB 4
-#endif
 // the implicit-GEMM convs on the bf16 split at 2 workgroups per CU instead of 3
-#ifndef M3D_TUNE_CONV_X3_OCC2
-#define M3D_TUNE_CONV_X3_OCC2 0
-#endif
 #ifndef M3D_TUNE_WINO_NY
 #define M3D_TUNE_WINO_NY 4
 #endif
@@ -222,95 +162,29 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_WINO_WGRAD_NZ
 #define M3D_TUNE_WINO_WGRAD_NZ 4
 #endif
-#ifndef M3D_TUNE_WINO_DGRAD_NZ
-#define M3D_TUNE_WINO_DGRAD_NZ 0
-#endif
 // the data gradient's y tile (conv3d.hip wino_dgrad_ny): 2 = F(2x2x4) data
 // gradients beside F(4x2x4) forwards / weight gradients (round 5, accuracy);
 // 0 = the forward's
 #ifndef M3D_TUNE_WINO_DGRAD_NY
 #define M3D_TUNE_WINO_DGRAD_NY 2
 #endif
-#ifndef M3D_TUNE_WINO_XCD
-#define M3D_TUNE_WINO_XCD 0
-#endif
-#ifndef M3D_TUNE_STEM_MFMA
-#define M3D_TUNE_STEM_MFMA 1
-#endif
-#ifndef M3D_TUNE_STEM_WGRAD
-#define M3D_TUNE_STEM_WGRAD 1
-#endif
-#ifndef M3D_TUNE_STEM_X3
-#define M3D_TUNE_STEM_X3 0
-#endif
 #ifndef M3D_TUNE_WGRAD1_X3_MIN_N
 #define M3D_TUNE_WGRAD1_X3_MIN_N 65
-#endif
-#ifndef M3D_TUNE_X3_BK
-#define M3D_TUNE_X3_BK 32
-#endif
-#ifndef M3D_TUNE_X3_OCC3
-#define M3D_TUNE_X3_OCC3 1
-#endif
-#ifndef M3D_TUNE_X3_PERSIST
-#define M3D_TUNE_X3_PERSIST 0
-#endif
-#ifndef M3D_TUNE_X3_256_DBG
-#define M3D_TUNE_X3_256_DBG 0
-#endif
-#ifndef M3D_TUNE_WINO_GRAD4
-#define M3D_TUNE_WINO_GRAD4 0
 #endif
 #ifndef M3D_TUNE_BN_BLOCKS
 #define M3D_TUNE_BN_BLOCKS 1024
 #endif
-#ifndef M3D_TUNE_NMS_REDUCE
-#define M3D_TUNE_NMS_REDUCE 1
-#endif
 #ifndef M3D_TUNE_ROI_SLICES
 #define M3D_TUNE_ROI_SLICES 8
-#endif
-#ifndef M3D_TUNE_ROI_REGION
-#define M3D_TUNE_ROI_REGION 0
-#endif
-#ifndef M3D_TUNE_ROI_BWD_GATHER
-#define M3D_TUNE_ROI_BWD_GATHER 1
-#endif
-#ifndef M3D_TUNE_ROI_SORT
-#define M3D_TUNE_ROI_SORT -1
-#endif
-#ifndef M3D_TUNE_ROI_STAGE
-#define M3D_TUNE_ROI_STAGE 0
-#endif
-#ifndef M3D_TUNE_ROI_ZSPLIT
-#define M3D_TUNE_ROI_ZSPLIT 1
-#endif
-#ifndef M3D_TUNE_ROI_PC
-#define M3D_TUNE_ROI_PC 0
 #endif
 // PyramidROIAlign forward in the separable row form (row_fwd_kernel) for pools
 // of depth >= this (0: off; A/B builds only -- bit-identical, but 1.03 ms vs the
 // line kernel's 0.88 ms at 256^3 14^3 and 0.24 vs 0.14 ms at 128^3, r04r)
-#ifndef M3D_TUNE_ROI_ROW
-#define M3D_TUNE_ROI_ROW 0
-#endif
 // ... its workgroups per output row (channel groups of 256 / CG channels)
-#ifndef M3D_TUNE_ROI_ROW_CG
-#define M3D_TUNE_ROI_ROW_CG 1
-#endif
 // x3_gemm256_af_kernel: A loaded three steps ahead (no wait inside a step).
 // Round 6 (profiles/r06_x3af_stamps_128.txt, per-step clock stamps): with A two
 // steps ahead the six unrolled step copies ran 3.9K-7.2K cycles (the compiler's
 // waits differed per copy, one drained the prefetch); three ahead, three copies,
 // 3.7K-4.6K; priced launch 0.998 -> 0.959 ms, 128^3 step 25.33 -> 24.96 ms (same box)
-#ifndef M3D_TUNE_X3AF_A3
-#define M3D_TUNE_X3AF_A3 1
-#endif
-#ifndef M3D_TUNE_X3AF
-#define M3D_TUNE_X3AF 0
-#endif
 // the 256x256 Winograd point GEMM only where it has at least this many tiles
 // (step A/B r04t1: 0 27.26 ms, 256 27.39, 512 27.36; isolated launches favoured 256)
-#ifndef M3D_TUNE_X3_256_MIN_TILES
-#define M3D_TUNE_X3_256_MIN_TILES 0
-#endif

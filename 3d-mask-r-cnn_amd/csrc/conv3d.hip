@@ -163,32 +163,12 @@ __device__ __forceinline__ uint32_t pk_bf16(f32x2_t v) {
 __device__ __forceinline__ f32x2_t unpk_bf16(uint32_t p) {
     return f32x2_t{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
 }
-#ifndef M3D_SPLIT_SCALAR
-#define M3D_SPLIT_SCALAR 0
-#endif
-#if M3D_SPLIT_SCALAR
-// two v_sub_f32 instead of one v_pk_add_f32 (packed f32 VALU beside MFMAs costs
-// more issue than its scalar pair, MI355X_MICROARCH.md cycle constants)
-__device__ __forceinline__ f32x2_t sub2(f32x2_t a, f32x2_t b) {
-    float r0, r1;
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r0) : "v"(a.x), "v"(b.x));
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r1) : "v"(a.y), "v"(b.y));
-    return f32x2_t{r0, r1};
-}
-__device__ __forceinline__ void split3x2(f32x2_t x, uint32_t& h, uint32_t& m, uint32_t& l) {
-    h = pk_bf16(x);
-    const f32x2_t r = sub2(x, unpk_bf16(h));
-    m = pk_bf16(r);
-    l = pk_bf16(sub2(r, unpk_bf16(m)));
-}
-#else
 __device__ __forceinline__ void split3x2(f32x2_t x, uint32_t& h, uint32_t& m, uint32_t& l) {
     h = pk_bf16(x);
     const f32x2_t r = x - unpk_bf16(h);
     m = pk_bf16(r);
     l = pk_bf16(r - unpk_bf16(m));
 }
-#endif
 __device__ __forceinline__ void split3x4(const float4& v, uint2* o) {
     uint32_t h0, m0, l0, h1, m1, l1;
     split3x2(f32x2_t{v.x, v.y}, h0, m0, l0);
@@ -197,111 +177,62 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2* o) {
     o[1] = make_uint2(m0, m1);
     o[2] = make_uint2(l0, l1);
 }
-// M3D_TUNE_X3_ACC bit 0: the point-GEMM kernels (x3_gemm*), bit 1: the
-// implicit-GEMM convs (conv_gemm_kernel X3), bit 2: the weight-gradient GEMMs
-constexpr int X3ACC_GEMM = M3D_TUNE_X3_ACC & 1, X3ACC_CONV = (M3D_TUNE_X3_ACC >> 1) & 1,
-              X3ACC_WG = (M3D_TUNE_X3_ACC >> 2) & 1;
 // One 16-deep k step of an fp32 product sum on the split: acc += sum_k a_k b_k
-// as the six bf16 MFMAs (small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi)
-// (hi,mid) (hi,hi)).  M3D_TUNE_X3_ACC 1 (round 5): the six run into a fresh
-// accumulator (C = 0) and the step's partial is added to acc by one VALU add
-// -- one rounding of |acc| per k step instead of six (each MFMA rounds its
-// result to fp32 at the accumulator's magnitude, however small its own
-// terms).  Halves the fp32 error of every x3 GEMM: a Winograd F(4x2x4) conv
-// 5.5e-6 -> 2.7e-6, F(2x2x4) 1.4e-6 -> 0.65e-6 of the output scale
-// (scripts/wino_stage_error.py, modes x3 / x3sep).  0: one accumulator chain.
-template <int X3ACC>
+// as the six bf16 MFMAs, small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi)
+// (hi,mid) (hi,hi), one accumulator chain.  (Round 5 measured the alternative
+// -- each k step's six into a fresh accumulator, one VALU add into acc -- on
+// the MI355X: the 128^3 gradient median rose 2.28e-6 -> 3.29e-6 and the step
+// slowed; the MFMA's accumulation into C beats an fp32 rounding per step.)
 __device__ __forceinline__ void x3_mac(floatx16& acc, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        const bf16x8& bh, const bf16x8& bm, const bf16x8& bl) {
-    if constexpr (X3ACC == 1) {
-        floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, floatx16{}, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, t, 0, 0, 0);
-        acc += t;
-    } else {
-        floatx16 c = acc;
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-    }
+    floatx16 c = acc;
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
 }
 // x3_mac of two accumulator tiles sharing the A fragment, their two six-MFMA
-// chains interleaved (M3D_TUNE_X3_PAIR): each accumulator sees its products in
-// x3_mac's order (bit-identical results), but consecutive MFMAs are independent,
-// so an MFMA does not wait for its predecessor's result.
-template <int X3ACC>
+// chains interleaved: each accumulator sees its products in x3_mac's order
+// (bit-identical results), but consecutive MFMAs are independent, so an MFMA
+// does not wait for its predecessor's result (weight-gradient GEMM -3 %).
 __device__ __forceinline__ void x3_mac_pair(floatx16& acc0, floatx16& acc1, const bf16x8& ah, const bf16x8& am,
                                             const bf16x8& al, const bf16x8& b0h, const bf16x8& b0m,
                                             const bf16x8& b0l, const bf16x8& b1h, const bf16x8& b1m,
                                             const bf16x8& b1l) {
-    if constexpr (X3ACC == 1 || !M3D_TUNE_X3_PAIR) {
-        x3_mac<X3ACC>(acc0, ah, am, al, b0h, b0m, b0l);
-        x3_mac<X3ACC>(acc1, ah, am, al, b1h, b1m, b1l);
-    } else {
-        floatx16 c0 = acc0, c1 = acc1;
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b0h, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b1h, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0m, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1m, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0l, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1l, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0h, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1h, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0m, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1m, c1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0h, c0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1h, c1, 0, 0, 0);
-    }
+    floatx16 c0 = acc0, c1 = acc1;
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b1h, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0m, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1m, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0l, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1l, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b1h, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0m, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1m, c1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0h, c0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1h, c1, 0, 0, 0);
 }
 // x3_mac over a wave's TM x TN accumulator tiles with fragments af[i][plane],
-// bf[j][plane].  X3ACC 1: a lag-1 pipeline -- tile q's six MFMAs issue beside
-// tile q-1's VALU add, a scheduling barrier per tile keeps two step partials
-// live (without it the compiler runs every tile's chain first and holds all
-// their partials: spills in the 128x128 kernels).
-// LAG false: each tile's partial added right behind its own chain (one partial
-// live; the add waits for the chain's last MFMA -- for kernels at the register limit)
-template <int TM, int TN, int X3ACC, bool LAG = true>
+// bf[j][plane], tile pairs interleaved (x3_mac_pair)
+template <int TM, int TN>
 __device__ __forceinline__ void x3_mac_tiles(floatx16 (&acc)[TM][TN], const bf16x8 (&af)[TM][3],
                                              const bf16x8 (&bf)[TN][3]) {
-    if constexpr (X3ACC == 1) {
-        floatx16 pend;
-#pragma unroll
-        for (int q = 0; q < TM * TN; ++q) {
-            const int i = q / TN, j = q % TN;
-            floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bf[j][0], floatx16{}, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bf[j][1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][2], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bf[j][0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bf[j][0], t, 0, 0, 0);
-            if constexpr (LAG) {
-                if (q > 0) acc[(q - 1) / TN][(q - 1) % TN] += pend;
-                pend = t;
-            } else {
-                acc[i][j] += t;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (LAG) acc[TM - 1][TN - 1] += pend;
-    } else if constexpr (TN % 2 == 0 && M3D_TUNE_X3_PAIR_TILES) {
+    if constexpr (TN % 2 == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; j += 2)
-                x3_mac_pair<0>(acc[i][j], acc[i][j + 1], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2],
-                               bf[j + 1][0], bf[j + 1][1], bf[j + 1][2]);
+                x3_mac_pair(acc[i][j], acc[i][j + 1], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2],
+                            bf[j + 1][0], bf[j + 1][1], bf[j + 1][2]);
     } else {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                x3_mac<0>(acc[i][j], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2]);
+                x3_mac(acc[i][j], af[i][0], af[i][1], af[i][2], bf[j][0], bf[j][1], bf[j][2]);
     }
 }
 // byte offset of (row, k) in an X3 LDS plane: 32 k x bf16 = 64-B rows, 16-B
@@ -480,7 +411,7 @@ __device__ __forceinline__ void epi_store4_pre(const ConvP& p, const Epi& e, int
 // spill at 3, and must not touch the register budget of the other forms)
 template <int BM, int BN, int WM, int WN, bool BT, bool AVEC, int BK, int NBUF, bool PERSIST = false,
           bool X3 = false, bool FBN = false>
-__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (X3ACC_CONV || M3D_TUNE_CONV_X3_OCC2)) ? 3 : 2)) void conv_gemm_kernel(ConvP p,
+__global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN ? 3 : 2)) void conv_gemm_kernel(ConvP p,
                                                                                                   Epi e) {
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(!X3 || (BK == 32 && NBUF == 1 && AVEC && (BT || BN >= 64)), "X3 mode");
@@ -721,13 +652,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
         }
     };
 
-#ifndef M3D_EPI_PREFETCH
-#define M3D_EPI_PREFETCH 1   // 0: the epilogue loads its residual / accumulated rows one store at a time
-#endif
-#ifndef M3D_CONV_DBG
-#define M3D_CONV_DBG 0   // timing probes (debug builds): 1 no epilogue, 2 no k-loop (epilogue only)
-#endif
-    const int nk = M3D_CONV_DBG == 2 ? 0 : (p.K + BK - 1) / BK;
+    const int nk = (p.K + BK - 1) / BK;
     const int h = lane >> 5, l32 = lane & 31;
     load_tile(0);
     store_tile(0);
@@ -749,7 +674,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
             const char* Bb = Ab + 3 * BM * BK * 2;
             // (fresh-accumulator form: one k step at a time -- unrolled, the two
             // steps' fragments and partials exceed the register budget)
-#pragma unroll X3ACC_CONV ? 1 : 2
+#pragma unroll 2
             for (int s16 = 0; s16 < BK / 16; ++s16) {
                 // lane (l32, h): row l32, k = 16 s16 + 8h .. +7 (one 16-B chunk)
                 bf16x8 af[TM][3], bfr[TN][3];
@@ -767,7 +692,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
                     for (int pl = 0; pl < 3; ++pl)
                         bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * (BN * BK * 2) + off);
                 }
-                x3_mac_tiles<TM, TN, X3ACC_CONV, false>(acc, af, bfr);
+                x3_mac_tiles<TM, TN>(acc, af, bfr);
             }
         } else {
         const float* As = smem + buf * (A_SZ + B_SZ);
@@ -829,19 +754,6 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
     // PERSIST: once the accumulators are staged in LDS (acc dead), map the
     // next tile and put its first k-tile loads in flight behind this tile's
     // global epilogue stores.
-#if M3D_CONV_DBG == 1
-    if constexpr (!PERSIST) {
-        float t = 0.0f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-        if (t == 1.2345f) e.y[0] = t;
-        return;
-    }
-#endif
     const int64_t m0c = m0;
     const int n0c = n0;
     const int64_t Ln = L + Lstep;
@@ -855,7 +767,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
     constexpr int C4T = BN / 4;
     constexpr int QN = (HR * C4T + 255) / 256;
     // residual / accumulated-destination rows loaded before the staging (block-uniform)
-    const bool pf = !PERSIST && M3D_EPI_PREFETCH && e.simple && e.split <= 0 && !(e.ldy & 3) &&
+    const bool pf = !PERSIST && e.simple && e.split <= 0 && !(e.ldy & 3) &&
                     ((e.res_mode == 1 && !e.accumulate) || (e.res_mode == 0 && e.accumulate));
     float fs[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // fused BN sums
     // fused BN: a thread's channel quad is the same in every batch (256 % C4T == 0)
@@ -893,7 +805,7 @@ __global__ __launch_bounds__(256, BK == 64 ? 1 : (NBUF == 1 && !FBN && !(X3 && (
         }
         // PB float4 per thread per batch: with pf, the batch's residual /
         // destination loads are all issued before its first store
-        constexpr int PB = QN < M3D_TUNE_EPI_PB ? QN : M3D_TUNE_EPI_PB;
+        constexpr int PB = QN < 4 ? QN : 4;
         static_assert(QN % PB == 0, "epilogue batches");
 #pragma unroll
         for (int q0 = 0; q0 < QN; q0 += PB) {
@@ -1246,19 +1158,6 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(ConvP p, const float
 }
 
 // ------------------------------------------------------------------ dispatch
-// M3D_GEMM_NBUF=1 (default: 3 blocks/CU, measured 3-5 % faster) or 2 (double-
-// buffered LDS, 2 blocks/CU) selects the k-loop (A/B testing)
-static int gemm_nbuf_env() {
-    static constexpr int v = M3D_TUNE_GEMM_NBUF;
-    return v;
-}
-
-// M3D_GEMM_PERSIST=0 disables the persistent tile loop of the batched
-// (Winograd) GEMMs (A/B testing; default on).
-static int gemm_persist_env() {
-    static constexpr int v = M3D_TUNE_GEMM_PERSIST;
-    return v;
-}
 // CUs of the calling thread's current device, asked per call (the runtime
 // answers from its device table): nothing is cached across calls or devices
 static int num_cus() {
@@ -1306,75 +1205,48 @@ static void launch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch)
         }
     }
     if constexpr (BK == 32 && AVEC) {      // (the scalar-A loader spills at 3 blocks/CU)
+        // one LDS stage at 3 blocks/CU (3-5 % faster than two stages at 2); the
+        // batched plain GEMMs (Winograd points) as a persistent tile loop
         const int64_t tiles = (int64_t)grid.x * grid.y * nbatch;
-        const int64_t resident = (int64_t)num_cus() * (gemm_nbuf_env() == 1 ? 3 : 2);
+        const int64_t resident = (int64_t)num_cus() * 3;
         const bool plain = e.simple && !e.bias && !e.scale && !e.res_mode && !e.relu && !e.z && !e.split &&
                            !e.accumulate && !e.deconv && !e.fbn && (e.ldy & 3) == 0;
+        const bool persist = nbatch > 1 && plain && tiles > 2 * resident;
+        ConvP pp = p;
+        pp.nbatch = nbatch;
+        const unsigned g = (unsigned)(resident / 8 * 8);
         if constexpr (BT || BN >= 64) {
-            if (conv_x3_env() && gemm_nbuf_env() == 1) {
-                if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
-                    ConvP pp = p;
-                    pp.nbatch = nbatch;
-                    const unsigned g = (unsigned)(resident / 8 * 8);
+            if (conv_x3_env()) {
+                if (persist)
                     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, true, true>), dim3(g),
                                        dim3(256), 0, s, pp, e);
-                } else {
+                else
                     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, false, true>), grid,
                                        dim3(256), 0, s, p, e);
-                }
                 return;
             }
         }
-        if (nbatch > 1 && plain && gemm_persist_env() && tiles > 2 * resident) {
-            ConvP pp = p;
-            pp.nbatch = nbatch;
-            const unsigned g = (unsigned)(resident / 8 * 8);
-            if (gemm_nbuf_env() == 1)
-                hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, true>), dim3(g), dim3(256),
-                                   0, s, pp, e);
-            else
-                hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 2, true>), dim3(g), dim3(256),
-                                   0, s, pp, e);
-            return;
-        }
-        if (gemm_nbuf_env() == 1) {
+        if (persist)
+            hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1, true>), dim3(g), dim3(256), 0, s,
+                               pp, e);
+        else
             hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 1>), grid, dim3(256), 0, s, p, e);
-            return;
-        }
+        return;
     }
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BT, AVEC, BK, 2>), grid, dim3(256), 0, s, p, e);
 }
 
-// M3D_GEMM_BK=64 selects 64-deep k-tiles (1 block/CU: measured 25-30% slower
-// than 32-deep at 2 blocks/CU; kept for A/B testing)
-static int gemm_bk_env() {
-    static constexpr int v = M3D_TUNE_GEMM_BK;
-    return v;
-}
-
-template <int BM, int BN, int WM, int WN, bool BT, bool AVEC>
-static void launch_gemm_bk(bool bk64, const ConvP& p, const Epi& e, hipStream_t s, int nbatch) {
-    if constexpr (AVEC) {
-        if (bk64) {
-            launch_gemm<BM, BN, WM, WN, BT, AVEC, 64>(p, e, s, nbatch);
-            return;
-        }
-    }
-    launch_gemm<BM, BN, WM, WN, BT, AVEC, 32>(p, e, s, nbatch);
-}
-
 template <bool BT, bool AVEC>
 static void dispatch_gemm(const ConvP& p, const Epi& e, hipStream_t s, int nbatch = 1) {
-    // 64-deep k-tiles when a k-tile stays inside one tap (C % 64 == 0)
-    const bool bk64 = AVEC && p.C % 64 == 0 && gemm_bk_env() == 64 && !e.fbn;
+    // 32-deep k-tiles (64-deep at 1 block/CU measured 25-30 % slower)
     if (p.N <= 32) {
         launch_gemm<128, 32, 4, 1, BT, AVEC, 32>(p, e, s, nbatch);
     } else if (p.N <= 64) {
-        launch_gemm_bk<128, 64, 4, 1, BT, AVEC>(bk64, p, e, s, nbatch);
+        launch_gemm<128, 64, 4, 1, BT, AVEC, 32>(p, e, s, nbatch);
     } else {
         const int64_t blocks128 = ((p.M + 127) / 128) * ((p.N + 127) / 128) * nbatch;
-        if (blocks128 < 512) launch_gemm_bk<64, 128, 2, 2, BT, AVEC>(bk64, p, e, s, nbatch);
-        else launch_gemm_bk<128, 128, 2, 2, BT, AVEC>(bk64, p, e, s, nbatch);
+        if (blocks128 < 512) launch_gemm<64, 128, 2, 2, BT, AVEC, 32>(p, e, s, nbatch);
+        else launch_gemm<128, 128, 2, 2, BT, AVEC, 32>(p, e, s, nbatch);
     }
 }
 
@@ -1384,26 +1256,12 @@ static int wgrad_minm_env() {
     static constexpr int v = M3D_TUNE_WGRAD_MINM;
     return v;
 }
-// M3D_WGRAD_K64=0 disables the 64-deep (K <= 64) weight-gradient tiles
-static int wgrad_k64_env() {
-    static constexpr int v = M3D_TUNE_WGRAD_K64;
-    return v;
-}
 
 template <int BI, int BJ, int WI, int WJ, bool AVEC, bool HALO = false>
 static void launch_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s, int nbatch = 1) {
     const int64_t tiles = (int64_t)((p.K + BI - 1) / BI) * ((p.N + BJ - 1) / BJ) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;                   // aim >= 1024 blocks
     int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
-    // M3D_TUNE_WGRAD_FILL: a launch whose grid at that floor is below one
-    // workgroup per CU (small-m gradients: the RPN heads' 1x1x1 weight gradient
-    // on P3-P6 ran 4-32 workgroups of 512 rows, ~38 us each regardless of m)
-    // halves the floor down to 64 rows until it fills the chip.
-    static constexpr int fill = M3D_TUNE_WGRAD_FILL;
-    if constexpr (fill != 0) {
-        const int64_t cus = num_cus();
-        while (minm > 64 && tiles * ((p.M + minm - 1) / minm) < cus) minm /= 2;
-    }
     const int64_t max_splits = (p.M + minm - 1) / minm;             // >= minm m per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -1504,7 +1362,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
     __syncthreads();
     for (int t = 0; t < nchunks; ++t) {
         if (t + 1 < nchunks) load(ms + (int64_t)(t + 1) * BKM);
-#pragma unroll X3ACC_WG ? 1 : 2
+#pragma unroll 2
         for (int s16 = 0; s16 < 2; ++s16) {
             bf16x8 af[TI][3], bfr[TJ][3];
 #pragma unroll
@@ -1519,7 +1377,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PL + off);
             }
-            x3_mac_tiles<TI, TJ, X3ACC_WG>(acc, af, bfr);
+            x3_mac_tiles<TI, TJ>(acc, af, bfr);
         }
         __syncthreads();
         if (t + 1 < nchunks) {
@@ -1675,7 +1533,7 @@ __device__ __forceinline__ void x3w_segment(char* __restrict__ smem, const float
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
                 continue;
             }
-            x3_mac_pair<X3ACC_WG>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+            x3_mac_pair(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
                                   bfr[1][0], bfr[1][1], bfr[1][2]);
         }
     };
@@ -1781,8 +1639,7 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
     const int64_t cus = num_cus();
     static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
-    static constexpr int dbg = M3D_TUNE_X3W_DBG;
-    if (M3D_TUNE_X3W_SK && dbg == 0 && !det().on && M >= 32 * W2_BK) {
+    if (M3D_TUNE_X3W_SK && !det().on && M >= 32 * W2_BK) {
         // stream-K (X3wSK): one balanced round of workgroups, each >= minm rows
         // (only for tiles of >= 32 steps: with short tiles the minm floor would
         // give one workgroup a run of tiles, each with its own atomic epilogue)
@@ -1799,10 +1656,7 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
                            (int64_t)0, bsa, bsb, bsc, WgOut{nullptr, 0, 0}, sk);
         return;
     }
-    // M3D_X3W_TR_FLOOR=1: splits = floor(CUs / tiles) (one wave of workgroups at
-    // one per CU) instead of the ceiling (e.g. 96 tiles: 2 x 96 vs 3 x 96 = 288)
-    static constexpr int fl = M3D_TUNE_X3W_TR_FLOOR;
-    int64_t splits = fl ? cus / tiles : (cus + tiles - 1) / tiles;
+    int64_t splits = (cus + tiles - 1) / tiles;
     // M3D_X3W_TR_MINM: fewest m rows per workgroup.  Every split adds a 256x256
     // fp32 atomic epilogue: the small-m 1x1x1 gradients of res4 / res5 (m = 8192
     // / 2048 at 128^3, 4 output tiles) split 64 ways at the old floor of 64 rows,
@@ -1812,35 +1666,13 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
-    // M3D_X3W_TR_QUANT=Q (A/B): pick splits in [1, max(splits, Q)] minimising
-    // the number of one-per-CU waves per unit of work, ceil(tiles * s / CUs) / s
-    // (e.g. the F(4x2x4) RPN gradient: 288 tiles = 1.125 waves run as 2 at
-    // s = 1, 9 / 8 at s = 8), within the m floor above.
-    static constexpr int quant = M3D_TUNE_X3W_TR_QUANT;
-    if constexpr (quant > 1) {
-        double best = 1e30;
-        const int64_t qmax = splits > quant ? splits : quant;
-        for (int64_t q = 1; q <= qmax && q <= max_splits; ++q) {
-            const double cost = (double)((tiles * q + cus - 1) / cus) / (double)q;
-            if (cost < best - 1e-9) { best = cost; splits = q; }
-        }
-    }
     const WgOut wo = wg_out(splits, nbatch, K, N);
     int64_t mper = (M + splits - 1) / splits;
     mper = (mper + W2_BK - 1) / W2_BK * W2_BK;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 255) / 256), (unsigned)((N + 255) / 256), (unsigned)(splits * nbatch));
-    const X3wSK nosk{};
-    if constexpr (dbg == 0) {
-        hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk);
-    } else switch (dbg) {
-        case 1: hipLaunchKernelGGL(x3_wgrad_tr_kernel<1>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
-        case 2: hipLaunchKernelGGL(x3_wgrad_tr_kernel<2>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
-        case 3: hipLaunchKernelGGL(x3_wgrad_tr_kernel<3>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
-        case 5: hipLaunchKernelGGL(x3_wgrad_tr_kernel<5>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
-        case 4: hipLaunchKernelGGL(x3_wgrad_tr_kernel<4>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk); break;
-        default: hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo, nosk);
-    }
+    hipLaunchKernelGGL(x3_wgrad_tr_kernel<0>, grid, dim3(512), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo,
+                       X3wSK{});
     wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
 }
 
@@ -1850,24 +1682,13 @@ static int wgrad_x3_env() { return (x3_mask() >> 2) & 1; }
 // C[b] += A[b]^T B[b]: A [M][K], B [M][N], C [K][N], batch strides bsa/bsb/bsc
 static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M, int K, int N, int nbatch,
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
-    // M3D_X3W_TR_MIN_M: smallest m (per batch) taking the 256x256 kernel (small-m
-    // gradients split m finely to fill the chip, one atomic epilogue per split)
-    static constexpr int64_t tr_min_m = M3D_TUNE_X3W_TR_MIN_M;
-    if (wgrad_tr_env() && K >= 192 && N >= 192 && M >= tr_min_m) {
+    if (wgrad_tr_env() && K >= 192 && N >= 192) {
         launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
         return;
     }
     const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
     int64_t splits = (1024 + tiles - 1) / tiles;
-    // M3D_X3W_MINM: this kernel's m-split floor (default: M3D_WGRAD_MINM's)
-    static constexpr int x3w_minm = M3D_TUNE_X3W_MINM;
-    const int64_t mfloor = x3w_minm > 0 ? x3w_minm : wgrad_minm_env();
-    int64_t minm = mfloor > 32 ? mfloor : 32;
-    static constexpr int fill = M3D_TUNE_WGRAD_FILL;   // as in launch_wgrad
-    if constexpr (fill != 0) {
-        const int64_t cus = num_cus();
-        while (minm > 64 && tiles * ((M + minm - 1) / minm) < cus) minm /= 2;
-    }
+    const int64_t minm = wgrad_minm_env() > 32 ? wgrad_minm_env() : 32;
     const int64_t max_splits = (M + minm - 1) / minm;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -1876,11 +1697,8 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
     mper = (mper + 31) / 32 * 32;
     splits = (M + mper - 1) / mper;
     dim3 grid((unsigned)((K + 127) / 128), (unsigned)((N + 127) / 128), (unsigned)(splits * nbatch));
-    static constexpr int occ = M3D_TUNE_X3W_OCC;
-    if constexpr (occ == 2)
-        hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
-    else
-        hipLaunchKernelGGL((x3_wgrad_kernel<3>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
+    // 2 blocks/CU (3 at 164 VGPRs: faster alone, step unchanged)
+    hipLaunchKernelGGL((x3_wgrad_kernel<2>), grid, dim3(256), 0, s, A, Bm, C, M, K, N, mper, bsa, bsb, bsc, wo);
     wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
 }
 
@@ -1965,23 +1783,12 @@ __device__ __forceinline__ void gt4(float v0, float v1, float v2, float v3, floa
 // written once and read once by the point GEMMs, and M is read once by the
 // output transform: non-temporal, so the streams do not evict the input tile
 // rows that neighbouring tiles re-read (each input element belongs to up to
-// 2x2x2 overlapping 4x4xP windows).  M3D_WINO_NT=0 for A/B.
-#ifndef M3D_WINO_NT
-#define M3D_WINO_NT 1
-#endif
+// 2x2x2 overlapping 4x4xP windows).
 __device__ __forceinline__ void wino_st(float* p, float v) {
-#if M3D_WINO_NT
     __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 __device__ __forceinline__ float wino_ld(const float* p) {
-#if M3D_WINO_NT
     return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
 }
 
 // z-axis transforms of F(NZ,3): P = NZ + 2 points
@@ -2523,76 +2330,6 @@ __global__ __launch_bounds__(256) void wino_grad_kernel(const float* __restrict_
         }
 }
 
-#if M3D_TUNE_WINO_GRAD4
-// The same transform with 4 consecutive channels per thread (N % 4 == 0):
-// 16-B loads and non-temporal 16-B stores (1 KiB per wave-instruction instead
-// of 256 B) for this write-dominated kernel (P*16 outputs per 2x2xNZ inputs).
-// Per element the same arithmetic as wino_grad_kernel (bit-identical).
-typedef float f4vec __attribute__((ext_vector_type(4)));
-template <int NZ>
-__global__ __launch_bounds__(256) void wino_grad4_kernel(const float* __restrict__ dz, WinoGeom g,
-                                                         int N, float* __restrict__ DY) {
-    constexpr int P = ZT<NZ>::P;
-    static_assert(WNY == 2, "wino_grad4_kernel: F(2,3) on y only");
-    const int N4 = N >> 2;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= g.T * N4) return;
-    const int n4 = (int)(i % N4);
-    const int64_t t = i / N4;
-    int b, ty, tx, tz;
-    tile_coords(t, g, b, ty, tx, tz);
-    f4vec ev[2][2][NZ];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-            for (int k = 0; k < NZ; ++k) {
-                const int y = 2 * ty + a, xx = 2 * tx + bb, z = NZ * tz + k;
-                ev[a][bb][k] = (y < g.H && xx < g.W && z < g.D)
-                                   ? *reinterpret_cast<const f4vec*>(
-                                         dz + ((((int64_t)b * g.H + y) * g.W + xx) * g.D + z) * N + 4 * n4)
-                                   : f4vec{0.f, 0.f, 0.f, 0.f};
-            }
-    // z transform (ZT::a on each of the 4 channels), then x (a4), then y (a4)
-    f4vec t1[2][2][P];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            float e[4][NZ], o[4][P];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                for (int k = 0; k < NZ; ++k) e[q][k] = ev[a][bb][k][q];
-                ZT<NZ>::a(e[q], o[q]);
-            }
-#pragma unroll
-            for (int k = 0; k < P; ++k) t1[a][bb][k] = f4vec{o[0][k], o[1][k], o[2][k], o[3][k]};
-        }
-    const int64_t stride = g.T * N;
-    float* out = DY + t * N + 4 * n4;
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        f4vec t2[2][4];
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            // a4(e0, e1) = [e0, e0 + e1, e0 - e1, -e1] per channel
-            const f4vec e0 = t1[a][0][k], e1 = t1[a][1][k];
-            t2[a][0] = e0; t2[a][1] = e0 + e1; t2[a][2] = e0 - e1; t2[a][3] = -e1;
-        }
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-            const f4vec e0 = t2[0][bb], e1 = t2[1][bb];
-            const f4vec o[4] = {e0, e0 + e1, e0 - e1, -e1};
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-                __builtin_nontemporal_store(o[a], reinterpret_cast<f4vec*>(out + (int64_t)((a * 4 + bb) * P + k) * stride));
-        }
-    }
-}
-
-#endif  // M3D_TUNE_WINO_GRAD4
 // dW[t][c][n] += (G^T (x) G^T (x) Gz^T) dWh[.][c][n]
 template <int NZ>
 __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ dWh, int C,
@@ -2694,9 +2431,6 @@ __device__ __forceinline__ int x3_off16(int row, int kc) {
     return row * 32 + (((kc ^ (row >> 3)) & 1) << 4);
 }
 
-#ifndef M3D_X3_DBG
-#define M3D_X3_DBG 0   // timing probes of x3_gemm_kernel (debug builds only): 1 no MFMA, 2 no loads
-#endif
 // BK 16: two LDS stages (one barrier per k-tile), 3 blocks/CU; BK 32: one
 // stage (two barriers per k-tile), 2 blocks/CU.
 template <int BK>
@@ -2760,10 +2494,6 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
 #pragma unroll
                 for (int u = 0; u < CPT; ++u) {
                     const int off = (int)(lrow[u] + (uint32_t)kt * (BK * 2));
-#if M3D_X3_DBG == 2   // timing probe: no global loads
-                    if constexpr (!AF32) va[q][u] = make_uint4(off, q, u, kt);
-                    vb[q][u] = make_uint4(kt, u, q, off);
-#else
                     if constexpr (AF32) {
                         if (q == 0) {   // element offset of the chunk = byte offset of its bf16 image / 2
                             fa[u][0] = bload4(ra[0], (uint32_t)off * 2u);
@@ -2773,7 +2503,6 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                         va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
                     }
                     vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
-#endif
                 }
         };
         auto store = [&](int buf) {
@@ -2811,7 +2540,7 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
             if (kt + 1 < nk) load(kt + 1);
             const char* As = smem + (NBUF == 2 ? (kt & 1) : 0) * STAGE;
             const char* Bs = As + 3 * PLA;
-#pragma unroll X3ACC_GEMM ? 1 : BK / 16
+#pragma unroll BK / 16
             for (int s16 = 0; s16 < BK / 16; ++s16) {
                 // lane (l32, h): row l32 of its 32-row blocks, k = 16 s16 + 8h .. +7
                 bf16x8 af[TM][3], bfr[TN][3];
@@ -2828,15 +2557,7 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                     for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PLB + off);
                 }
                 // small terms first: (lo,hi) (mid,mid) (hi,lo) (mid,hi) (hi,mid) (hi,hi)
-#if M3D_X3_DBG == 1   // timing probe: no MFMA (fragments still consumed)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j][0] += (float)(af[i][0][0] ^ af[i][1][1] ^ af[i][2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
-#else
-                x3_mac_tiles<TM, TN, X3ACC_GEMM>(acc, af, bfr);
-#endif
+                x3_mac_tiles<TM, TN>(acc, af, bfr);
             }
             if constexpr (NBUF == 2) {
                 // the other stage was last read in iteration kt-1, before its closing barrier
@@ -2975,7 +2696,7 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
                     acc[i][j][0] += (float)(af[0][0] ^ af[1][1] ^ af[2][2] ^ bfr[j][0][3] ^ bfr[j][1][4] ^ bfr[j][2][5]);
                 continue;
             }
-            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+            x3_mac_pair(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
                                     bfr[1][0], bfr[1][1], bfr[1][2]);
         }
     }
@@ -3028,8 +2749,6 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_kernel(X3G g) {
 // alias and inserts no vmcnt(0) drain of the prefetch.  Same split, same MFMA
 // order: bit-identical to x3_gemm256_kernel.
 template <int N_> struct IC { static constexpr int v = N_; };
-// M3D_TUNE_X3AF (A/B bits): 1 static s_setprio 1 for waves 4-7, 2 s_setprio
-// around each step's MFMA cluster, 8 all six stages in ONE __shared__ array
 // EPI (compile-time, one instantiation per epilogue so each gets its own
 // register allocation): 0 the plain C store, 1 the forward conv epilogue,
 // 2 the fused BN-ReLU backward (X3Epi.on)
@@ -3049,22 +2768,11 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     char* const sB2 = sAll + 15 * G2_PL;
     const uint32_t st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
     const uint32_t st_r0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#elif M3D_TUNE_X3AF & 8
-    __shared__ __attribute__((aligned(16))) char sAll[18 * G2_PL];
-    char* const sA0 = sAll;
-    char* const sA1 = sAll + 3 * G2_PL;
-    char* const sA2 = sAll + 6 * G2_PL;
-    char* const sB0 = sAll + 9 * G2_PL;
-    char* const sB1 = sAll + 12 * G2_PL;
-    char* const sB2 = sAll + 15 * G2_PL;
 #else
     __shared__ __attribute__((aligned(16))) char sA0[3 * G2_PL], sA1[3 * G2_PL], sA2[3 * G2_PL];
     __shared__ __attribute__((aligned(16))) char sB0[3 * G2_PL], sB1[3 * G2_PL], sB2[3 * G2_PL];
 #endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#if M3D_TUNE_X3AF & 1
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
     const int wm = wave >> 2, wn = wave & 3, h = lane >> 5, l32 = lane & 31;
     const int64_t nbx = (g.M + 255) / 256, nby = g.N / 256;
     const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
@@ -3097,41 +2805,18 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         else if constexpr (decltype(st)::v == 1) return sB1;
         else return sB2;
     };
-#ifndef M3D_X3AF_KB
-#define M3D_X3AF_KB 0
-#endif
-#if M3D_X3AF_KB   // timing probe: k-blocked addressing (wrong values)
-    const __amdgpu_buffer_rsrc_t rak = make_rsrc(g.af + bz * g.bsa, (uint64_t)g.M * g.K * 4);
-    __amdgpu_buffer_rsrc_t rbk[3];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) rbk[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb, (uint64_t)g.N * g.K * 2);
-#endif
     using AReg = float4;
     auto load_a = [&](int kt, float4 (&v)[2]) {
         const bool in = kt < nk;
-#if M3D_X3AF_KB & 2
-        const uint32_t o = ((uint32_t)(kt * g.M + m0 + arow) * 16u + (uint32_t)ach * 8u) * 4u;
-        v[0] = bload4(rak, in ? o : M3D_OOB);
-        v[1] = bload4(rak, in ? o + 16u : M3D_OOB);
-#else
         const uint32_t o = aoff0 + (uint32_t)kt * (G2_BK * 4);
         v[0] = bload4(ra, in ? o : M3D_OOB);
         v[1] = bload4(ra, in ? o + 16u : M3D_OOB);
-#endif
     };
     auto dma_b = [&](auto st, int kt) {
         char* S = stB(st) + wave * 1024;
-#if M3D_X3AF_KB & 1
-        const uint32_t off = kt < nk ? ((uint32_t)(kt * g.N + n0 + lrow) * 16u) * 2u +
-                                           (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4)
-                                     : M3D_OOB;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) g2_dma(rbk[pl], S + pl * G2_PL, off);
-#else
         const uint32_t off = kt < nk ? lsrc + (uint32_t)kt * (G2_BK * 2) : M3D_OOB;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G2_PL, off);
-#endif
     };
     auto split_a = [&](auto st, const AReg (&v)[2]) {
         char* S = stA(st) + awr;
@@ -3149,7 +2834,6 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-#if M3D_TUNE_X3AF_A3
     // A three steps ahead (three register sets): per step A(kt+3) then B(kt+2)
     // are issued, so A(kt+1) (issued at step kt-2, before B(kt)) is retired by
     // the top-of-step wait for B(kt) and no wait sits inside the step
@@ -3161,15 +2845,6 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
     dma_b(IC<1>{}, 1);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A(0)
     split_a(IC<0>{}, xa);
-#else
-    float4 xa[2], ya[2];            // A rows of the even / odd steps
-    load_a(0, xa);
-    dma_b(IC<0>{}, 0);
-    load_a(1, ya);
-    dma_b(IC<1>{}, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A(0)
-    split_a(IC<0>{}, xa);
-#endif
 #if M3D_X3AF_STAMP
     const uint32_t st_t1 = (uint32_t)__builtin_amdgcn_s_memtime();
 #endif
@@ -3182,14 +2857,8 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #if M3D_X3AF_STAMP
         if (tid == 0 && kt < 56) stampbuf[kt] = (uint32_t)__builtin_amdgcn_s_memtime();
 #endif
-#if M3D_TUNE_X3AF_A3
         load_a(kt + 3, nxt);
         dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
-#else
-        load_a(kt + 2, nxt);
-        dma_b(IC<(s0 + 2) % 3>{}, kt + 2);       // stage last read at step kt-1
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");              // A(kt+1)
-#endif
         split_a(IC<(s0 + 1) % 3>{}, cur);        // stage last read at step kt-2
         const char* SA = stA(st);
         const char* SB = stB(st);
@@ -3201,65 +2870,23 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
             for (int pl = 0; pl < 3; ++pl)
                 bfr[j][pl] = *reinterpret_cast<const bf16x8*>(SB + pl * G2_PL + off);
         }
-#if M3D_TUNE_X3AF & 2
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#if M3D_TUNE_X3_QUAD
-        // two A rows' fragments at once: four independent six-MFMA chains interleaved
-#pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-            bf16x8 af[2][3];
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii) {
-                const int off = x3_off16(wm * 128 + (i + ii) * 32 + l32, h);
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) af[ii][pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
-            }
-            floatx16 c00 = acc[i][0], c01 = acc[i][1], c10 = acc[i + 1][0], c11 = acc[i + 1][1];
-            // per accumulator x3_mac's order: (l,h) (m,m) (h,l) (m,h) (h,m) (h,h)
-            const int pa[6] = {2, 1, 0, 1, 0, 0}, pb[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t) {
-                c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][pa[t]], bfr[0][pb[t]], c00, 0, 0, 0);
-                c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][pa[t]], bfr[1][pb[t]], c01, 0, 0, 0);
-                c10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][pa[t]], bfr[0][pb[t]], c10, 0, 0, 0);
-                c11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][pa[t]], bfr[1][pb[t]], c11, 0, 0, 0);
-            }
-            acc[i][0] = c00; acc[i][1] = c01; acc[i + 1][0] = c10; acc[i + 1][1] = c11;
-        }
-#else
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int off = x3_off16(wm * 128 + i * 32 + l32, h);
             bf16x8 af[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G2_PL + off);
-            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
+            x3_mac_pair(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
                                     bfr[1][0], bfr[1][1], bfr[1][2]);
         }
-#endif
-#if M3D_TUNE_X3AF & 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
     };
     // stage kt % 3 and register set kt % 2 static: six steps per trip
-#if M3D_TUNE_X3AF_A3
     // step kt: cur = set (kt+1) % 3 holds A(kt+1), nxt = set kt % 3 (A(kt) split at step kt-1)
     for (int kt = 0;;) {
         step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
         step(IC<1>{}, kt, za, ya); if (++kt >= nk) break;
         step(IC<2>{}, kt, xa, za); if (++kt >= nk) break;
     }
-#else
-    for (int kt = 0;;) {
-        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
-        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
-        step(IC<2>{}, kt, ya, xa); if (++kt >= nk) break;
-        step(IC<0>{}, kt, xa, ya); if (++kt >= nk) break;
-        step(IC<1>{}, kt, ya, xa); if (++kt >= nk) break;
-        step(IC<2>{}, kt, xa, ya); if (++kt >= nk) break;
-    }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
 #if M3D_X3AF_STAMP
     const uint32_t st_t2 = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -3401,161 +3028,6 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #endif
 }
 
-#if M3D_TUNE_X3_AF128
-// ---- the same GEMM with 256x128 tiles, 4 waves, two workgroups per CU -------
-// x3_gemm256_af_kernel holds one workgroup per CU (144 KB of LDS), so while it
-// stores its tile (the fp32 C it writes is 2/3 of its HBM traffic) the CU's
-// MFMA pipes idle.  Here a workgroup is 4 waves on a 256x128 tile (each wave
-// the same 128x64 block, fragments and MFMA order: bit-identical results) with
-// two 36-KB LDS stages, so two workgroups fit a CU and one's stores overlap the
-// other's main loop.  Per step and wave: B-DMA(kt+1) (3 ops, the stage read at
-// step kt-1), then A-load(kt+2) (4 ops, two rows per thread); vmcnt(4) at the
-// top retires B(kt), vmcnt(7) the A rows of step kt+1 before they are split.
-constexpr int G3_PLA = 256 * G2_BK * 2;   // one A plane of a stage: 8 KB
-constexpr int G3_PLB = 128 * G2_BK * 2;   // one B plane of a stage: 4 KB
-__global__ __launch_bounds__(256, 2) void x3_gemm_af128_kernel(X3G g) {
-    __shared__ __attribute__((aligned(16))) char sA0[3 * G3_PLA], sA1[3 * G3_PLA];
-    __shared__ __attribute__((aligned(16))) char sB0[3 * G3_PLB], sB1[3 * G3_PLB];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
-    const int64_t nbx = (g.M + 255) / 256, nby = g.N / 128;
-    const int64_t per_batch = nbx * nby, total = per_batch * g.nbatch;
-    const int64_t L = (int64_t)blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
-    if (L >= total) return;
-    const int64_t xcd = L % 8, q8 = total / 8, r8 = total % 8;
-    const int64_t T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
-    const int64_t bz = T / per_batch, Tt = T - bz * per_batch;
-    const int64_t m0 = (Tt / nby) * 256;
-    const int64_t n0 = (Tt % nby) * 128;
-    const int nk = g.K / G2_BK;
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.af + bz * g.bsa + m0 * g.K, (uint64_t)(g.M - m0) * g.K * 4);
-    const int arow = tid >> 1, ach = tid & 1;             // rows arow and arow + 128, k chunk ach
-    const uint32_t aoff0 = ((uint32_t)arow * (uint32_t)g.K + (uint32_t)ach * 8u) * 4u;
-    const uint32_t aoff1 = aoff0 + 128u * (uint32_t)g.K * 4u;
-    const int awr0 = x3_off16(arow, ach), awr1 = x3_off16(arow + 128, ach);
-    __amdgpu_buffer_rsrc_t rb[3];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-        rb[pl] = make_rsrc(g.b + pl * g.psb + bz * g.bsb + n0 * g.K, (uint64_t)128 * g.K * 2);
-    const int lrow = 32 * wave + (lane >> 1);
-    const uint32_t lsrc = (uint32_t)lrow * (uint32_t)g.K * 2u + (uint32_t)(((lane & 1) ^ ((lrow >> 3) & 1)) << 4);
-    auto stA = [&](auto st) -> char* {
-        if constexpr (decltype(st)::v == 0) return sA0;
-        else return sA1;
-    };
-    auto stB = [&](auto st) -> char* {
-        if constexpr (decltype(st)::v == 0) return sB0;
-        else return sB1;
-    };
-    auto load_a = [&](int kt, float4 (&v)[4]) {
-        const bool in = kt < nk;
-        const uint32_t o = (uint32_t)kt * (G2_BK * 4);
-        v[0] = bload4(ra, in ? aoff0 + o : M3D_OOB);
-        v[1] = bload4(ra, in ? aoff0 + o + 16u : M3D_OOB);
-        v[2] = bload4(ra, in ? aoff1 + o : M3D_OOB);
-        v[3] = bload4(ra, in ? aoff1 + o + 16u : M3D_OOB);
-    };
-    auto dma_b = [&](auto st, int kt) {
-        char* S = stB(st) + wave * 1024;
-        const uint32_t off = kt < nk ? lsrc + (uint32_t)kt * (G2_BK * 2) : M3D_OOB;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) g2_dma(rb[pl], S + pl * G3_PLB, off);
-    };
-    auto split_a = [&](auto st, const float4 (&v)[4]) {
-        char* S = stA(st);
-        uint2 lo4[3], hi4[3];
-        split3x4(v[0], lo4);
-        split3x4(v[1], hi4);
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            *reinterpret_cast<uint4*>(S + awr0 + q * G3_PLA) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
-        split3x4(v[2], lo4);
-        split3x4(v[3], hi4);
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            *reinterpret_cast<uint4*>(S + awr1 + q * G3_PLA) = make_uint4(lo4[q].x, lo4[q].y, hi4[q].x, hi4[q].y);
-    };
-    floatx16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-    float4 xa[4], ya[4];            // A rows of the even / odd steps
-    load_a(0, xa);
-    dma_b(IC<0>{}, 0);
-    load_a(1, ya);
-    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");   // A(0)
-    split_a(IC<0>{}, xa);
-    // step kt on stage kt % 2: cur holds A(kt+1) (loaded at step kt-1), nxt
-    // receives A(kt+2) (its A(kt) was split at step kt-1)
-    auto step = [&](auto st, int kt, float4 (&cur)[4], float4 (&nxt)[4]) {
-        constexpr int s0 = decltype(st)::v;
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");   // B(kt); own A(kt) writes
-        __builtin_amdgcn_s_barrier();
-        dma_b(IC<1 - s0>{}, kt + 1);            // stage last read at step kt-1
-        load_a(kt + 2, nxt);
-        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");              // A(kt+1)
-        split_a(IC<1 - s0>{}, cur);
-        const char* SA = stA(st);
-        const char* SB = stB(st);
-        bf16x8 bfr[2][3];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int off = x3_off16(wn * 64 + j * 32 + l32, h);
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                bfr[j][pl] = *reinterpret_cast<const bf16x8*>(SB + pl * G3_PLB + off);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int off = x3_off16(wm * 128 + i * 32 + l32, h);
-            bf16x8 af[3];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) af[pl] = *reinterpret_cast<const bf16x8*>(SA + pl * G3_PLA + off);
-            x3_mac_pair<X3ACC_GEMM>(acc[i][0], acc[i][1], af[0], af[1], af[2], bfr[0][0], bfr[0][1], bfr[0][2],
-                                    bfr[1][0], bfr[1][1], bfr[1][2]);
-        }
-    };
-    for (int kt = 0;;) {
-        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
-        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
-        step(IC<0>{}, kt, ya, xa); if (++kt >= nk) break;
-        step(IC<1>{}, kt, xa, ya); if (++kt >= nk) break;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing (zero) loads
-    const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = (int)n0 + wn * 64 + j * 32 + l32;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float v = acc[i][j][r];
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
-                                                      (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u),
-                                                      0, 0);
-            }
-        }
-}
-
-// M3D_X3_AF128=1: the fp32-A point GEMMs on x3_gemm_af128_kernel (A/B)
-static int x3_af128_env() {
-    static constexpr int v = M3D_TUNE_X3_AF128;
-    return v;
-}
-
-#endif  // M3D_TUNE_X3_AF128
-
-// M3D_X3_256 (default 1): the Winograd point GEMMs with N % 256 == 0 on
-// x3_gemm256_kernel; 0 keeps x3_gemm_kernel everywhere (A/B)
-static int x3_256_env() {
-    static constexpr int v = M3D_TUNE_X3_256;
-    return v;
-}
 
 // M3D_WINO_NZ = 2 selects the F(2x2x2) tiles (A/B testing; default 4: F(2x2x4))
 static int wino_nz() {
@@ -3575,11 +3047,8 @@ static int wino_wgrad_nz() {
     static constexpr int v = M3D_TUNE_WINO_WGRAD_NZ;
     return v;
 }
-// M3D_WINO_DGRAD_NZ overrides the data-gradient tile (default: the forward's)
-static int wino_dgrad_nz() {
-    static constexpr int v = M3D_TUNE_WINO_DGRAD_NZ;   // 0: the forward's tile
-    return v ? v : wino_nz();
-}
+// the data gradient's z tile: the forward's
+static int wino_dgrad_nz() { return wino_nz(); }
 // The data gradient's y tile (round 5): F(2,3) along y by default, i.e.
 // F(2x2x4) tiles, while the forward and the weight gradient keep F(4x2x4).
 // The data gradients carry the step's gradient error (every layer's dx feeds
@@ -3605,8 +3074,7 @@ static WinoGeom wino_geom(int64_t B, int64_t H, int64_t W, int64_t D, int64_t Di
     g.halo = nullptr;
     g.hlo = g.hhi = 0;
     g.tz_mode = 0;
-    static constexpr int xcd = M3D_TUNE_WINO_XCD;
-    g.xcd = xcd;
+    g.xcd = 0;
     return g;
 }
 
@@ -3899,27 +3367,13 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
             for (int kz = 0; kz < 7; ++kz) {
                 const float a = wa[kz];
                 const float2 bv = *reinterpret_cast<const float2*>(wb + kz * 128);
-#if defined(M3D_STEM_DBG) && M3D_STEM_DBG == 2
-                acc0[kz] += a * bv.x;             // timing probe: no MFMA
-                acc1[kz] += a * bv.y;
-#else
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc1, 0, 0, 0);
-#endif
             }
             wa += STEM_WZ;
             wb += 7 * 128;
         }
         __builtin_amdgcn_wave_barrier();          // window reads done before the staging writes
-#if defined(M3D_STEM_DBG) && M3D_STEM_DBG == 1
-        {   // timing probe: no epilogue (one store per lane keeps the MFMAs live)
-            float t = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) t += acc0[r] + acc1[r];
-            if (t == 1.2345f) e.y[lane] = t;
-            continue;
-        }
-#endif
         const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
         const int oz0 = tz * STEM_TZ;
 #pragma unroll
@@ -3954,383 +3408,12 @@ __global__ __launch_bounds__(512) void stem_fwd_kernel(ConvP p, Epi e, int tz_n,
     }
 }
 
-#if M3D_TUNE_STEM_X3
-// ---- the stem forward on the exact bf16 split (A/B builds: M3D_TUNE_STEM_X3) ----
-// stem_fwd_kernel above runs the f32 MFMA (1/16 of the bf16 rate), which bounds
-// it near 1.2 ms at 256^3 even at full issue.  Here the product runs as 6
-// v_mfma_f32_32x32x16_bf16 on the 3-way split of both operands (as the
-// Winograd GEMMs; exact to the f32 rounding).  The bf16 MFMA wants 8
-// consecutive k per lane as one 16-B read, so K is ordered k = kz * 56 + R
-// (R = ky * 7 + kx padded 49 -> 56, kz padded 7 -> 8 in the last chunk: 25
-// chunks of 16) and each wave's window is stored TRANSPOSED, [z (40)][R (56)]
-// bf16 per plane: a lane (output z m, k-group g) reads window[m + kz][R0 .. R0+7]
-// with R0 = k0 % 56 a multiple of 8 -- 16-B aligned, rows 112 B apart
-// (conflict-free over 16 lanes).  A workgroup = 4 waves and one 32-channel
-// half of the output (weights [plane][n][k] in LDS, 76.8 KB); every wave owns
-// its tile (one output column x 32 z x 32 channels: ONE accumulator) and its
-// window (13.4 KB), refilled from registers prefetched during the previous
-// tile's MFMAs; lanes load (z, R-pair) values so each plane gets one b32 write
-// per pair.  Same epilogue order as epi_store4 (bias, z, frozen BN, activation).
-constexpr int SX_R = 56, SX_ZR = 40, SX_KC = 25, SX_K = SX_KC * 16;
-constexpr int SX_PL = SX_ZR * SX_R * 2;          // window plane bytes (4480)
-constexpr int SX_WPL = 32 * SX_K * 2;            // weight plane bytes (25600)
-constexpr int SX_PAIRS = 38 * 25;                // (z, R pair) values per window: R 0..49 (49 = pad)
-constexpr int SX_PER = (SX_PAIRS + 63) / 64;     // 15 per lane
-constexpr int SX_SLD = 36;                       // epilogue staging row stride (floats)
-
-__global__ __launch_bounds__(256, 1) void stem_fwd_x3_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
-    __shared__ __attribute__((aligned(16))) char wsh[3 * SX_WPL];
-    __shared__ __attribute__((aligned(16))) char win[4][3 * SX_PL];
-    __shared__ __attribute__((aligned(16))) float stg[4][32 * SX_SLD];   // epilogue staging (the window's
-                                                                        // pad cells must stay zero)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int hc = blockIdx.x & 1;                                   // output channels hc*32 .. +31
-    for (int i = tid; i < 32 * SX_K; i += 256) {
-        const int n = i / SX_K, k = i - n * SX_K;
-        const int kz = k / SX_R, R = k - kz * SX_R;
-        const float v = (kz < 7 && R < 49) ? p.w[(R * 7 + kz) * 64 + hc * 32 + n] : 0.0f;
-        uint32_t h, m, l;
-        split3(v, h, m, l);
-        unsigned short* W = reinterpret_cast<unsigned short*>(wsh);
-        W[i] = (unsigned short)h;
-        W[32 * SX_K + i] = (unsigned short)m;
-        W[64 * SX_K + i] = (unsigned short)l;
-    }
-    char* ww = win[wave];
-    for (int i = lane; i < SX_ZR * SX_R; i += 64) {                  // pad cells stay zero
-        const int zz = i / SX_R, R = i - zz * SX_R;
-        if (R >= 49 || zz >= 38)
-            for (int pl = 0; pl < 3; ++pl) reinterpret_cast<unsigned short*>(ww + pl * SX_PL)[i] = 0;
-    }
-    __syncthreads();
-    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
-    auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
-        tz = (int)(t % tz_n); t /= tz_n;
-        ox = (int)(t % p.OW); t /= p.OW;
-        oy = (int)(t % p.OH);
-        b = (int)(t / p.OH);
-    };
-    auto xval = [&](const float* xb, int b, int gy, int gx, int gz) -> float {
-        if (gy < 0 || gy >= p.H || gx < 0 || gx >= p.W || gz < 0 || gz >= p.D) return 0.0f;
-        if (p.halo) {
-            const int zl = gz - p.hnlo;
-            if ((unsigned)zl < (unsigned)p.hdl) return xb[gy * row + gx * plane + zl];
-            return p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
-                          (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
-        }
-        return xb[gy * row + gx * plane + gz];
-    };
-    auto fetch = [&](int64_t tile, float (&v)[SX_PER][2]) {
-        int b, oy, ox, tz;
-        decode(tile, b, oy, ox, tz);
-        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
-        const float* xb = p.a + b * img;
-#pragma unroll
-        for (int q = 0; q < SX_PER; ++q) {
-            const int j = lane + 64 * q;
-            v[q][0] = v[q][1] = 0.0f;
-            if (j < SX_PAIRS) {
-                const int zz = j / 25, rp = j - zz * 25;
-                const int R0 = 2 * rp, R1 = R0 + 1;
-                v[q][0] = xval(xb, b, gy0 + R0 / 7, gx0 + R0 % 7, gz0 + zz);
-                if (R1 < 49) v[q][1] = xval(xb, b, gy0 + R1 / 7, gx0 + R1 % 7, gz0 + zz);
-            }
-        }
-    };
-    auto stage = [&](const float (&v)[SX_PER][2]) {
-#pragma unroll
-        for (int q = 0; q < SX_PER; ++q) {
-            const int j = lane + 64 * q;
-            if (j < SX_PAIRS) {
-                const int zz = j / 25, rp = j - zz * 25;
-                uint32_t h0, m0, l0, h1, m1, l1;
-                split3(v[q][0], h0, m0, l0);
-                split3(v[q][1], h1, m1, l1);
-                const int off = (zz * SX_R + 2 * rp) * 2;
-                *reinterpret_cast<uint32_t*>(ww + off) = h0 | (h1 << 16);
-                *reinterpret_cast<uint32_t*>(ww + SX_PL + off) = m0 | (m1 << 16);
-                *reinterpret_cast<uint32_t*>(ww + 2 * SX_PL + off) = l0 | (l1 << 16);
-            }
-        }
-    };
-    const int g = lane >> 5, l32 = lane & 31;
-    const char* wb = wsh + (l32 * SX_K + 8 * g) * 2;                 // B: column n = l32, k = 16c + 8g
-    const char* wa = ww + l32 * (SX_R * 2);                          // A: row m = l32
-    const int n = hc * 32 + 4 * (lane & 7);
-    const float4 bb = e.bias ? ld4(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 sc = e.scale ? ld4(e.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
-    const float4 sh = e.scale ? ld4(e.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const int64_t w0 = (int64_t)(blockIdx.x >> 1) * 4 + wave, wstride = (int64_t)(gridDim.x >> 1) * 4;
-    float pre[SX_PER][2];
-    if (w0 < ntiles) fetch(w0, pre);
-    for (int64_t tile = w0; tile < ntiles; tile += wstride) {
-        stage(pre);
-        __builtin_amdgcn_wave_barrier();
-        if (tile + wstride < ntiles) fetch(tile + wstride, pre);      // next window in flight
-        floatx16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-        for (int c = 0; c < SX_KC; ++c) {
-            // k0 = 16c + 8g: kz = k0 / 56, R0 = k0 % 56 (both halves of a chunk within one kz
-            // except where 16c + 8 crosses a multiple of 56)
-            const int k0a = 16 * c, k0b = 16 * c + 8;
-            const int offa = (k0a / SX_R) * (SX_R * 2) + (k0a % SX_R) * 2;
-            const int offb = (k0b / SX_R) * (SX_R * 2) + (k0b % SX_R) * 2;
-            const int aoff = g ? offb : offa;
-            bf16x8 af[3], bw[3];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                af[pl] = *reinterpret_cast<const bf16x8*>(wa + pl * SX_PL + aoff);
-                bw[pl] = *reinterpret_cast<const bf16x8*>(wb + pl * SX_WPL + c * 32);
-            }
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bw[0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bw[1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bw[0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bw[0], acc, 0, 0, 0);
-        }
-        __builtin_amdgcn_wave_barrier();          // window reads done before the staging writes
-        int b, oy, ox, tz;
-        decode(tile, b, oy, ox, tz);
-        float* st = stg[wave];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * g) * SX_SLD + l32] = acc[r];
-        __builtin_amdgcn_wave_barrier();
-        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
-        const int oz0 = tz * STEM_TZ;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {                 // 32 rows x 8 float4 = 4 per lane
-            const int rr = (lane >> 3) + 8 * q;
-            float4 v = *reinterpret_cast<const float4*>(st + rr * SX_SLD + 4 * (lane & 7));
-            if (oz0 + rr >= p.OD) continue;
-            const int64_t m = mbase + oz0 + rr;
-            if (e.bias) { v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w; }
-            if (e.z) st4(e.z + m * 64 + n, v);
-            if (e.scale) {
-                v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
-                v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
-            }
-            if (e.relu) {
-                v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
-            }
-            st4(e.y + m * 64 + n, v);
-        }
-        __builtin_amdgcn_wave_barrier();          // staging reads done before the next window
-    }
-}
-
-// ---- stem forward, bf16 split, weights in registers (M3D_STEM_X3=2) ---------
-// The 32x32 form above keeps 77 KB of weights in LDS, so one workgroup (one
-// wave per SIMD) fits a CU and every LDS latency is exposed.  Here each wave
-// owns 16 output channels (a quarter) and keeps its B operand -- the split
-// weights of those channels for all of K -- in registers (13 chunks of 32 k x
-// 3 planes x 4 VGPRs), loaded once; the four waves of a workgroup share one
-// window per tile (double-buffered, built by all 256 threads) and run
-// v_mfma_f32_16x16x32_bf16 on the tile's two 16-row halves.  K = kz * 56 + R
-// as above, padded to 416 (kz = 7 rows read with zero weights).  Outputs are
-// staged per workgroup as [32 z][64 ch] and leave as 256-B rows.
-constexpr int SY_KC = 13;                         // 32-k chunks (416 = 7.43 x 56)
-constexpr int SY_PER = (SX_PAIRS + 255) / 256;    // window pairs per thread (4)
-constexpr int SY_SLD = 68;                        // staging row stride (floats)
-typedef float floatx4_t __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256, 2) void stem_fwd_x3b_kernel(ConvP p, Epi e, int tz_n, int64_t ntiles) {
-    __shared__ __attribute__((aligned(16))) char win[2][3 * SX_PL];
-    __shared__ __attribute__((aligned(16))) float stg[32 * SY_SLD];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, l16 = lane & 15;
-    // B: this wave's 16 channels (n = 16 wave + l16), k = 32 c + 8 g + j
-    bf16x8 bw[SY_KC][3];
-#pragma unroll
-    for (int c = 0; c < SY_KC; ++c) {
-        const int k0 = 32 * c + 8 * g, kz = k0 / SX_R, R0 = k0 - kz * SX_R;
-        uint32_t hp[4] = {0, 0, 0, 0}, mp[4] = {0, 0, 0, 0}, lp[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int R = R0 + j;
-            const float v = (kz < 7 && R < 49) ? p.w[(R * 7 + kz) * 64 + 16 * wave + l16] : 0.0f;
-            uint32_t h, m, l;
-            split3(v, h, m, l);
-            hp[j >> 1] |= h << (16 * (j & 1));
-            mp[j >> 1] |= m << (16 * (j & 1));
-            lp[j >> 1] |= l << (16 * (j & 1));
-        }
-        bw[c][0] = __builtin_bit_cast(bf16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
-        bw[c][1] = __builtin_bit_cast(bf16x8, make_uint4(mp[0], mp[1], mp[2], mp[3]));
-        bw[c][2] = __builtin_bit_cast(bf16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
-    }
-    for (int i = tid; i < 2 * SX_ZR * SX_R; i += 256) {          // pad cells stay zero
-        const int bf = i / (SX_ZR * SX_R), c = i - bf * SX_ZR * SX_R;
-        const int zz = c / SX_R, R = c - zz * SX_R;
-        if (R >= 49 || zz >= 38)
-            for (int pl = 0; pl < 3; ++pl) reinterpret_cast<unsigned short*>(win[bf] + pl * SX_PL)[c] = 0;
-    }
-    // A offset of this lane in chunk c: row l16 (+16 for the second half), k0 = 32 c + 8 g;
-    // computed in the loop from compile-time constants (no per-chunk registers)
-    const int arow = l16 * (SX_R * 2);
-    auto aoff = [&](int c) -> int {
-        auto o = [](int k0) { return (k0 / SX_R) * (SX_R * 2) + (k0 % SX_R) * 2; };
-        const int o0 = o(32 * c), o1 = o(32 * c + 8), o2 = o(32 * c + 16), o3 = o(32 * c + 24);
-        return arow + (g == 0 ? o0 : g == 1 ? o1 : g == 2 ? o2 : o3);
-    };
-    const size_t plane = (size_t)(p.halo ? p.hdl : p.D), row = (size_t)p.W * plane, img = (size_t)p.H * row;
-    auto decode = [&](int64_t t, int& b, int& oy, int& ox, int& tz) {
-        tz = (int)(t % tz_n); t /= tz_n;
-        ox = (int)(t % p.OW); t /= p.OW;
-        oy = (int)(t % p.OH);
-        b = (int)(t / p.OH);
-    };
-    auto xval = [&](const float* xb, int b, int gy, int gx, int gz) -> float {
-        if (gy < 0 || gy >= p.H || gx < 0 || gx >= p.W || gz < 0 || gz >= p.D) return 0.0f;
-        if (p.halo) {
-            const int zl = gz - p.hnlo;
-            if ((unsigned)zl < (unsigned)p.hdl) return xb[gy * row + gx * plane + zl];
-            return p.halo[(((size_t)b * p.H + gy) * p.W + gx) * (2 * p.hr) +
-                          (zl < 0 ? zl + p.hr : p.hr + zl - p.hdl)];
-        }
-        return xb[gy * row + gx * plane + gz];
-    };
-    // fast path of tiles whose window lies inside the slab: offsets from the
-    // window origin, no per-value bounds / halo checks
-    auto fetch = [&](int64_t tile, float (&v)[SY_PER][2]) {
-        int b, oy, ox, tz;
-        decode(tile, b, oy, ox, tz);
-        const int gy0 = 2 * oy - p.py, gx0 = 2 * ox - p.px, gz0 = tz * STEM_TZ - p.pz;
-        const float* xb = p.a + b * img;
-        const int zl0 = p.halo ? gz0 - p.hnlo : gz0, zlim = p.halo ? p.hdl : p.D;
-        if (gy0 >= 0 && gy0 + 6 < p.H && gx0 >= 0 && gx0 + 6 < p.W && zl0 >= 0 && zl0 + 37 < zlim) {
-            const float* base = xb + gy0 * row + gx0 * plane + zl0;
-#pragma unroll
-            for (int q = 0; q < SY_PER; ++q) {
-                const int j = tid + 256 * q;
-                const int zz = j / 25, rp = j - zz * 25, R0 = 2 * rp, dy = R0 / 7, dx = R0 - 7 * dy;
-                const float* a0 = base + (dy * (int)row + dx * (int)plane + zz);
-                // R0 + 1: the next kx, or the next ky row when dx == 6 (R 49 is padding)
-                const float* a1 = dx < 6 ? a0 + plane : a0 + (row - 6 * plane);
-                v[q][0] = j < SX_PAIRS ? a0[0] : 0.0f;
-                v[q][1] = (j < SX_PAIRS && R0 + 1 < 49) ? a1[0] : 0.0f;
-            }
-            return;
-        }
-#pragma unroll
-        for (int q = 0; q < SY_PER; ++q) {
-            const int j = tid + 256 * q;
-            v[q][0] = v[q][1] = 0.0f;
-            if (j < SX_PAIRS) {
-                const int zz = j / 25, rp = j - zz * 25;
-                const int R0 = 2 * rp, R1 = R0 + 1;
-                v[q][0] = xval(xb, b, gy0 + R0 / 7, gx0 + R0 % 7, gz0 + zz);
-                if (R1 < 49) v[q][1] = xval(xb, b, gy0 + R1 / 7, gx0 + R1 % 7, gz0 + zz);
-            }
-        }
-    };
-    auto stage = [&](char* ww, const float (&v)[SY_PER][2]) {
-#pragma unroll
-        for (int q = 0; q < SY_PER; ++q) {
-            const int j = tid + 256 * q;
-            if (j < SX_PAIRS) {
-                const int zz = j / 25, rp = j - zz * 25;
-                uint32_t h0, m0, l0, h1, m1, l1;
-                split3(v[q][0], h0, m0, l0);
-                split3(v[q][1], h1, m1, l1);
-                const int off = (zz * SX_R + 2 * rp) * 2;
-                *reinterpret_cast<uint32_t*>(ww + off) = h0 | (h1 << 16);
-                *reinterpret_cast<uint32_t*>(ww + SX_PL + off) = m0 | (m1 << 16);
-                *reinterpret_cast<uint32_t*>(ww + 2 * SX_PL + off) = l0 | (l1 << 16);
-            }
-        }
-    };
-    const int n4 = 4 * (tid & 15);                                   // epilogue: 16 float4 per row
-    float pre[SY_PER][2];
-    int64_t tile = blockIdx.x;
-    if (tile < ntiles) fetch(tile, pre);
-    int buf = 0;
-    if (tile < ntiles) stage(win[0], pre);
-    __syncthreads();
-    for (; tile < ntiles; tile += gridDim.x) {
-        const int64_t next = tile + gridDim.x;
-#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 3
-        (void)next;                                                  // timing probe: no window fetch
-#else
-        if (next < ntiles) fetch(next, pre);                         // next window in flight
-#endif
-        const char* W = win[buf];
-        floatx4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 1
-        acc0[0] = (float)W[aoff(0)];                                 // timing probe: no MFMA
-#else
-#pragma unroll
-        for (int c = 0; c < SY_KC; ++c) {
-            bf16x8 a0[3], a1[3];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                a0[pl] = *reinterpret_cast<const bf16x8*>(W + pl * SX_PL + aoff(c));
-                a1[pl] = *reinterpret_cast<const bf16x8*>(W + pl * SX_PL + aoff(c) + 16 * SX_R * 2);
-            }
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[2], bw[c][0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[2], bw[c][0], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[1], bw[c][1], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[1], bw[c][1], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][2], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][2], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[1], bw[c][0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[1], bw[c][0], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][1], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][1], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[0], bw[c][0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0], bw[c][0], acc1, 0, 0, 0);
-        }
-#endif
-        // D of 16x16x32: row 4 g + r, column l16
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            stg[(4 * g + r) * SY_SLD + 16 * wave + l16] = acc0[r];
-            stg[(16 + 4 * g + r) * SY_SLD + 16 * wave + l16] = acc1[r];
-        }
-        if (next < ntiles) stage(win[buf ^ 1], pre);
-        __syncthreads();                                             // staging + next window written
-        int b, oy, ox, tz;
-        decode(tile, b, oy, ox, tz);
-        const int64_t mbase = (((int64_t)b * p.OH + oy) * p.OW + ox) * p.OD;
-        const int oz0 = tz * STEM_TZ;
-        const float4 bb = e.bias ? ld4(e.bias + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 sc = e.scale ? ld4(e.scale + n4) : make_float4(1.f, 1.f, 1.f, 1.f);
-        const float4 sh = e.scale ? ld4(e.shift + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {                                // 32 rows x 16 float4
-            const int rr = (tid >> 4) + 16 * q;
-            float4 v = *reinterpret_cast<const float4*>(stg + rr * SY_SLD + n4);
-            if (oz0 + rr >= p.OD) continue;
-            const int64_t m = mbase + oz0 + rr;
-            if (e.bias) { v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w; }
-#if defined(M3D_STEMX_DBG) && M3D_STEMX_DBG == 2
-            if (v.x == 1.2345f) st4(e.y + m * 64 + n4, v);           // timing probe: no stores
-            continue;
-#endif
-            if (e.z) st4(e.z + m * 64 + n4, v);
-            if (e.scale) {
-                v.x = v.x * sc.x + sh.x; v.y = v.y * sc.y + sh.y;
-                v.z = v.z * sc.z + sh.z; v.w = v.w * sc.w + sh.w;
-            }
-            if (e.relu) {
-                v.x = act(e.relu, v.x); v.y = act(e.relu, v.y); v.z = act(e.relu, v.z); v.w = act(e.relu, v.w);
-            }
-            st4(e.y + m * 64 + n4, v);
-        }
-        __syncthreads();                                             // staging read before the next tile's writes
-        buf ^= 1;
-    }
-}
-#endif  // M3D_TUNE_STEM_X3
 
 static bool stem_ok(int64_t Cin, int kh, int kw, int kd, int64_t Cout, int sy, int sx, int sz, int dly, int dlx,
                     int dlz, int res_mode, int64_t split_n, int64_t ldy) {
-    static constexpr int env = M3D_TUNE_STEM_MFMA;
     // the kernel's own epilogue covers bias / z / frozen BN / activation, plain
     // [M, 64] stores (no residual, split or accumulate)
-    return env && Cin == 1 && kh == 7 && kw == 7 && kd == 7 && Cout == 64 && sy == 2 && sx == 2 && sz == 1 &&
+    return Cin == 1 && kh == 7 && kw == 7 && kd == 7 && Cout == 64 && sy == 2 && sx == 2 && sz == 1 &&
            dly == 1 && dlx == 1 && dlz == 1 && res_mode == 0 && split_n <= 0 && (ldy <= 0 || ldy == 64);
 }
 
@@ -4446,10 +3529,6 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(ConvP p, const float* _
         }
 }
 
-static bool stem_wgrad_env() {
-    static constexpr int v = M3D_TUNE_STEM_WGRAD;
-    return v != 0;
-}
 
 static int launch_stem_wgrad(const ConvP& p, const float* dz, float* dw, hipStream_t s) {
     const int ncu = num_cus();
@@ -4476,21 +3555,6 @@ static int launch_stem(const ConvP& p, const Epi& e, hipStream_t s) {
     // vs 0.28 ms alone at 128^3); with 4 per CU the others absorb its share
     // M3D_STEM_X3=1 / 2: the bf16-split forms (measured slower than the f32 kernel: 2.65 / 2.24-2.5 vs
     // 2.2 ms at 256^3, DESIGN.md round-3 list); default the f32 MFMA kernel
-#if M3D_TUNE_STEM_X3
-    static constexpr int x3 = M3D_TUNE_STEM_X3;
-    if constexpr (x3 == 2) {
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, 2 * (int64_t)ncu));
-        hipLaunchKernelGGL(stem_fwd_x3b_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
-        return check_launch("stem_fwd_x3b_kernel");
-    }
-    if constexpr (x3 == 1) {
-        // one workgroup per CU (131 KB of LDS): pairs of workgroups take the two
-        // 32-channel halves of the same tiles, each wave its own tiles
-        const unsigned grid = (unsigned)(2 * std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, ncu / 2)));
-        hipLaunchKernelGGL(stem_fwd_x3_kernel, dim3(grid), dim3(256), 0, s, p, e, tz_n, ntiles);
-        return check_launch("stem_fwd_x3_kernel");
-    }
-#endif
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 7) / 8, 4 * (int64_t)ncu));
     hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, s, p, e, tz_n, ntiles);
     return check_launch("stem_fwd_kernel");
@@ -4878,7 +3942,7 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
     const bool vec = (Cin % 4) == 0;
-    if (stem_wgrad_env() && stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
+    if (stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
         return launch_stem_wgrad(p, dz, dw, st(s));
     // 1x1x1 stride-1 convs: im2col is x itself, the plain weight-gradient GEMM
     // dW += x^T dz -- on the exact bf16 split like the Winograd ones
@@ -4889,7 +3953,7 @@ extern "C" int m3d_conv3d_bwd_weight(const float* x, const float* dz, int64_t B,
         launch_wgrad_x3(x, dz, dw, p.M, (int)Cin, (int)Cout, 1, 0, 0, 0, st(s));
         return check_launch("x3_wgrad_kernel (1x1x1)");
     }
-    if (vec && p.K <= 64 && wgrad_k64_env()) {        // e.g. the 64 -> 256 1x1 convs of stage 2
+    if (vec && p.K <= 64) {        // e.g. the 64 -> 256 1x1 convs of stage 2
         if (Cout <= 64) launch_wgrad<64, 64, 2, 2, true>(p, dz, dw, st(s));
         else launch_wgrad<64, 128, 2, 2, true>(p, dz, dw, st(s));
     } else if (Cout <= 64) {
@@ -4962,7 +4026,7 @@ extern "C" int m3d_conv3d_bwd_weight_halo(const float* x, const float* halo, int
             sy, sx, sz, py, px, pz, B * OH * OW * OD, (int)(kh * kw * kd * Cin), nullptr,
             (int)Cout, 0, 0, 0, 0};
     if ((rc = conv_halo_geom(p, halo, has_lo, has_hi, r, Dl, kd, sz, pz, OD))) return rc;
-    if (stem_wgrad_env() && stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
+    if (stem_ok(Cin, kh, kw, kd, Cout, sy, sx, sz, 1, 1, 1, 0, 0, 0))
         return launch_stem_wgrad(p, dz, dw, st(s));
     const bool vec = (Cin % 4) == 0;
     if (Cout <= 64) {
@@ -5091,20 +4155,6 @@ static WinoWs wino_ws(void* ws, const WinoGeom& g, int64_t Cin, int64_t Cout, in
         }                                                                                                  \
     } while (0)
 
-// M3D_X3_BK (16 | 32) and M3D_X3_PERSIST (0 | 1): x3_gemm_kernel variant (A/B)
-static int x3_bk_env() {
-    static constexpr int v = M3D_TUNE_X3_BK;
-    return v;
-}
-static int x3_occ3_env() {
-    static constexpr int v = M3D_TUNE_X3_OCC3;
-    return v;
-}
-static int x3_persist_env() {
-    static constexpr int v = M3D_TUNE_X3_PERSIST;
-    return v;
-}
-
 static int x3_af32_env() { return (x3_mask() >> 4) & 1; }
 
 // the P point GEMMs M[xi] = U[xi] V[xi] on split planes (U: T x K, V: N x K);
@@ -5119,56 +4169,19 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
     q.M = T; q.K = K; q.N = N; q.nbatch = P;
     q.psa = (int64_t)P * T * K; q.psb = (int64_t)P * K * N;
     q.bsa = T * K; q.bsb = (int64_t)K * N; q.bsc = T * N;
-#if M3D_TUNE_X3_AF128
-    if (M3D_TUNE_X3_AF128 && af32 && x3_256_env() && N % 128 == 0 && T >= 256) {
-        const int64_t t128 = ((T + 255) / 256) * (N / 128) * P;
-        const dim3 grid((unsigned)(t128 < 65536 ? t128 : 65536), (unsigned)((t128 + 65535) / 65536));
-        hipLaunchKernelGGL(x3_gemm_af128_kernel, grid, dim3(256), 0, s, q);
-        return;
-    }
-#endif
-    // M3D_TUNE_X3_256_MIN_TILES: fewest 256x256 tiles (all batches) for the
-    // 256-kernel; below it the 128x128 x3_gemm_kernel fills the chip better
-    const int64_t t256n = ((T + 255) / 256) * (N / 256) * P;
-    if (af32 && x3_256_env() && N % 256 == 0 && T >= 256 && t256n >= M3D_TUNE_X3_256_MIN_TILES) {
+    // the 256x256 kernels where N fills whole 256-column tiles (x3_gemm256_kernel:
+    // 1.345 vs 1.368 ms on the priced launch against the 128x128 kernel)
+    if (N % 256 == 0 && T >= 256) {
         const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
         const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
-        hipLaunchKernelGGL(x3_gemm256_af_kernel<0>, grid, dim3(512), 0, s, q);
+        if (af32) hipLaunchKernelGGL(x3_gemm256_af_kernel<0>, grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
         return;
     }
-    if (!af32 && x3_256_env() && N % 256 == 0 && T >= 256) {
-        const int64_t t256 = ((T + 255) / 256) * (N / 256) * P;
-        const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
-        static constexpr int dbg = M3D_TUNE_X3_256_DBG;
-        if constexpr (dbg == 0) {
-            hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
-        } else switch (dbg) {
-            case 1: hipLaunchKernelGGL(x3_gemm256_kernel<1>, grid, dim3(512), 0, s, q); break;
-            case 2: hipLaunchKernelGGL(x3_gemm256_kernel<2>, grid, dim3(512), 0, s, q); break;
-            case 3: hipLaunchKernelGGL(x3_gemm256_kernel<3>, grid, dim3(512), 0, s, q); break;
-            case 4: hipLaunchKernelGGL(x3_gemm256_kernel<4>, grid, dim3(512), 0, s, q); break;
-            default: hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
-        }
-        return;
-    }
+    // 128x128 tiles, BK 32, 3 blocks per CU (2 with A in fp32)
     const int64_t tiles = ((T + 127) / 128) * ((N + 127) / 128) * P;
-    const bool bk16 = x3_bk_env() == 16;
-    const bool occ3 = !bk16 && x3_occ3_env() && !X3ACC_GEMM;   // (fresh accumulators: no room at 3/CU)
-    const int64_t resident = (int64_t)num_cus() * (bk16 || occ3 ? 3 : 2);
-    const bool persist = x3_persist_env() && tiles > 2 * resident;
-    const dim3 grid(persist ? (unsigned)(resident / 8 * 8) : (unsigned)tiles);
-    if (af32) {
-        hipLaunchKernelGGL((x3_gemm_kernel<32, false, 2, true>), dim3((unsigned)tiles), dim3(256), 0, s, q);
-    } else if (bk16) {
-        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<16, true>), grid, dim3(256), 0, s, q);
-        else hipLaunchKernelGGL((x3_gemm_kernel<16, false>), grid, dim3(256), 0, s, q);
-    } else if (occ3) {
-        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<32, true, 3>), grid, dim3(256), 0, s, q);
-        else hipLaunchKernelGGL((x3_gemm_kernel<32, false, 3>), grid, dim3(256), 0, s, q);
-    } else {
-        if (persist) hipLaunchKernelGGL((x3_gemm_kernel<32, true>), grid, dim3(256), 0, s, q);
-        else hipLaunchKernelGGL((x3_gemm_kernel<32, false>), grid, dim3(256), 0, s, q);
-    }
+    if (af32) hipLaunchKernelGGL((x3_gemm_kernel<32, false, 2, true>), dim3((unsigned)tiles), dim3(256), 0, s, q);
+    else hipLaunchKernelGGL((x3_gemm_kernel<32, false, 3>), dim3((unsigned)tiles), dim3(256), 0, s, q);
 }
 
 // x -> three bf16 planes of split3 (planes at x3 + p * n), one element per thread
@@ -5309,7 +4322,7 @@ static int conv1_x3_launch(const float* a, const uint16_t* planes, int64_t M, in
     const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
     // the epilogue in the GEMM's own stores when it is element-local (same-shape
     // residual); the FPN's upsampled residual (res_mode 2) takes the second pass
-    const bool fuse = M3D_TUNE_CONV1_EPI && e && e->res_mode <= 1 && !e->accumulate && e->split <= 0 &&
+    const bool fuse = e && e->res_mode <= 1 && !e->accumulate && e->split <= 0 &&
                       e->ldy == N && e->simple;
     if (fuse) {
         q.ep.bias = e->bias; q.ep.scale = e->scale; q.ep.shift = e->shift;
@@ -5706,13 +4719,6 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
     else
         WINO_INPUT(nz, false, dim3(grid_for(g.T * Cin, 256)), st(s), x, g, (int)Cin, ws.U);
     // M3D_WINO_GRAD4=1: the float4 form (measured slower: 278 vs 253 us avg, write-bound)
-#if M3D_TUNE_WINO_GRAD4
-    static constexpr int grad4 = M3D_TUNE_WINO_GRAD4;
-    if (grad4 && Cout % 4 == 0)
-        WINO_LAUNCH_NZ(nz, wino_grad4_kernel, dim3(grid_for(g.T * (Cout / 4), 256)), dim3(256), 0, st(s), dz, g,
-                       (int)Cout, ws.M);
-    else
-#endif
         WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
     if (wgrad_x3_env() && Cout > 64) {

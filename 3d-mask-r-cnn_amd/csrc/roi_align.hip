@@ -411,314 +411,8 @@ __global__ __launch_bounds__(256) void line_fwd_sl_kernel(LineArgs a, Pyr P, con
     }
 }
 
-#if M3D_TUNE_ROI_ROW
-// ---- PyramidROIAlign forward, separable row form ----------------------------------
-// One workgroup per output row (n, y) over all C = 256 channels.  tri() lerps z
-// first (per corner column), then x, then y, so the z-lerped value of a (source
-// row, x column) at sample z is shared by every output x whose corners use that
-// column: per z sample the workgroup loads the rows ty / by of each distinct x
-// column once (the line kernel loads 8 corner rows per output), z-lerps them
-// into LDS, and every (x, channel quad) finishes the x- and y-lerps from LDS
-// with tri()'s operations (bit-identical).  The distinct columns are the union
-// of the samples' floor / ceil indices (<= 2 cw slots).  The next sample's
-// corner rows are loaded while the current one's outputs are written (one
-// register stage); a floor plane equal to the previous ceil plane is reused.
-// tri()'s x- then y-lerp of the four z-lerped corners (same operations), scrubbed
-__device__ __forceinline__ float row_xy(float tl, float tr, float bl, float br, float xl, float yl) {
-    const float top = tl + (tr - tl) * xl;
-    const float bot = bl + (br - bl) * xl;
-    return scrub(top + (bot - top) * yl);
-}
 
-// sample z's planes (fz = -1: outside the map, extrapolate)
-__device__ __forceinline__ void row_zplanes(float z1, float z2, int D, int cd, int z, float zsc, int& fz, int& kz,
-                                            float& zl) {
-    const float in_z = axis_coord(z1, z2, D, cd, z, zsc);
-    if (in_z < 0 || in_z > (float)(D - 1)) { fz = -1; kz = -1; zl = 0.0f; return; }
-    fz = (int)floorf(in_z); kz = (int)ceilf(in_z); zl = in_z - (float)fz;
-}
 
-template <int CW_MAX, int NT, int CG>
-__global__ __launch_bounds__(NT) void row_fwd_kernel(LineArgs a, Pyr P) {
-    constexpr int XS = 2 * CW_MAX;
-    constexpr int C4 = 64 / CG;                           // channel quads of this group (C = 256)
-    constexpr int IPT = (2 * XS * C4 + NT - 1) / NT;        // (row, slot, quad) items per thread
-    __shared__ float4 T[2 * XS][C4];
-    __shared__ int s_l[CW_MAX], s_r[CW_MAX], s_oob[CW_MAX], s_col[XS], s_ns;
-    __shared__ float s_xl[CW_MAX];
-    const int tid = threadIdx.x;
-    const int64_t rb = xcd_block();                       // (row, channel group), groups adjacent
-    const int64_t row = rb / CG;
-    const int cg = (int)(rb - row * CG);
-    if (row >= a.lines) return;                           // (block-uniform)
-    const int y = (int)(row % a.ch);
-    const int64_t n = row / a.ch;
-    const int l = a.levels[n] - 2;
-    const int H = P.H[l], W = P.W[l], D = P.D[l];
-    const float4* img = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)(n / a.N) * H * W * D * a.C) + cg * C4;
-    const float* box = a.boxes + n * 6;
-    const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
-    const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
-    const float zsc = axis_scale(z1, z2, D, a.cd);
-    float4* o = reinterpret_cast<float4*>(a.out) + (row * a.cw) * (int64_t)a.cd * 64 + cg * C4;
-    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
-    if (in_y < 0 || in_y > (float)(H - 1)) {
-        for (int i = tid; i < a.cw * a.cd * C4; i += NT) st_nt(o + (int64_t)(i / C4) * 64 + i % C4, ex);
-        return;
-    }
-    const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
-    const float yl = in_y - (float)ty;
-    if (tid < a.cw) {
-        const float in_x = axis_coord(x1, x2, W, a.cw, tid, axis_scale(x1, x2, W, a.cw));
-        const bool oob = in_x < 0 || in_x > (float)(W - 1);
-        s_oob[tid] = oob;
-        s_l[tid] = oob ? 0 : (int)floorf(in_x);
-        s_r[tid] = oob ? 0 : (int)ceilf(in_x);
-        s_xl[tid] = oob ? 0.0f : in_x - floorf(in_x);
-    }
-    __syncthreads();
-    if (tid == 0) {                                       // sorted distinct columns
-        int ns = 0;
-        for (int j = 0; j < a.cw; ++j) {
-            if (s_oob[j]) continue;
-            for (int side = 0; side < 2; ++side) {
-                const int v = side ? s_r[j] : s_l[j];
-                int k = 0;
-                while (k < ns && s_col[k] < v) ++k;
-                if (k < ns && s_col[k] == v) continue;
-                for (int m = ns; m > k; --m) s_col[m] = s_col[m - 1];
-                s_col[k] = v;
-                ++ns;
-            }
-        }
-        s_ns = ns;
-    }
-    __syncthreads();
-    const int ns = s_ns;
-    int my_sl = 0, my_sr = 0;
-    if (tid < a.cw && !s_oob[tid]) {
-        for (int k = 0; k < ns; ++k) {
-            if (s_col[k] == s_l[tid]) my_sl = k;
-            if (s_col[k] == s_r[tid]) my_sr = k;
-        }
-    }
-    const int nr = ty == by ? 1 : 2;
-    const int bot = (nr - 1) * ns;                        // T row offset of the bottom source row
-    const size_t rowD = (size_t)D * 64, rowW = (size_t)W * rowD;
-    // this thread's items: T row j = r * ns + slot, channel quad q (fixed over z)
-    const float4* cp[IPT];
-    int tj[IPT];
-#pragma unroll
-    for (int u = 0; u < IPT; ++u) {
-        const int i = tid + NT * u;
-        const int j = i / C4, q = i & (C4 - 1);
-        const int r = j >= ns ? 1 : 0;
-        tj[u] = j < nr * ns ? j : -1;
-        cp[u] = img + (r ? by : ty) * rowW + s_col[tj[u] < 0 ? 0 : j - r * ns] * rowD + q;
-    }
-    __syncthreads();
-    if (tid < a.cw) { s_l[tid] = my_sl; s_r[tid] = my_sr; }
-    // loads of the first in-range sample (z planes uniform: row_zplanes)
-    float4 f[IPT], k[IPT];
-    int fz, kz, pk = -1;
-    float zl;
-    row_zplanes(z1, z2, D, a.cd, 0, zsc, fz, kz, zl);
-    if (fz >= 0) {
-#pragma unroll
-        for (int u = 0; u < IPT; ++u) {
-            if (tj[u] >= 0) {
-                f[u] = cp[u][(size_t)fz * 64];
-                k[u] = cp[u][(size_t)kz * 64];            // (kz == fz: the same row)
-            }
-        }
-        pk = kz;
-    }
-    for (int z = 0; z < a.cd; ++z) {
-        const bool in = fz >= 0;
-        if (in) {
-#pragma unroll
-            for (int u = 0; u < IPT; ++u) {
-                if (tj[u] >= 0) {
-                    float4 t;
-                    t.x = f[u].x + (k[u].x - f[u].x) * zl;
-                    t.y = f[u].y + (k[u].y - f[u].y) * zl;
-                    t.z = f[u].z + (k[u].z - f[u].z) * zl;
-                    t.w = f[u].w + (k[u].w - f[u].w) * zl;
-                    T[tj[u]][tid & (C4 - 1)] = t;
-                }
-            }
-        }
-        // the next sample's corner rows in flight across the barrier and the stores
-        if (z + 1 < a.cd) {
-            row_zplanes(z1, z2, D, a.cd, z + 1, zsc, fz, kz, zl);
-            if (fz >= 0) {
-                // uniform branches, no per-item selects: a select between a register
-                // array element and a load becomes a select of addresses, and the
-                // array is then kept in scratch
-                if (fz == pk) {
-#pragma unroll
-                    for (int u = 0; u < IPT; ++u)
-                        if (tj[u] >= 0) f[u] = k[u];
-                } else {
-#pragma unroll
-                    for (int u = 0; u < IPT; ++u)
-                        if (tj[u] >= 0) f[u] = cp[u][(size_t)fz * 64];
-                }
-                if (kz != fz) {
-#pragma unroll
-                    for (int u = 0; u < IPT; ++u)
-                        if (tj[u] >= 0) k[u] = cp[u][(size_t)kz * 64];
-                } else {
-#pragma unroll
-                    for (int u = 0; u < IPT; ++u)
-                        if (tj[u] >= 0) k[u] = f[u];
-                }
-                pk = kz;
-            }
-        }
-        __syncthreads();
-        for (int i = tid; i < a.cw * C4; i += NT) {
-            const int x = i / C4, q = i & (C4 - 1);
-            float4 res = ex;
-            if (in && !s_oob[x]) {
-                const int a0 = s_l[x], a1 = s_r[x];
-                const float xl = s_xl[x];
-                const float4 tl = T[a0][q], tr = T[a1][q];
-                const float4 bl = T[bot + a0][q], br = T[bot + a1][q];
-                res = make_float4(row_xy(tl.x, tr.x, bl.x, br.x, xl, yl), row_xy(tl.y, tr.y, bl.y, br.y, xl, yl),
-                                  row_xy(tl.z, tr.z, bl.z, br.z, xl, yl), row_xy(tl.w, tr.w, bl.w, br.w, xl, yl));
-            }
-            st_nt(o + ((int64_t)x * a.cd + z) * 64 + q, res);
-        }
-        __syncthreads();                                  // T read before the next sample writes it
-    }
-}
-
-#endif  // M3D_TUNE_ROI_ROW
-
-#if M3D_TUNE_ROI_PC
-// Producer / consumer form of line_fwd_sl_kernel<8> (M3D_ROI_PC=1): a
-// workgroup of 8 waves -- waves 0-3 gather and interpolate (loads only), waves
-// 4-7 store what their partner produced one z step earlier (stores only),
-// handing each z sample over through a double-buffered LDS slot with one
-// workgroup barrier per step.  Loads and stores then sit on different waves'
-// vmcnt counters: the gather never waits behind an output store.  Every wave
-// runs the same cd + 1 steps (uniform barriers; inactive waves / lanes idle).
-__global__ __launch_bounds__(512) void line_fwd_pc_kernel(LineArgs a, Pyr P, const int32_t* __restrict__ wperm) {
-    constexpr int SL = 8, LPL = 64 / SL;
-    __shared__ float4 slot[2][4][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const bool producer = wave < 4;
-    const int pw = wave & 3;
-    const int64_t items = a.lines;
-    const int64_t waves_per_slice = (items + SL - 1) / SL;
-    const int64_t bs8 = ((waves_per_slice + 3) / 4 + 7) / 8 * 8;
-    const int slice = (int)(blockIdx.x / bs8);
-    const int64_t lr = blockIdx.x - (int64_t)slice * bs8;
-    int64_t wv = ((lr % 8) * (bs8 / 8) + lr / 8) * 4 + pw;
-    bool active = slice < SL && wv < waves_per_slice;
-    if (active && wperm) wv = wperm[wv];
-    const int64_t line = wv * SL + lane / LPL;
-    active = active && line < items;
-    const int c = slice * LPL + (lane % LPL);
-    const int C4 = a.C >> 2;
-    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
-    // geometry of this lane's line (producers only read it; consumers need o)
-    float4* o = nullptr;
-    const float4* col[4] = {nullptr, nullptr, nullptr, nullptr};
-    float z1 = 0.f, z2 = 0.f, zsc = 0.f, yl = 0.f, xl = 0.f;
-    int D = 1;
-    bool yx_oob = true;
-    if (active) {
-        int64_t t = line;
-        const int x = (int)(t % a.cw); t /= a.cw;
-        const int y = (int)(t % a.ch);
-        const int64_t n = t / a.ch;
-        const int l = a.levels[n] - 2;
-        const int H = P.H[l], W = P.W[l];
-        D = P.D[l];
-        const float* box = a.boxes + n * 6;
-        const float y1 = box[0], x1 = box[1], y2 = box[3], x2 = box[4];
-        z1 = box[2]; z2 = box[5];
-        const float in_y = axis_coord(y1, y2, H, a.ch, y, axis_scale(y1, y2, H, a.ch));
-        const float in_x = axis_coord(x1, x2, W, a.cw, x, axis_scale(x1, x2, W, a.cw));
-        zsc = axis_scale(z1, z2, D, a.cd);
-        o = reinterpret_cast<float4*>(a.out + line * (int64_t)a.cd * a.C);
-        yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
-        if (!yx_oob) {
-            const int ty = (int)floorf(in_y), by = (int)ceilf(in_y);
-            const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
-            yl = in_y - (float)ty; xl = in_x - (float)lx;
-            const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
-            const float4* base = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)(n / a.N) * P.H[l] * W * D * a.C);
-            col[0] = base + ty * rowW + lx * rowD; col[1] = base + ty * rowW + rx * rowD;
-            col[2] = base + by * rowW + lx * rowD; col[3] = base + by * rowW + rx * rowD;
-        }
-    }
-    int pk = -1;
-    float4 kv[4];
-    for (int step = 0; step <= a.cd; ++step) {
-        if (producer && step < a.cd && active) {
-            const int z = step;
-            float4 r = ex;
-            const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
-            if (!yx_oob && !(in_z < 0 || in_z > (float)(D - 1))) {
-                const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
-                const float zl = in_z - (float)fz;
-                float4 fv[4];
-                if (fz == pk) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) fv[q] = kv[q];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
-                }
-                if (kz != fz) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) kv[q] = fv[q];
-                }
-                pk = kz;
-                r = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
-                r.x = scrub(r.x); r.y = scrub(r.y); r.z = scrub(r.z); r.w = scrub(r.w);
-            }
-            slot[step & 1][pw][lane] = r;
-        }
-        if (!producer && step >= 1 && active) {
-            const int z = step - 1;
-            st_nt(o + (int64_t)z * C4 + c, slot[(step - 1) & 1][pw][lane]);
-        }
-        __syncthreads();
-    }
-}
-#endif  // M3D_TUNE_ROI_PC
-
-// Spatial order of the lines (m3d_pyramid_roi_align3d_fwd_ws): a counting sort
-// by the owner (y, x) column of each line -- bucket = level base + (b, ty, lx)
-// in raster order -- so lines of different, overlapping ROIs that read the
-// same feature-map columns run next to each other, on one XCD (its L2).  The
-// order inside a bucket comes from atomics; every line writes only its own
-// output, so the result does not depend on it.
-__global__ void line_key_kernel(LineArgs a, Pyr P, RegionBase rb, int32_t* __restrict__ keys,
-                                int32_t* __restrict__ counts) {
-    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (L >= a.lines) return;
-    int64_t t = L;
-    const int x = (int)(t % a.cw); t /= a.cw;
-    const int y = (int)(t % a.ch);
-    const int64_t n = t / a.ch;
-    const int l = a.levels[n] - 2;
-    const int H = P.H[l], W = P.W[l];
-    const int64_t b = n / a.N;
-    const float* box = a.boxes + n * 6;
-    const int ty = owner_idx(axis_coord(box[0], box[3], H, a.ch, y, axis_scale(box[0], box[3], H, a.ch)), H);
-    const int lx = owner_idx(axis_coord(box[1], box[4], W, a.cw, x, axis_scale(box[1], box[4], W, a.cw)), W);
-    const int32_t k = (int32_t)(rb.base[l] + (b * H + ty) * W + lx);
-    keys[L] = k;
-    atomicAdd(counts + k, 1);
-}
 
 // exclusive prefix sum of counts[0..n) into offs, one workgroup of 1024
 __global__ __launch_bounds__(1024) void excl_scan_kernel(const int32_t* __restrict__ counts, int64_t n,
@@ -775,191 +469,9 @@ __global__ void line_scatter_kernel(const int32_t* __restrict__ keys, int64_t li
     perm[atomicAdd(offs + keys[L], 1)] = (int32_t)L;
 }
 
-// ROI order (M3D_ROI_SORT=2): the boxes ranked by (level, Morton code of the
-// centre's owner voxel), ties by index; perm[line] keeps each ROI's lines
-// contiguous (consecutive x lines share corner columns in L1) while
-// overlapping ROIs run next to each other.  One workgroup; O(n^2) ranking
-// over at most a few thousand boxes.
-__device__ __forceinline__ uint32_t morton2(uint32_t y, uint32_t x) {
-    uint32_t r = 0;
-    for (int i = 0; i < 12; ++i) r |= (((y >> i) & 1u) << (2 * i + 1)) | (((x >> i) & 1u) << (2 * i));
-    return r;
-}
-__global__ __launch_bounds__(1024) void roi_rank_kernel(LineArgs a, Pyr P, int64_t nbox,
-                                                        uint64_t* __restrict__ keys, int32_t* __restrict__ inv) {
-    for (int64_t n = threadIdx.x; n < nbox; n += 1024) {
-        const int l = a.levels[n] - 2;
-        const float* bx = a.boxes + n * 6;
-        const int cy = owner_idx(0.5f * (bx[0] + bx[3]) * (float)(P.H[l] - 1), P.H[l]);
-        const int cx = owner_idx(0.5f * (bx[1] + bx[4]) * (float)(P.W[l] - 1), P.W[l]);
-        const int64_t b = n / a.N;
-        keys[n] = ((uint64_t)b << 58) | ((uint64_t)l << 56) | ((uint64_t)morton2(cy, cx) << 32) | (uint64_t)n;
-    }
-    __syncthreads();
-    for (int64_t n = threadIdx.x; n < nbox; n += 1024) {
-        const uint64_t k = keys[n];
-        int64_t rank = 0;
-        for (int64_t j = 0; j < nbox; ++j) rank += keys[j] < k;
-        inv[rank] = (int32_t)n;
-    }
-}
-__global__ void roi_perm_kernel(const int32_t* __restrict__ inv, int64_t lines, int per_box,
-                                int32_t* __restrict__ perm) {
-    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (L >= lines) return;
-    const int64_t r = L / per_box;
-    perm[L] = (int32_t)(inv[r] * (int64_t)per_box + (L - r * per_box));
-}
-
 static int roi_slices() {
     static constexpr int env = M3D_TUNE_ROI_SLICES;
     return env;
-}
-
-// ---- PyramidROIAlign forward, region-major --------------------------------------
-// The ROI-major line kernel reads each ROI's own corner rows once, but rows
-// shared by overlapping ROIs are fetched again for every ROI (PMC traffic 2x
-// the globally unique bytes at 256^3, 512 ROIs).  Here a workgroup owns a
-// TY x TX x TZ block of one pyramid level's voxels and produces every ROI
-// sample whose floor corner lies in the block (samples outside the map are
-// assigned by the clamped coordinate, so every sample has exactly one owner):
-// the block's rows are read by all ROIs within the workgroup's short lifetime
-// and stay in L2, and the blocks are issued XCD-contiguously with z fastest,
-// so the z-neighbour's halo plane is in the same L2.  Per sample the
-// arithmetic is line_fwd_kernel's (bit-identical).  The sample coordinate is
-// monotone in the sample index (boxes_adj has y2 > y1 etc.), so the samples of
-// a box in a block are one contiguous index range per axis: lanes evaluate the
-// 64 sample coordinates of an axis and one ballot gives the range.
-struct RegionGrid {
-    int64_t off[5];              // first block of each level
-    int gy[4], gx[4], gz[4];     // blocks per axis and level
-};
-
-template <int TY, int TX, int TZ>
-__global__ __launch_bounds__(256) void region_fwd_kernel(LineArgs a, Pyr P, RegionGrid G) {
-    const int64_t blk = xcd_block();
-    if (blk >= G.off[4]) return;
-    int l = 0;
-    while (l < 3 && blk >= G.off[l + 1]) ++l;
-    int64_t r = blk - G.off[l];
-    const int bz = (int)(r % G.gz[l]); r /= G.gz[l];
-    const int bx = (int)(r % G.gx[l]); r /= G.gx[l];
-    const int by = (int)(r % G.gy[l]);
-    const int64_t b = r / G.gy[l];
-    const int H = P.H[l], W = P.W[l], D = P.D[l];
-    const int Y0 = by * TY, X0 = bx * TX, Z0 = bz * TZ;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int C4 = a.C >> 2;
-    const float4* base = reinterpret_cast<const float4*>(P.fmaps[l] + (size_t)b * H * W * D * a.C);
-    const size_t rowD = (size_t)D * C4, rowW = (size_t)W * rowD;
-    const float4 ex = make_float4(a.extrap, a.extrap, a.extrap, a.extrap);
-    int64_t k = 0;                                   // running work-unit counter (wave-uniform)
-    for (int64_t n0 = 0; n0 < a.N; n0 += 64) {
-        bool rel = false;
-        const int64_t nl = n0 + lane;
-        if (nl < a.N && a.levels[b * a.N + nl] == l + 2) {
-            const float* bx6 = a.boxes + (b * a.N + nl) * 6;
-            auto hit = [](float b1, float b2, int S, int n, int A0, int T) {
-                const float sc = axis_scale(b1, b2, S, n);
-                const int lo = owner_idx(axis_coord(b1, b2, S, n, 0, sc), S);
-                const int hi = owner_idx(axis_coord(b1, b2, S, n, n - 1, sc), S);
-                return hi >= A0 && lo < A0 + T;
-            };
-            rel = hit(bx6[0], bx6[3], H, a.ch, Y0, TY) && hit(bx6[1], bx6[4], W, a.cw, X0, TX) &&
-                  hit(bx6[2], bx6[5], D, a.cd, Z0, TZ);
-        }
-        for (uint64_t rm = __ballot(rel); rm; rm &= rm - 1) {
-            const int64_t n = b * a.N + n0 + __builtin_ctzll(rm);
-            const float* box = a.boxes + n * 6;
-            const float y1 = box[0], x1 = box[1], z1 = box[2], y2 = box[3], x2 = box[4], z2 = box[5];
-            const float ysc = axis_scale(y1, y2, H, a.ch), xsc = axis_scale(x1, x2, W, a.cw);
-            const float zsc = axis_scale(z1, z2, D, a.cd);
-            const int oy = owner_idx(axis_coord(y1, y2, H, a.ch, lane, ysc), H);
-            const int ox = owner_idx(axis_coord(x1, x2, W, a.cw, lane, xsc), W);
-            const int oz = owner_idx(axis_coord(z1, z2, D, a.cd, lane, zsc), D);
-            const uint64_t my = __ballot(lane < a.ch && oy >= Y0 && oy < Y0 + TY);
-            const uint64_t mx = __ballot(lane < a.cw && ox >= X0 && ox < X0 + TX);
-            const uint64_t mz = __ballot(lane < a.cd && oz >= Z0 && oz < Z0 + TZ);
-            if (!my || !mx || !mz) continue;
-            const int ny = __builtin_popcountll(my), nx = __builtin_popcountll(mx);
-            const int y0 = __builtin_ctzll(my), x0 = __builtin_ctzll(mx);
-            const int z0 = __builtin_ctzll(mz), z1e = z0 + __builtin_popcountll(mz);
-            const int64_t units = (int64_t)ny * nx;
-            // this wave's units: global unit index (k + u) == wave (mod 4)
-            for (int64_t u = (wave - k % 4 + 4) % 4; u < units; u += 4) {
-                const int y = y0 + (int)(u / nx), x = x0 + (int)(u % nx);
-                const float in_y = axis_coord(y1, y2, H, a.ch, y, ysc);
-                const float in_x = axis_coord(x1, x2, W, a.cw, x, xsc);
-                float4* o = reinterpret_cast<float4*>(a.out + ((n * a.ch + y) * a.cw + x) * (int64_t)a.cd * a.C);
-                const bool yx_oob = (in_y < 0 || in_y > (float)(H - 1)) || (in_x < 0 || in_x > (float)(W - 1));
-                if (yx_oob) {
-                    for (int z = z0; z < z1e; ++z)
-                        for (int c = lane; c < C4; c += 64) st_nt(o + (int64_t)z * C4 + c, ex);
-                    continue;
-                }
-                const int ty = (int)floorf(in_y), byy = (int)ceilf(in_y);
-                const int lx = (int)floorf(in_x), rx = (int)ceilf(in_x);
-                const float yl = in_y - (float)ty, xl = in_x - (float)lx;
-                const float4* col[4] = {base + ty * rowW + lx * rowD, base + ty * rowW + rx * rowD,
-                                        base + byy * rowW + lx * rowD, base + byy * rowW + rx * rowD};
-                for (int c = lane; c < C4; c += 64) {
-                    int pk = -1;
-                    float4 kv[4];
-                    for (int z = z0; z < z1e; ++z) {
-                        const float in_z = axis_coord(z1, z2, D, a.cd, z, zsc);
-                        float4 rv;
-                        if (in_z < 0 || in_z > (float)(D - 1)) {
-                            rv = ex;
-                        } else {
-                            const int fz = (int)floorf(in_z), kz = (int)ceilf(in_z);
-                            const float zl = in_z - (float)fz;
-                            float4 fv[4];
-                            if (fz == pk) {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) fv[q] = kv[q];
-                            } else {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) fv[q] = col[q][(size_t)fz * C4 + c];
-                            }
-                            if (kz != fz) {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) kv[q] = col[q][(size_t)kz * C4 + c];
-                            } else {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) kv[q] = fv[q];
-                            }
-                            pk = kz;
-                            rv = tri4(fv[0], kv[0], fv[1], kv[1], fv[2], kv[2], fv[3], kv[3], yl, xl, zl);
-                            rv.x = scrub(rv.x); rv.y = scrub(rv.y); rv.z = scrub(rv.z); rv.w = scrub(rv.w);
-                        }
-                        st_nt(o + (int64_t)z * C4 + c, rv);
-                    }
-                }
-            }
-            k += units;
-        }
-    }
-}
-
-// block shape of the region-major forward: M3D_ROI_REGION = 0 (off: line kernel,
-// default -- measured 3x slower at 256^3), 1 (2x2x8), 2 (4x4x4),
-// 3 (2x2x16), 4 (4x4x8)
-static int roi_region_mode() {
-    static constexpr int env = M3D_TUNE_ROI_REGION;
-    return env;
-}
-
-template <int TY, int TX, int TZ>
-static void launch_region_fwd(const LineArgs& a, const Pyr& P, int64_t B, hipStream_t s) {
-    RegionGrid G{};
-    G.off[0] = 0;
-    for (int l = 0; l < 4; ++l) {
-        G.gy[l] = (P.H[l] + TY - 1) / TY;
-        G.gx[l] = (P.W[l] + TX - 1) / TX;
-        G.gz[l] = (P.D[l] + TZ - 1) / TZ;
-        G.off[l + 1] = G.off[l] + B * G.gy[l] * G.gx[l] * G.gz[l];
-    }
-    hipLaunchKernelGGL((region_fwd_kernel<TY, TX, TZ>), dim3((unsigned)G.off[4]), dim3(256), 0, s, a, P, G);
 }
 
 // ---- trilinear backward in gather form ----------------------------------------
@@ -1076,10 +588,9 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(GatherArgs a, Pyr P) {
 }
 
 // the gather-form backward for C in {64, 128, 256, 512} and crops <= 32 per
-// axis (M3D_ROI_BWD_GATHER=0: the per-sample atomic scatter everywhere)
+// axis (the per-sample atomic scatter elsewhere)
 static bool gather_bwd_ok(int64_t C, int ch, int cw, int cd) {
-    static constexpr int env = M3D_TUNE_ROI_BWD_GATHER;
-    return env && (C == 64 || C == 128 || C == 256 || C == 512) && ch <= 32 && cw <= 32 && cd <= 32;
+    return (C == 64 || C == 128 || C == 256 || C == 512) && ch <= 32 && cw <= 32 && cd <= 32;
 }
 
 template <bool PYR>
@@ -1976,52 +1487,19 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
     if ((C & 3) == 0) {
         LineArgs a{nullptr, nullptr, boxes_adj, levels, N, B * N * ph * pw, 0, 0, 0, (int)C, ph, pw, pd,
                    0.0f, out};
-#if M3D_TUNE_ROI_ROW
-        {
-            if (C == 256 && pw <= 14 && pd >= M3D_TUNE_ROI_ROW) {
-                LineArgs ra = a;
-                ra.lines = B * N * ph;
-                if constexpr (M3D_TUNE_ROI_ROW_CG == 2)
-                    hipLaunchKernelGGL((row_fwd_kernel<14, 256, 2>), dim3((unsigned)(2 * ra.lines)), dim3(256), 0, s,
-                                       ra, P);
-                else if constexpr (M3D_TUNE_ROI_ROW_CG == 4)
-                    hipLaunchKernelGGL((row_fwd_kernel<14, 256, 4>), dim3((unsigned)(4 * ra.lines)), dim3(256), 0, s,
-                                       ra, P);
-                else
-                    hipLaunchKernelGGL((row_fwd_kernel<14, 512, 1>), dim3((unsigned)ra.lines), dim3(512), 0, s, ra, P);
-                return check_launch("row_fwd_kernel");
-            }
-        }
-#endif
         const int sl = roi_slices();
         if (C == 256 && (sl == 2 || sl == 4 || sl == 8 || sl == 16)) {
             const int32_t* perm = nullptr;
             const int32_t* wperm = nullptr;
             int64_t nb = 0, nl = 0;
             const size_t need = pyr_sort_layout(fshape, B, N, ph, pw, &nb, &nl);
-            // default order: waves sorted by their feature-map column (mode 3) for the
-            // 14^3 mask pool -- PMC fabric reads at 256^3 / 512 ROIs 3.41 -> 1.89 GB,
-            // 128^3 / 128 ROIs 0.167 -> 0.140 ms -- and launch order for small 7^3
-            // launches (their lines are short and the sort does not pay); M3D_ROI_SORT overrides
-            static constexpr int sort_env0 = M3D_TUNE_ROI_SORT;
-            // register-staged z parts (M3D_ROI_STAGE = PD, 0: off): zs = ceil(pd / PD) parts per line
-            static constexpr int stage_env = M3D_TUNE_ROI_STAGE;
-            const int spd = (stage_env == 4 || stage_env == 7 || stage_env == 14) && sl == 8 ? stage_env : 0;
-            // ... and for the 7^3 pool once the launch is large (512 ROIs at 256^3: PMC
-            // traffic 1.34 -> 1.09 GB at the same time; at 128^3 the sort costs 4 us of 58)
-            int sort_env = sort_env0 >= 0 ? sort_env0 : ((pd >= 14 || a.lines >= 16384) ? 3 : 0);
-            if (sort_env == 3 && spd && spd < pd) sort_env = 0;   // the wave order sorts whole lines
-            if (sort_env == 2 && workspace && ws_bytes >= need && nl < INT32_MAX && B * N <= nb) {
-                // ROI order: keys [B*N] (uint64, 8-B aligned at the start), inv [B*N], perm [lines]
-                uint64_t* rkeys = (uint64_t*)workspace;
-                int32_t* inv = (int32_t*)(rkeys + B * N);
-                int32_t* pm = inv + B * N;
-                hipLaunchKernelGGL(roi_rank_kernel, dim3(1), dim3(1024), 0, s, a, P, B * N, rkeys, inv);
-                hipLaunchKernelGGL(roi_perm_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, inv, nl, ph * pw, pm);
-                rc = check_launch("roi order");
-                if (rc) return rc;
-                perm = pm;
-            } else if (sort_env == 3 && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
+            // waves sorted by their feature-map column for the 14^3 mask pool -- PMC
+            // fabric reads at 256^3 / 512 ROIs 3.41 -> 1.89 GB, 128^3 / 128 ROIs 0.167
+            // -> 0.140 ms -- and for the 7^3 pool once the launch is large (512 ROIs at
+            // 256^3: PMC traffic 1.34 -> 1.09 GB); launch order for small 7^3 launches
+            // (their lines are short: at 128^3 the sort costs 4 us of 58)
+            const bool wave_sort = pd >= 14 || a.lines >= 16384;
+            if (wave_sort && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
                 const int64_t nw = (nl + sl - 1) / sl;
                 int32_t* counts = (int32_t*)workspace;
                 int32_t* offs = counts + nb;
@@ -2042,46 +1520,10 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 rc = check_launch("wave sort");
                 if (rc) return rc;
                 wperm = pm;
-            } else if (sort_env == 1 && workspace && ws_bytes >= need && nb < INT32_MAX && nl < INT32_MAX) {
-                int32_t* counts = (int32_t*)workspace;
-                int32_t* offs = counts + nb;
-                int32_t* keys = offs + nb;
-                int32_t* pm = keys + nl;
-                RegionBase rb{};
-                int64_t acc = 0;
-                for (int l = 0; l < 4; ++l) {
-                    rb.base[l] = acc;
-                    acc += B * fshape[l][0] * fshape[l][1];
-                }
-                if (hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)nb, s) != hipSuccess)
-                    return check_launch("memset line buckets");
-                hipLaunchKernelGGL(line_key_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, a, P, rb, keys, counts);
-                hipLaunchKernelGGL(excl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, nb, offs);
-                hipLaunchKernelGGL(line_scatter_kernel, dim3(grid_for(nl, 256)), dim3(256), 0, s, keys, nl, offs, pm);
-                rc = check_launch("line sort");
-                if (rc) return rc;
-                perm = pm;
             }
-            static constexpr int zs_env = M3D_TUNE_ROI_ZSPLIT;
-            const int zs = spd ? (int)((pd + spd - 1) / spd)
-                               : (wperm ? 1 : std::max(1, std::min(zs_env, (int)pd)));
+            const int zs = 1;
             const int64_t bs8 = (((a.lines * zs + sl - 1) / sl + 3) / 4 + 7) / 8 * 8;
             const unsigned grid = (unsigned)(bs8 * sl);
-#if M3D_TUNE_ROI_PC
-            static constexpr int pc_env = M3D_TUNE_ROI_PC;
-            if (pc_env && sl == 8 && zs == 1 && !spd && !perm) {
-                hipLaunchKernelGGL(line_fwd_pc_kernel, dim3(grid), dim3(512), 0, s, a, P, wperm);
-                return check_launch("line_fwd_pc_kernel");
-            }
-#endif
-#if M3D_TUNE_ROI_STAGE
-            if (spd) {
-                if (spd == 14) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 14>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-                else if (spd == 7) hipLaunchKernelGGL((line_fwd_sl_kernel<8, 7>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-                else hipLaunchKernelGGL((line_fwd_sl_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
-                return check_launch("line_fwd_sl_kernel<staged>");
-            }
-#endif
             if constexpr (M3D_TUNE_ROI_SLICES == 2)
                 hipLaunchKernelGGL(line_fwd_sl_kernel<2>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
             else if constexpr (M3D_TUNE_ROI_SLICES == 4)
@@ -2092,18 +1534,6 @@ static int pyramid_fwd_impl(const float* const fmaps[4], const int64_t fshape[4]
                 hipLaunchKernelGGL(line_fwd_sl_kernel<8>, dim3(grid), dim3(256), 0, s, a, P, perm, zs, wperm);
             return check_launch("line_fwd_sl_kernel");
         }
-#if M3D_TUNE_ROI_REGION
-        const int mode = roi_region_mode();
-        if (mode && ph <= 64 && pw <= 64 && pd <= 64) {
-            switch (mode) {
-                case 2: launch_region_fwd<4, 4, 4>(a, P, B, s); break;
-                case 3: launch_region_fwd<2, 2, 16>(a, P, B, s); break;
-                case 4: launch_region_fwd<4, 4, 8>(a, P, B, s); break;
-                default: launch_region_fwd<2, 2, 8>(a, P, B, s);
-            }
-            return check_launch("region_fwd_kernel");
-        }
-#endif
         hipLaunchKernelGGL(line_fwd_kernel<true>, dim3(grid_for(a.lines, 4)), dim3(256), 0, s, a, P);
         return check_launch("line_fwd_kernel");
     }

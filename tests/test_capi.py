@@ -191,3 +191,15 @@ def test_wino_dgrad_workspace_follows_the_call_tile():
         assert rc == -1 and b"workspace too small" in L.m3d_last_error()
         rc = L.m3d_conv3d_bwd_data_wino_vy(fake, fake, B, H, W, D, C1, C2, D, 1, fake, 0, fake, big, 0, 3, None)
         assert rc == -1 and b"tile_y" in L.m3d_last_error()
+
+
+def test_compile_time_switches_are_few():
+    """the refuted and measured-slower kernel variants are
+    deleted, not parked behind switches: at most 25 M3D_TUNE_* constants."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = set()
+    for f in glob.glob(os.path.join(root, "3d-mask-r-cnn_amd", "csrc", "*")):
+        names |= set(re.findall(r"\bM3D_TUNE_[A-Z0-9_]+", open(f).read()))
+    assert len(names) <= 25, sorted(names)
