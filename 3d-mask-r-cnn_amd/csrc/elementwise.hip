@@ -280,6 +280,156 @@ __global__ __launch_bounds__(256) void maxpool_fwd4z_kernel(const float4* __rest
     }
 }
 
+// maxpool_fwd4z_kernel specialised to the stem's pool (KL.MaxPooling3D((3,3,3),
+// (2,2,1), 'same'): core/models.py:244), no halo.  Per (y, x) tap column the
+// R + 2 input planes of the run are loaded as one unrolled batch (independent
+// loads in flight; the general kernel's runtime-bounded z loop issued them one
+// at a time behind its compares), clamped in range and masked; the compares
+// then run in the general kernel's order (ky, kx, iz ascending, first maximum
+// wins): bit-identical values and argmax.
+template <int R>
+__global__ __launch_bounds__(256) void maxpool_fwd333_kernel(const float4* __restrict__ x, int H, int W, int D,
+                                                             int C4, int OH, int OW, int nrun, uint32_t total,
+                                                             float4* __restrict__ y, uchar4* __restrict__ am) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int run = (int)(t % (uint32_t)nrun); t /= (uint32_t)nrun;
+        const int ox = (int)(t % (uint32_t)OW); t /= (uint32_t)OW;
+        const int oy = (int)(t % (uint32_t)OH);
+        const uint32_t b = t / (uint32_t)OH;
+        const int oz0 = run * R;                       // OD == D ('same', stride 1 along z)
+        const int nr = D - oz0 < R ? D - oz0 : R;
+        float best[R][4];
+        int bi[R][4];
+        bool any[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            any[r] = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { best[r][q] = -INFINITY; bi[r][q] = 0; }
+        }
+        // 'same' padding of a 3-window, stride 2: pad-before (k - 1 - (H - 1) % 2) / 2
+        const int py = (2 - (H - 1) % 2) / 2, px = (2 - (W - 1) % 2) / 2;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int iy = oy * 2 - py + ky;
+            if (iy < 0 || iy >= H) continue;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int ix = ox * 2 - px + kx;
+                if (ix < 0 || ix >= W) continue;
+                const uint32_t col = ((b * (uint32_t)H + iy) * (uint32_t)W + ix) * (uint32_t)D;
+                const int base = (ky * 3 + kx) * 3;
+                float4 v[R + 2];
+#pragma unroll
+                for (int p = 0; p < R + 2; ++p) {          // plane iz = oz0 - 1 + p
+                    int iz = oz0 - 1 + p;
+                    iz = iz < 0 ? 0 : (iz >= D ? D - 1 : iz);
+                    v[p] = x[(col + (uint32_t)iz) * (uint32_t)C4 + c];
+                }
+#pragma unroll
+                for (int p = 0; p < R + 2; ++p) {
+                    const int iz = oz0 - 1 + p;
+                    if (iz < 0 || iz >= D) continue;
+                    const float vv[4] = {v[p].x, v[p].y, v[p].z, v[p].w};
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kz = p - r;
+                        if (r < nr && kz >= 0 && kz < 3) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                if (!any[r] || vv[q] > best[r][q]) { best[r][q] = vv[q]; bi[r][q] = base + kz; }
+                            any[r] = true;
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t o0 = ((b * (uint32_t)OH + oy) * (uint32_t)OW + ox) * (uint32_t)D + oz0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r >= nr) break;
+            const uint32_t o = (o0 + r) * (uint32_t)C4 + c;
+            y[o] = make_float4(best[r][0], best[r][1], best[r][2], best[r][3]);
+            if (am) am[o] = make_uchar4((unsigned char)bi[r][0], (unsigned char)bi[r][1], (unsigned char)bi[r][2],
+                                        (unsigned char)bi[r][3]);
+        }
+    }
+}
+
+// maxpool_bwd4z_kernel specialised as maxpool_fwd333_kernel: per (oy, ox)
+// output column the R + 2 (argmax, gradient) rows of the run are loaded as one
+// unrolled batch, then added in the general kernel's order (oy, ox, oz
+// ascending): bit-identical sums.
+template <int R>
+__global__ __launch_bounds__(256) void maxpool_bwd333_kernel(const float4* __restrict__ dy,
+                                                             const uchar4* __restrict__ am, int H, int W, int D,
+                                                             int C4, int OH, int OW, int nrun, uint32_t total,
+                                                             float4* __restrict__ dx) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t c = i % (uint32_t)C4;
+        uint32_t t = i / (uint32_t)C4;
+        const int run = (int)(t % (uint32_t)nrun); t /= (uint32_t)nrun;
+        const int ix = (int)(t % (uint32_t)W); t /= (uint32_t)W;
+        const int iy = (int)(t % (uint32_t)H);
+        const uint32_t b = t / (uint32_t)H;
+        const int iz0 = run * R;
+        const int nr = D - iz0 < R ? D - iz0 : R;
+        float acc[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] = 0.0f;
+        const int py = (2 - (H - 1) % 2) / 2, px = (2 - (W - 1) % 2) / 2;
+        const int oy_lo = max(0, (iy + py - 1) / 2), oy_hi = min(OH - 1, (iy + py) / 2);
+        const int ox_lo = max(0, (ix + px - 1) / 2), ox_hi = min(OW - 1, (ix + px) / 2);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+            const int ky = iy - (oy * 2 - py);
+            if (ky < 0 || ky >= 3) continue;
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int kx = ix - (ox * 2 - px);
+                if (kx < 0 || kx >= 3) continue;
+                const uint32_t row = ((b * (uint32_t)OH + oy) * (uint32_t)OW + ox) * (uint32_t)D;
+                const int base = (ky * 3 + kx) * 3;
+                uchar4 a[R + 2];
+                float4 g[R + 2];
+#pragma unroll
+                for (int p = 0; p < R + 2; ++p) {          // output plane oz = iz0 - 1 + p
+                    int oz = iz0 - 1 + p;
+                    oz = oz < 0 ? 0 : (oz >= D ? D - 1 : oz);
+                    const uint32_t o = (row + (uint32_t)oz) * (uint32_t)C4 + c;
+                    a[p] = am[o];
+                    g[p] = dy[o];
+                }
+#pragma unroll
+                for (int p = 0; p < R + 2; ++p) {
+                    const int oz = iz0 - 1 + p;
+                    if (oz < 0 || oz >= D) continue;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kz = r - p + 2;           // iz0 + r - (oz - 1)
+                        if (r < nr && kz >= 0 && kz < 3) {
+                            const unsigned char id = (unsigned char)(base + kz);
+                            if (a[p].x == id) acc[r][0] += g[p].x;
+                            if (a[p].y == id) acc[r][1] += g[p].y;
+                            if (a[p].z == id) acc[r][2] += g[p].z;
+                            if (a[p].w == id) acc[r][3] += g[p].w;
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t bhw = (b * (uint32_t)H + iy) * (uint32_t)W + ix;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r >= nr) break;
+            dx[(bhw * (uint32_t)D + iz0 + r) * (uint32_t)C4 + c] =
+                make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        }
+    }
+}
+
 template <bool HALO, int R>
 __global__ __launch_bounds__(256) void maxpool_bwd4z_kernel(const float4* __restrict__ dy,
                                                             const uchar4* __restrict__ am, int H, int W, int D,
@@ -772,6 +922,15 @@ extern "C" int m3d_maxpool3d_fwd(const float* x, int64_t B, int64_t H, int64_t W
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && B * H * W * D * C / 4 < 0x7FFFFFFF && total / 4 < 0x7FFFFFFF &&
         ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        if (sz == 1 && kh == 3 && kw == 3 && kd == 3 && sy == 2 && sx == 2 && OD == D && pz == 1 &&
+            py == (2 - (H - 1) % 2) / 2 && px == (2 - (W - 1) % 2) / 2 && OH == (H + 1) / 2 && OW == (W + 1) / 2) {
+            const int nrun = (int)((OD + POOL_ZRUN - 1) / POOL_ZRUN);
+            const int64_t nt = B * OH * OW * nrun * (C / 4);
+            hipLaunchKernelGGL((maxpool_fwd333_kernel<POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                               (const float4*)x, (int)H, (int)W, (int)D, (int)(C / 4), (int)OH, (int)OW, nrun,
+                               (uint32_t)nt, (float4*)y, (uchar4*)argmax);
+            return check_launch("maxpool_fwd333_kernel");
+        }
         if (sz == 1) {
             const int nrun = (int)((OD + POOL_ZRUN - 1) / POOL_ZRUN);
             const int64_t nt = B * OH * OW * nrun * (C / 4);
@@ -804,6 +963,15 @@ extern "C" int m3d_maxpool3d_bwd(const float* dy, const uint8_t* argmax, int64_t
     if (total == 0) return M3D_OK;
     if (C % 4 == 0 && total / 4 < 0x7FFFFFFF && B * OH * OW * OD * C / 4 < 0x7FFFFFFF &&
         ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)argmax & 3) == 0) {
+        if (sz == 1 && kh == 3 && kw == 3 && kd == 3 && sy == 2 && sx == 2 && OD == D && pz == 1 &&
+            py == (2 - (H - 1) % 2) / 2 && px == (2 - (W - 1) % 2) / 2 && OH == (H + 1) / 2 && OW == (W + 1) / 2) {
+            const int nrun = (int)((D + POOL_ZRUN - 1) / POOL_ZRUN);
+            const int64_t nt = B * H * W * nrun * (C / 4);
+            hipLaunchKernelGGL((maxpool_bwd333_kernel<POOL_ZRUN>), dim3(ew_grid(nt)), dim3(256), 0, st(s),
+                               (const float4*)dy, (const uchar4*)argmax, (int)H, (int)W, (int)D, (int)(C / 4),
+                               (int)OH, (int)OW, nrun, (uint32_t)nt, (float4*)dx);
+            return check_launch("maxpool_bwd333_kernel");
+        }
         if (sz == 1) {
             const int nrun = (int)((D + POOL_ZRUN - 1) / POOL_ZRUN);
             const int64_t nt = B * H * W * nrun * (C / 4);

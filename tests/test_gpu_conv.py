@@ -176,6 +176,46 @@ def test_maxpool_same_and_subsample(cuda, C):
     np.testing.assert_array_equal(s.detach().cpu().numpy(), x[:, ::2, ::2].numpy())
 
 
+@pytest.mark.parametrize("shape", [(1, 16, 16, 21, 64), (2, 9, 7, 8, 16), (1, 12, 10, 3, 32)])
+def test_maxpool_333_specialised_equals_general(cuda, shape):
+    """maxpool_fwd333 / bwd333 (the stem pool, (3,3,3) / (2,2,1) 'same') against
+    the general z-run kernels they replace, run through the slab form with no
+    neighbours (m3d_maxpool3d_*_halo: the general kernels on the same grid):
+    values, argmax and input gradients bit-identical, odd / even H and W,
+    ragged and single-run depths.  Ties are made likely (values on a coarse
+    grid) so the first-maximum rule is exercised."""
+    from m3d import _lib
+    L = _lib.load()
+    B, H, W, D, C = shape
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    py, px = (2 - (H - 1) % 2) // 2, (2 - (W - 1) % 2) // 2
+    g = torch.Generator(device=cuda).manual_seed(4)
+    x = torch.randint(-4, 5, shape, device=cuda, generator=g).float() * 0.25
+    y1 = torch.empty((B, OH, OW, D, C), device=cuda)
+    y2 = torch.empty_like(y1)
+    a1 = torch.empty((B, OH, OW, D, C), device=cuda, dtype=torch.uint8)
+    a2 = torch.empty_like(a1)
+    halo = torch.zeros((B, H, W, 2, C), device=cuda)
+    _lib.check(L.m3d_maxpool3d_fwd(x.data_ptr(), B, H, W, D, C, 3, 3, 3, 2, 2, 1, py, px, 1, OH, OW, D,
+                                   y1.data_ptr(), a1.data_ptr(), _lib.stream()), "maxpool fwd")
+    _lib.check(L.m3d_maxpool3d_fwd_halo(x.data_ptr(), halo.data_ptr(), 0, 0, 1, B, H, W, D, C, 3, 3, 3, 2, 2, 1,
+                                        py, px, 1, OH, OW, D, y2.data_ptr(), a2.data_ptr(), _lib.stream()),
+               "halo fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2) and torch.equal(a1, a2)
+    dy = torch.randn((B, OH, OW, D, C), device=cuda, generator=g)
+    d1 = torch.empty_like(x)
+    d2 = torch.empty_like(x)
+    dh = torch.zeros_like(halo)
+    _lib.check(L.m3d_maxpool3d_bwd(dy.data_ptr(), a1.data_ptr(), B, H, W, D, C, 3, 3, 3, 2, 2, 1, py, px, 1, OH,
+                                   OW, D, d1.data_ptr(), _lib.stream()), "maxpool bwd")
+    _lib.check(L.m3d_maxpool3d_bwd_halo(dy.data_ptr(), a2.data_ptr(), 0, 0, 1, B, H, W, D, C, 3, 3, 3, 2, 2, 1,
+                                        py, px, 1, OH, OW, D, d2.data_ptr(), dh.data_ptr(), _lib.stream()),
+               "halo bwd")
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+
+
 def test_sgd_keras_matches_formula(cuda):
     from m3d import _lib
     from m3d.params import ParamStore
