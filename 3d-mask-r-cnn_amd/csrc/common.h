@@ -136,7 +136,7 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 // x3_mac_tiles (the 128x128 x3 GEMMs: small-channel Winograd point GEMMs and
 // weight gradients): tile pairs' chains interleaved -- 128^3 step 25.61-25.66
 // vs 25.76-25.85 ms (graph), 25.63-25.64 vs 25.76-25.82 eager, same box
-// (scripts/gpu_r05_pt.sh); bit-identical per accumulator
+// (scripts/archive/gpu_r05_pt.sh); bit-identical per accumulator
 // Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z.
 // 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
 // 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at

@@ -61,7 +61,7 @@ WGRAD_STREAM = True
 # step 26.23 vs 26.25 ms), but a HIP-graph replay puts a node's first-captured
 # successor on the node's own queue: with the weight gradient first, the
 # compute path hopped onto the weight-gradient queue behind its backlog and the
-# replay ran 28.7 ms; data gradient first, 26.04 ms (scripts/gpu_r05_graph3.sh).
+# replay ran 28.7 ms; data gradient first, 26.04 ms (scripts/archive/gpu_r05_graph3.sh).
 WGRAD_LAST = True
 _SIDE = {}
 _SIDE_USED = set()
@@ -105,7 +105,7 @@ def _throttle(key, side):
 # and peer devices, which no consumer of these events needs), "1" device-scope
 # release, "0" plain event, "torch":
 # Stream.wait_stream.  The fork showed as a ~7.5 us compute-queue bubble per
-# layer in the 128^3 kernel trace; A/B (scripts/gpu_r03x.sh, same box): mode 2
+# layer in the 128^3 kernel trace; A/B (scripts/archive/gpu_r03x.sh, same box): mode 2
 # 29.80 / 29.90 ms per step, torch / 0 / 1 30.05-30.10 ms.
 FORK_EVENT = "2"
 
@@ -311,7 +311,7 @@ def _splitk(xshape, geo, cin, cout, bwd_data):
 # faster from 256 tiles at short K too (256 -> 64: 0.37 vs 0.49 ms), but
 # inside the 256^3 step (fused BN-ReLU backward epilogues) it is not: slab step
 # 159.1 / 159.7 ms with the round-4 rule (K >= 256) for the data gradient vs
-# 160.2 / 167.8 with K >= 32 (scripts/gpu_r05_slab_ab.sh), so that rule stays.
+# 160.2 / 167.8 with K >= 32 (scripts/archive/gpu_r05_slab_ab.sh), so that rule stays.
 CONV1_X3_FWD_TILES = 128
 CONV1_X3_DGRAD_TILES = 256
 CONV1_X3_MIN_K = 32             # forward; round 4: 256 (and 256 tiles)
@@ -572,12 +572,12 @@ class BiasSums:
 # clears it); None: every bias-only unit reduces its own bias gradient inline.
 BIAS_BATCH = None
 # Batch the bias-only units' reductions (True) or launch one per unit (False,
-# default).  Measured at 128^3 (scripts/gpu_r05_bias.sh, same box): eager
+# default).  Measured at 128^3 (scripts/archive/gpu_r05_bias.sh, same box): eager
 # neutral (26.34 vs 26.32 ms, 655 vs 679 launches per step), but the HIP-graph
 # replay of the step slows from 26.0-26.2 to 30.6-30.7 ms with it on; under
 # rocprofv3 the batched replay shows no such loss (its queue assignment is the
 # clean one, r05gtrace2), so the cause is not found -- off until it is.  Ruled
-# out (scripts/gpu_r05_bias2.sh / _bias3.sh): where the flushes land (batches of
+# out (scripts/archive/gpu_r05_bias2.sh / _bias3.sh): where the flushes land (batches of
 # 2 / 4 / 16: all 30.1-30.2 ms), the item table's kernel-argument size (a
 # 4-item build: 30.1 ms) and which units are deferred (the FPN's alone, or the
 # RPN heads' one sum alone: 29.9-30.0 ms) -- one reduction moved from the
@@ -686,7 +686,7 @@ BN_FUSE = True
 # False: that GEMM's plain store, then the producer's bn_act_bwd).  Off: the
 # fused epilogue's per-half-tile BN sums spill in x3_gemm256_af_kernel<2>
 # (484 us per P2 launch), and the step is faster unfused -- 25.05 / 25.15 vs
-# 25.49 / 25.53 ms at 128^3, same box (scripts/gpu_r05_fuse_ab.sh).
+# 25.49 / 25.53 ms at 128^3, same box (scripts/archive/gpu_r05_fuse_ab.sh).
 X3_BN_FUSE = False
 
 

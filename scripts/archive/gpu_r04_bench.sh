@@ -1,6 +1,6 @@
 #!/bin/bash
 # The full bench line (with step-roofline tables) + host overhead on one box.
-# Usage: gpurun --timeout 900 -- bash scripts/gpu_r04_bench.sh TAG
+# Usage: gpurun --timeout 900 -- bash scripts/archive/gpu_r04_bench.sh TAG
 set -o pipefail
 TAG=${1:-r04}
 OUT=gpurun_out/$TAG

@@ -1,5 +1,5 @@
 #!/bin/bash
-# ROI kernels: parity tests + grad-image / forward timing.  Usage: gpurun -- bash scripts/gpu_r04_roi.sh TAG
+# ROI kernels: parity tests + grad-image / forward timing.  Usage: gpurun -- bash scripts/archive/gpu_r04_roi.sh TAG
 set -o pipefail
 TAG=${1:-r04roi}
 OUT=gpurun_out/$TAG

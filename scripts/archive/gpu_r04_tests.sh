@@ -1,5 +1,5 @@
 #!/bin/bash
-# All -m gpu tests + smoke on one box.  Usage: gpurun --timeout 1100 -- bash scripts/gpu_r04_tests.sh TAG
+# All -m gpu tests + smoke on one box.  Usage: gpurun --timeout 1100 -- bash scripts/archive/gpu_r04_tests.sh TAG
 set -o pipefail
 TAG=${1:-r04}
 OUT=gpurun_out/$TAG

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Serialized kernel trace (weight gradients in line, M3D_WGRAD_STREAM=0) of a
-# few 128^3 steps, for per-layer attribution.  Usage: gpurun -- bash scripts/gpu_r04_trace.sh TAG [S]
+# few 128^3 steps, for per-layer attribution.  Usage: gpurun -- bash scripts/archive/gpu_r04_trace.sh TAG [S]
 set -o pipefail
 TAG=${1:-r04tr}; S=${2:-128}
 OUT=gpurun_out/$TAG

@@ -1,6 +1,6 @@
 #!/bin/bash
 # x3 GEMM A/B: python scripts/x3_ab.py over the given make-ab libraries.
-# Usage: gpurun -- bash scripts/gpu_r04_x3ab.sh TAG lib1.so lib2.so ...
+# Usage: gpurun -- bash scripts/archive/gpu_r04_x3ab.sh TAG lib1.so lib2.so ...
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG

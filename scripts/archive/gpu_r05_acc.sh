@@ -2,7 +2,7 @@
 # Accuracy / step-time A/B of x3 accumulation and data-gradient tile builds:
 # the conv / Winograd / GEMM GPU tests under the default library, then per
 # library the 128^3 gradient error table (grad_table.py) and two interleaved
-# short bench runs (GRAD_LIBS / BENCH_LIBS: subsets), then the conv / Winograd / GEMM GPU tests (default library).  Usage: gpurun -- bash scripts/gpu_r05_acc.sh TAG libm3d.so libm3d_X.so ...
+# short bench runs (GRAD_LIBS / BENCH_LIBS: subsets), then the conv / Winograd / GEMM GPU tests (default library).  Usage: gpurun -- bash scripts/archive/gpu_r05_acc.sh TAG libm3d.so libm3d_X.so ...
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG

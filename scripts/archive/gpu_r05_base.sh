@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 baseline: the GPU suite, then per-layer conv table (each conv alone) and serialized
 # kernel traces (weight gradients in line) of the 128^3 and 256^3 steps.
-# Usage: gpurun -- bash scripts/gpu_r05_base.sh TAG
+# Usage: gpurun -- bash scripts/archive/gpu_r05_base.sh TAG
 set -o pipefail
 TAG=${1:-r05base}
 OUT=gpurun_out/$TAG

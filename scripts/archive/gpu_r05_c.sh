@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU suite + gradient error table (base host variants) + a short 128^3 bench
-# of the current tree.  Usage: gpurun -- bash scripts/gpu_r05_c.sh TAG
+# of the current tree.  Usage: gpurun -- bash scripts/archive/gpu_r05_c.sh TAG
 set -o pipefail
 TAG=${1:-r05c}
 OUT=gpurun_out/$TAG

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 evidence, call A: all -m gpu tests, smoke(), the full bench line
-# (with the step-roofline tables).  Call B: scripts/gpu_r05_prof.sh.
-# Usage: gpurun --timeout 1200 -- bash scripts/gpu_r05_final.sh TAG
+# (with the step-roofline tables).  Call B: scripts/archive/gpu_r05_prof.sh.
+# Usage: gpurun --timeout 1200 -- bash scripts/archive/gpu_r05_final.sh TAG
 set -o pipefail
 TAG=${1:-r05final}
 OUT=gpurun_out/$TAG

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-tensor gradient error tables (scripts/grad_table.py) of host variants and
-# of the F(2x2x4) build (libm3d_ny2.so).  Usage: gpurun -- bash scripts/gpu_r05_grad.sh TAG [variants]
+# of the F(2x2x4) build (libm3d_ny2.so).  Usage: gpurun -- bash scripts/archive/gpu_r05_grad.sh TAG [variants]
 set -o pipefail
 TAG=${1:-r05grad}; VAR=${2:-base,wino_min128,wino_min256,no_wino}
 OUT=gpurun_out/$TAG

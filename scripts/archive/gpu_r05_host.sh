@@ -3,7 +3,7 @@
 # batched paths' tests, the host enqueue profile of the 128^3 step
 # (scripts/host_overhead.py: enqueue vs wall per step and a cProfile of the
 # enqueue) and the per-layer conv table at 256^3.
-# Usage: gpurun -- bash scripts/gpu_r05_host.sh TAG
+# Usage: gpurun -- bash scripts/archive/gpu_r05_host.sh TAG
 set -o pipefail
 TAG=${1:-r05host}
 OUT=gpurun_out/$TAG

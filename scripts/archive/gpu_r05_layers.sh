@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-layer conv table (scripts/conv_layers.py) at SIZE for each library build.
-# Usage: gpurun -- bash scripts/gpu_r05_layers.sh TAG SIZE libm3d.so libm3d_X.so ...
+# Usage: gpurun -- bash scripts/archive/gpu_r05_layers.sh TAG SIZE libm3d.so libm3d_X.so ...
 set -o pipefail
 TAG=$1; SIZE=$2; shift 2
 OUT=gpurun_out/$TAG

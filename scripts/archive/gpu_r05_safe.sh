@@ -2,7 +2,7 @@
 # Staged check after a GPU fault: the x3 GEMM / conv / Winograd / BN-affine
 # tests with serialized launches first (a fault names its kernel), then the
 # 128^3 gradient error tables of the given libraries and short benches.
-# Usage: gpurun -- bash scripts/gpu_r05_safe.sh TAG libm3d.so [libm3d_X.so ...]
+# Usage: gpurun -- bash scripts/archive/gpu_r05_safe.sh TAG libm3d.so [libm3d_X.so ...]
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG

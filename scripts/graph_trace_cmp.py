@@ -1,5 +1,5 @@
 """Compare rocprofv3 kernel traces of the eager and the HIP-graph-replayed
-training step (scripts/gpu_r05_gtrace.sh): per step, the span, the summed
+training step (scripts/archive/gpu_r05_gtrace.sh): per step, the span, the summed
 kernel time, the union of busy time, the queues kernels landed on and the
 kernel groups whose time differs most.  Steps are delimited by the optimizer's
 sgd_update_kernel (one per step, after the backward)."""
