@@ -1399,6 +1399,129 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
         }
 }
 
+// ---- the same product for K, N <= 64 (the res2 64 -> 64 Winograd gradients) --
+// x3_wgrad_kernel's 128x128 tile at K = N = 64 runs four times the MFMAs it
+// needs (three of its four waves multiply zeros).  Here a workgroup owns the
+// whole 64x64 output and the four waves split the m chunk instead: a chunk is
+// 64 rows of m, staged as two 32-m sub-images per plane (the x3_off image of
+// x3_wgrad_kernel, 64 rows each), and wave w multiplies m rows 16w..16w+15 into
+// its own 64x64 accumulator (2 x 2 MFMA blocks).  The four partial tiles are
+// summed through LDS in wave order at the end: one output per element and
+// workgroup (fp32 atomics, or the deterministic partials, as x3_wgrad_kernel).
+// grid: splits * batch workgroups (x), XCD-contiguous order.
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __restrict__ A,
+                                                              const float* __restrict__ Bm,
+                                                              float* __restrict__ C, int64_t M, int K, int N,
+                                                              int64_t m_per_split, int64_t bsa, int64_t bsb,
+                                                              int64_t bsc, WgOut wo) {
+    constexpr int TI = 2, TJ = 2, BKM = 64;
+    constexpr int SUB = 64 * 64;                         // one 32-m sub-image: 64 rows x 64 B
+    constexpr int PL = 2 * SUB;                          // one plane of a 64-m chunk
+    constexpr int RED = 4 * 64 * 64 * 4;                 // the four waves' partial tiles
+    constexpr int SMEM = RED > 6 * PL ? RED : 6 * PL;
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int64_t total = gridDim.x;
+    const int64_t Lb = blockIdx.x;
+    const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
+    const int64_t bz = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
+    const int64_t batch = bz / nsplit;
+    float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
+    A += batch * bsa;
+    Bm += batch * bsb;
+    C += batch * bsc;
+    const int64_t ms = (bz % nsplit) * m_per_split;
+    const int64_t me = ms + m_per_split < M ? ms + m_per_split : M;
+    if (ms >= me) return;                                // (block-uniform)
+    // loader role (wave-uniform): operand, float4 column (16 = 64 columns), 8-row group (8 = 64 rows)
+    const bool isB = __builtin_amdgcn_readfirstlane(tid) >= 128;
+    const int lt = tid & 127, c4 = lt & 15, grp = lt >> 4;
+    const int ld = isB ? N : K;
+    const int col = c4 * 4;
+    const bool colok = col < ld;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(isB ? (const void*)Bm : (const void*)A, (uint64_t)M * ld * 4);
+    char* const Pb = smem + (isB ? 3 * PL : 0);
+    const int soff = (grp >> 2) * SUB;
+    float4 v[8];
+    auto load = [&](int64_t mb) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int64_t m = mb + grp * 8 + r;
+            v[r] = bload4(rs, (colok && m < me) ? (uint32_t)(m * ld + col) * 4u : M3D_OOB);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t hh[8], mm[8], ll[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) split3(f4get(v[r], c), hh[r], mm[r], ll[r]);
+            const int off = soff + x3_off(col + c, (grp & 3) * 8);
+            *reinterpret_cast<uint4*>(Pb + off) =
+                make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+            *reinterpret_cast<uint4*>(Pb + PL + off) =
+                make_uint4(mm[0] | (mm[1] << 16), mm[2] | (mm[3] << 16), mm[4] | (mm[5] << 16), mm[6] | (mm[7] << 16));
+            *reinterpret_cast<uint4*>(Pb + 2 * PL + off) =
+                make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+        }
+    };
+    floatx16 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    // this wave's 16 m rows of a chunk: sub-image wave / 2, k 16 (wave % 2) + 8h
+    const char* const As = smem + (wave >> 1) * SUB;
+    const char* const Bs = As + 3 * PL;
+    const int kq = 16 * (wave & 1) + 8 * h;
+    const int nchunks = (int)((me - ms + BKM - 1) / BKM);
+    load(ms);
+    store();
+    __syncthreads();
+    for (int t = 0; t < nchunks; ++t) {
+        if (t + 1 < nchunks) load(ms + (int64_t)(t + 1) * BKM);
+        bf16x8 af[TI][3], bfr[TJ][3];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int off = x3_off(i * 32 + l32, kq);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * PL + off);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const int off = x3_off(j * 32 + l32, kq);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PL + off);
+        }
+        x3_mac_tiles<TI, TJ>(acc, af, bfr);
+        __syncthreads();
+        if (t + 1 < nchunks) {
+            store();
+            __syncthreads();
+        }
+    }
+    // (the loop's last barrier ended every read of the operand images)
+    float* const R = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                R[(wave * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + j * 32 + l32] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int idx = tid + 256 * q, k = idx >> 6, n = idx & 63;
+        const float s = ((R[idx] + R[4096 + idx]) + R[8192 + idx]) + R[12288 + idx];
+        if (k < K && n < N) wg_put(wo, C, wp, (int64_t)k * N + n, s);
+    }
+}
+
 // ---- weight-gradient GEMM, 256x256 tiles, transposed LDS reads -------------
 // Same product as x3_wgrad_kernel (C[b][k][n] += sum_m A[b][m][k] B[b][m][n],
 // fp32 operands with the reduction index m as their rows, exact bf16 split).
@@ -1684,6 +1807,21 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
                             int64_t bsa, int64_t bsb, int64_t bsc, hipStream_t s) {
     if (wgrad_tr_env() && K >= 192 && N >= 192) {
         launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
+        return;
+    }
+    if (K <= 64 && N <= 64) {          // x3_wgrad64_kernel: one 64x64 tile, the m chunk over the waves
+        int64_t splits = (1024 + nbatch - 1) / nbatch;
+        const int64_t minm = wgrad_minm_env() > 64 ? wgrad_minm_env() : 64;
+        const int64_t max_splits = (M + minm - 1) / minm;
+        if (splits > max_splits) splits = max_splits;
+        if (splits < 1) splits = 1;
+        const WgOut wo = wg_out(splits, nbatch, K, N);
+        int64_t mper = (M + splits - 1) / splits;
+        mper = (mper + 63) / 64 * 64;
+        splits = (M + mper - 1) / mper;
+        hipLaunchKernelGGL((x3_wgrad64_kernel<2>), dim3((unsigned)(splits * nbatch)), dim3(256), 0, s, A, Bm, C, M,
+                           K, N, mper, bsa, bsb, bsc, wo);
+        wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
         return;
     }
     const int64_t tiles = (int64_t)((K + 127) / 128) * ((N + 127) / 128) * nbatch;
@@ -2439,12 +2577,16 @@ __device__ __forceinline__ int x3_soff(int row, int kc) {
     else return x3_off(row, kc * 8);
 }
 
-template <int BK, bool PERSIST, int OCC = (BK == 16 ? 3 : 2), bool AF32 = false>
+// BNT 64: 128x64 tiles for N = 64 (the res2 64-channel Winograd layers; a
+// 128-column tile would multiply 64 columns of zeros), each wave 64 x 32.
+template <int BK, bool PERSIST, int OCC = (BK == 16 ? 3 : 2), bool AF32 = false, int BNT = 128>
 __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
     static_assert(BK == 16 || BK == 32, "BK");
-    constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+    static_assert(BNT == 128 || BNT == 64, "BNT");
+    constexpr int BM = 128, BN = BNT, TM = 2, TN = BNT / 64;
     constexpr int NBUF = BK == 16 ? 2 : 1;
     constexpr int KCH = BK / 8, CPT = BM * KCH / 256;   // 16-B chunks per row / per thread and plane
+    constexpr int CPTB = BN * KCH / 256;                // the same for B (BN rows)
     constexpr int PLA = BM * BK * 2, PLB = BN * BK * 2;   // bytes per plane
     constexpr int STAGE = 3 * (PLA + PLB);
     constexpr int LDT = BN + 8, HR = 64;                  // epilogue staging (2 row halves)
@@ -2486,7 +2628,7 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
             const int c = tid + 256 * u;
             lrow[u] = (uint32_t)((c / KCH) * g.K + (c % KCH) * 8) * 2u;
         }
-        uint4 va[AF32 ? 1 : 3][CPT], vb[3][CPT];
+        uint4 va[AF32 ? 1 : 3][CPT], vb[3][CPTB];
         float4 fa[AF32 ? CPT : 1][2];   // AF32: the 8 fp32 k of each A chunk
         auto load = [&](int kt) {
 #pragma unroll
@@ -2502,7 +2644,8 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
                     } else {
                         va[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra[q], off, 0, 0));
                     }
-                    vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
+                    if (u < CPTB)
+                        vb[q][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb[q], off, 0, 0));
                 }
         };
         auto store = [&](int buf) {
@@ -2522,8 +2665,10 @@ __global__ __launch_bounds__(256, OCC) void x3_gemm_kernel(X3G g) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) *reinterpret_cast<uint4*>(As + q * PLA + soff[u]) = va[q][u];
                 }
+                if (u < CPTB) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) *reinterpret_cast<uint4*>(Bs + q * PLB + soff[u]) = vb[q][u];
+                    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint4*>(Bs + q * PLB + soff[u]) = vb[q][u];
+                }
             }
         };
         floatx16 acc[TM][TN];
@@ -4178,6 +4323,12 @@ static void wino_gemm_x3(const WinoWs& ws, int64_t T, int K, int N, int P, hipSt
         else hipLaunchKernelGGL(x3_gemm256_kernel<0>, grid, dim3(512), 0, s, q);
         return;
     }
+    if (N == 64) {             // 128x64 tiles (the res2 64-channel layers)
+        const int64_t tiles = ((T + 127) / 128) * P;
+        if (af32) hipLaunchKernelGGL((x3_gemm_kernel<32, false, 2, true, 64>), dim3((unsigned)tiles), dim3(256), 0, s, q);
+        else hipLaunchKernelGGL((x3_gemm_kernel<32, false, 3, false, 64>), dim3((unsigned)tiles), dim3(256), 0, s, q);
+        return;
+    }
     // 128x128 tiles, BK 32, 3 blocks per CU (2 with A in fp32)
     const int64_t tiles = ((T + 127) / 128) * ((N + 127) / 128) * P;
     if (af32) hipLaunchKernelGGL((x3_gemm_kernel<32, false, 2, true>), dim3((unsigned)tiles), dim3(256), 0, s, q);
@@ -4721,7 +4872,8 @@ static int bwd_weight_wino(const float* x, const float* u_in, const float* dz, i
     // M3D_WINO_GRAD4=1: the float4 form (measured slower: 278 vs 253 us avg, write-bound)
         WINO_LAUNCH_NZ(nz, wino_grad_kernel, dim3(grid_for(g.T * Cout, 256)), dim3(256), 0, st(s), dz, g,
                        (int)Cout, ws.M);
-    if (wgrad_x3_env() && Cout > 64) {
+    // (Cin, Cout <= 64: x3_wgrad64_kernel, the whole 64x64 product per workgroup)
+    if (wgrad_x3_env() && (Cout > 64 || Cin <= 64)) {
         launch_wgrad_x3(ws.U, ws.M, ws.V, g.T, (int)Cin, (int)Cout, wino_points(nz), g.T * Cin, g.T * Cout,
                         (int64_t)Cin * Cout, st(s));
     } else {

@@ -359,11 +359,13 @@ def test_wgrad_gemm_stream_k_shapes(cuda, nb, M, K, N):
 
 
 @pytest.mark.parametrize("nb,M,K,N", [(3, 300, 96, 160), (2, 300, 64, 256), (3, 1000, 256, 512),
-                                     (1, 256, 128, 256), (2, 257, 512, 768), (96, 520, 256, 512)])
+                                     (1, 256, 128, 256), (2, 257, 512, 768), (96, 520, 256, 512),
+                                     (3, 300, 64, 64), (144, 520, 64, 64)])
 def test_split3_exact_and_gemm_x3(cuda, nb, M, K, N):
     """m3d_split3_f32: hi + mid + lo == x exactly (float64 sum of the bf16
     planes); m3d_gemm_x3 (the Winograd point-GEMM kernels: x3_gemm_kernel,
-    and x3_gemm256_kernel for N % 256 == 0, M >= 256) against float64, ragged
+    its 128x64 tile for N == 64, and x3_gemm256_kernel for N % 256 == 0,
+    M >= 256) against float64, ragged
     M tiles; m3d_gemm_x3_af (fp32 A) bit-identical to it."""
     from m3d import _lib
     L = _lib.load()
@@ -618,9 +620,10 @@ def test_wino_shared_weight_transform_bit_identical(cuda):
         assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("cin,cout", [(128, 128), (256, 512)])
+@pytest.mark.parametrize("cin,cout", [(128, 128), (256, 512), (64, 64), (64, 128)])
 def test_wino_weight_gradient_accuracy(cuda, cin, cout):
-    """The Winograd weight gradient (the step's 3^3 convs with >= 128 channels,
+    """The Winograd weight gradient (the step's 3^3 convs with >= 64 channels;
+    64 -> 64 runs x3_wgrad64_kernel, 64 -> 128 x3_wgrad_kernel,
     F(2x2x4) tiles by default, M3D_WINO_WGRAD_NZ=2 for F(2x2x2)) against
     float64: the fp32 summation over the tiles passes through G^T, whose F(4,3)
     rows amplify it -- held to 2e-5 of the gradient's scale (the direct fp32

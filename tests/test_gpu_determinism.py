@@ -36,8 +36,10 @@ def _wgrad_wino(L, _lib, x, dz, cout, cuda):
 
 
 # (kernel, Cin, Cout, algorithm): conv_wgrad_kernel (3^3, 64 ch), x3_wgrad_kernel
-# (1^3, 256 -> 128), x3_wgrad_tr_kernel (Winograd 256 -> 256), conv_wgrad 1^3 64 -> 64
-CASES = [(3, 64, 64, "direct"), (1, 256, 128, "direct"), (3, 256, 256, "wino"), (1, 64, 64, "direct")]
+# (1^3, 256 -> 128), x3_wgrad_tr_kernel (Winograd 256 -> 256), conv_wgrad 1^3 64 -> 64,
+# x3_wgrad64_kernel (Winograd 64 -> 64, the res2 branch2b gradients)
+CASES = [(3, 64, 64, "direct"), (1, 256, 128, "direct"), (3, 256, 256, "wino"), (1, 64, 64, "direct"),
+         (3, 64, 64, "wino")]
 
 
 @pytest.mark.parametrize("k,cin,cout,alg", CASES)
