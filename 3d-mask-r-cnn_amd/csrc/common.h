@@ -122,37 +122,12 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3W_SK
 #define M3D_TUNE_X3W_SK 1
 #endif
-// wave-quantised m-splits for the 256x256 weight-gradient kernel (A/B only):
-// Q = 8 / 16 measured 25.5 / 25.45 vs 25.2-25.4 ms at 128^3 and 149.2-149.6 vs
-// 148.3-148.5 ms at 256^3 (profiles/r04q_wgrad_quant_ab.txt): the kernel runs on
-// the side stream beside the data gradient, which fills the tail wave anyway.
-// small-m weight gradients: lower the m floor until the grid fills the chip
-// (A/B only): 128^3 25.19 vs 25.18 ms with the RPN heads' gradient on the side
-// stream, 25.19 vs 25.31-25.38 ms without (profiles/r04s_rpn_wgrad_ab.txt) --
-// the side stream alone removes the same cost from the critical path.
-// the x3 GEMMs' two accumulator tiles per A fragment issued interleaved
-// (x3_mac_pair; 0: one tile's six-MFMA chain after the other)
-// x3_gemm256_af_kernel: two A rows' fragments per step, four chains interleaved (A/B)
-// x3_mac_tiles (the 128x128 x3 GEMMs: small-channel Winograd point GEMMs and
-// weight gradients): tile pairs' chains interleaved -- 128^3 step 25.61-25.66
-// vs 25.76-25.85 ms (graph), 25.63-25.64 vs 25.76-25.82 eager, same box
-// (scripts/archive/gpu_r05_pt.sh); bit-identical per accumulator
+// (Measured-slower variants and their switches were removed in round 6:
+// DESIGN.md section 8 lists them, docs/DESIGN_HISTORY.md has their numbers.)
 // Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z.
 // 4 (round 4): 4x2x4 tiles, 144 points per 32 outputs instead of 96 per 16 --
 // 25 % fewer point-GEMM FLOPs and transform bytes; step 26.9 -> 25.0 ms at
 // 128^3 (same box, r04ny4_ab), parity suite green (profiles/r04ny4_parity_tests.log)
-// x3 GEMM accumulation (conv3d.hip x3_mac): 0 = one MFMA accumulator chain
-// (default); bits 0/1/2 = each 16-deep k step's six bf16 MFMAs into a fresh
-// accumulator added to the running sum by one VALU add, for the point GEMMs /
-// implicit-GEMM convs / weight gradients.  The host model predicted half the
-// error; measured on the MI355X the 128^3 gradient median got WORSE (3.29e-6
-// vs 2.28e-6 with bit 0, F(2x2x4) data gradients) and the step slower (27.2 vs
-// 26.6 ms, gpurun_out/r05safe): the MFMA accumulator does better than an
-// fp32 rounding per instruction.  Kept as an A/B switch.
-// 1x1x1 conv epilogue inside x3_gemm256_af_kernel (1) or as a second pass (0)
-// conv_gemm epilogue: float4 rows per thread whose residual / destination loads
-// are issued together before their stores (4: round 4)
-// the implicit-GEMM convs on the bf16 split at 2 workgroups per CU instead of 3
 #ifndef M3D_TUNE_WINO_NY
 #define M3D_TUNE_WINO_NY 4
 #endif
@@ -169,7 +144,7 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #define M3D_TUNE_WINO_DGRAD_NY 2
 #endif
 #ifndef M3D_TUNE_WGRAD1_X3_MIN_N
-#define M3D_TUNE_WGRAD1_X3_MIN_N 65
+#define M3D_TUNE_WGRAD1_X3_MIN_N 65   // 64 (x3_wgrad64_kernel for 256 -> 64, 64 -> 64): step-neutral, 64 -> 64 slower alone (r06c64b)
 #endif
 #ifndef M3D_TUNE_BN_BLOCKS
 #define M3D_TUNE_BN_BLOCKS 1024
@@ -177,14 +152,3 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_ROI_SLICES
 #define M3D_TUNE_ROI_SLICES 8
 #endif
-// PyramidROIAlign forward in the separable row form (row_fwd_kernel) for pools
-// of depth >= this (0: off; A/B builds only -- bit-identical, but 1.03 ms vs the
-// line kernel's 0.88 ms at 256^3 14^3 and 0.24 vs 0.14 ms at 128^3, r04r)
-// ... its workgroups per output row (channel groups of 256 / CG channels)
-// x3_gemm256_af_kernel: A loaded three steps ahead (no wait inside a step).
-// Round 6 (profiles/r06_x3af_stamps_128.txt, per-step clock stamps): with A two
-// steps ahead the six unrolled step copies ran 3.9K-7.2K cycles (the compiler's
-// waits differed per copy, one drained the prefetch); three ahead, three copies,
-// 3.7K-4.6K; priced launch 0.998 -> 0.959 ms, 128^3 step 25.33 -> 24.96 ms (same box)
-// the 256x256 Winograd point GEMM only where it has at least this many tiles
-// (step A/B r04t1: 0 27.26 ms, 256 27.39, 512 27.36; isolated launches favoured 256)

@@ -1399,16 +1399,18 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad_kernel(const float* __restr
         }
 }
 
-// ---- the same product for K, N <= 64 (the res2 64 -> 64 Winograd gradients) --
+// ---- the same product on 64x64 tiles (K or N <= 64: the res2 gradients) -----
 // x3_wgrad_kernel's 128x128 tile at K = N = 64 runs four times the MFMAs it
-// needs (three of its four waves multiply zeros).  Here a workgroup owns the
-// whole 64x64 output and the four waves split the m chunk instead: a chunk is
+// needs (three of its four waves multiply zeros), at K = 64 twice.  Here a
+// workgroup owns one 64x64 output tile and the four waves split the m chunk
+// instead of the tile: a chunk is
 // 64 rows of m, staged as two 32-m sub-images per plane (the x3_off image of
 // x3_wgrad_kernel, 64 rows each), and wave w multiplies m rows 16w..16w+15 into
 // its own 64x64 accumulator (2 x 2 MFMA blocks).  The four partial tiles are
 // summed through LDS in wave order at the end: one output per element and
 // workgroup (fp32 atomics, or the deterministic partials, as x3_wgrad_kernel).
-// grid: splits * batch workgroups (x), XCD-contiguous order.
+// grid: tiles * splits * batch workgroups (x), XCD-contiguous order with the
+// tiles of one (batch, split) adjacent, so they share its m rows in one L2.
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __restrict__ A,
                                                               const float* __restrict__ Bm,
@@ -1425,7 +1427,11 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __res
     const int64_t total = gridDim.x;
     const int64_t Lb = blockIdx.x;
     const int64_t xcd = Lb % 8, q8 = total / 8, r8 = total % 8;
-    const int64_t bz = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int64_t Lt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Lb / 8;
+    const int tk = (K + 63) / 64, tiles = tk * ((N + 63) / 64);
+    const int tile = (int)(Lt % tiles);
+    const int k0 = (tile % tk) * 64, n0 = (tile / tk) * 64;
+    const int64_t bz = Lt / tiles;
     const int64_t nsplit = (M + m_per_split - 1) / m_per_split;
     const int64_t batch = bz / nsplit;
     float* const wp = wo.part ? wo.part + (bz % nsplit) * wo.pstride + batch * (int64_t)K * N : nullptr;
@@ -1439,11 +1445,12 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __res
     const bool isB = __builtin_amdgcn_readfirstlane(tid) >= 128;
     const int lt = tid & 127, c4 = lt & 15, grp = lt >> 4;
     const int ld = isB ? N : K;
-    const int col = c4 * 4;
+    const int col = (isB ? n0 : k0) + c4 * 4;
     const bool colok = col < ld;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(isB ? (const void*)Bm : (const void*)A, (uint64_t)M * ld * 4);
     char* const Pb = smem + (isB ? 3 * PL : 0);
     const int soff = (grp >> 2) * SUB;
+    const int lrow = c4 * 4;                             // the column's row in the tile image
     float4 v[8];
     auto load = [&](int64_t mb) {
 #pragma unroll
@@ -1458,7 +1465,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __res
             uint32_t hh[8], mm[8], ll[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) split3(f4get(v[r], c), hh[r], mm[r], ll[r]);
-            const int off = soff + x3_off(col + c, (grp & 3) * 8);
+            const int off = soff + x3_off(lrow + c, (grp & 3) * 8);
             *reinterpret_cast<uint4*>(Pb + off) =
                 make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
             *reinterpret_cast<uint4*>(Pb + PL + off) =
@@ -1516,7 +1523,7 @@ __global__ __launch_bounds__(256, OCC) void x3_wgrad64_kernel(const float* __res
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        const int idx = tid + 256 * q, k = idx >> 6, n = idx & 63;
+        const int idx = tid + 256 * q, k = k0 + (idx >> 6), n = n0 + (idx & 63);
         const float s = ((R[idx] + R[4096 + idx]) + R[8192 + idx]) + R[12288 + idx];
         if (k < K && n < N) wg_put(wo, C, wp, (int64_t)k * N + n, s);
     }
@@ -1809,8 +1816,9 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
         launch_wgrad_tr(A, Bm, C, M, K, N, nbatch, bsa, bsb, bsc, s);
         return;
     }
-    if (K <= 64 && N <= 64) {          // x3_wgrad64_kernel: one 64x64 tile, the m chunk over the waves
-        int64_t splits = (1024 + nbatch - 1) / nbatch;
+    if (K <= 64 || N <= 64) {          // x3_wgrad64_kernel: 64x64 tiles, the m chunk over the waves
+        const int64_t tiles = (int64_t)((K + 63) / 64) * ((N + 63) / 64);
+        int64_t splits = (1024 + tiles * nbatch - 1) / (tiles * nbatch);
         const int64_t minm = wgrad_minm_env() > 64 ? wgrad_minm_env() : 64;
         const int64_t max_splits = (M + minm - 1) / minm;
         if (splits > max_splits) splits = max_splits;
@@ -1819,7 +1827,7 @@ static void launch_wgrad_x3(const float* A, const float* Bm, float* C, int64_t M
         int64_t mper = (M + splits - 1) / splits;
         mper = (mper + 63) / 64 * 64;
         splits = (M + mper - 1) / mper;
-        hipLaunchKernelGGL((x3_wgrad64_kernel<2>), dim3((unsigned)(splits * nbatch)), dim3(256), 0, s, A, Bm, C, M,
+        hipLaunchKernelGGL((x3_wgrad64_kernel<2>), dim3((unsigned)(tiles * splits * nbatch)), dim3(256), 0, s, A, Bm, C, M,
                            K, N, mper, bsa, bsb, bsc, wo);
         wg_finish(wo, splits, nbatch, K, N, bsc, C, s);
         return;

@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 P=res2a_branch2b+res2b_branch2b+res2c_branch2b
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_conv.py \
-  -k "split3_exact_and_gemm_x3 or wino_weight_gradient_accuracy or conv_block_fwd_bwd" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+  -k "split3_exact_and_gemm_x3 or wino_weight_gradient_accuracy or conv_block_fwd_bwd or batched_wgrad_gemm" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_determinism.py \
   -k "weight_gradient_bitwise" >> $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 grep -c PASSED $OUT/tests.log

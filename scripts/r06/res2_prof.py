@@ -52,6 +52,14 @@ for name, (H, W, D) in {"res2_128": (32, 32, 128), "res2_256": (64, 64, 256)}.it
             "dgrad"))
     r["wgrad_ms"] = timed(lambda: _lib.check(L.m3d_conv3d_bwd_weight_wino(
         x.data_ptr(), dz.data_ptr(), 1, H, W, D, C, C, D, 1, dw.data_ptr(), ws.data_ptr(), nb, None, s), "wgrad"))
+    for ci, co in ((64, 256), (256, 64), (64, 64)):      # the res2 1x1x1 weight gradients
+        x1 = torch.randn((1, H, W, D, ci), device=dev, generator=g)
+        dz1 = torch.randn((1, H, W, D, co), device=dev, generator=g)
+        dw1 = torch.zeros((1, 1, 1, ci, co), device=dev)
+        r[f"wgrad1_{ci}_{co}_ms"] = timed(lambda: _lib.check(L.m3d_conv3d_bwd_weight(
+            x1.data_ptr(), dz1.data_ptr(), 1, H, W, D, ci, 1, 1, 1, co, H, W, D, 1, 1, 1, 0, 0, 0, dw1.data_ptr(), s),
+            "wgrad1"))
+        del x1, dz1, dw1
     r["tensor_mb"] = H * W * D * C * 4 / 1e6
     out[name] = r
     print(name, json.dumps(r), flush=True)

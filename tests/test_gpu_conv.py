@@ -71,6 +71,7 @@ CASES = [
     ((64, 60, 8), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),    # stem: several tiles per wave
     ((20, 18, 80), 1, 64, (7, 7, 7), (2, 2, 1), 3, True, True, False),   # stem: windows inside the volume
     ((3, 5, 9), 32, 160, (3, 3, 3), (1, 1, 1), "same", True, False, True),
+    ((8, 8, 6), 256, 64, (1, 1, 1), (1, 1, 1), "valid", True, True, False),   # x3_wgrad64_kernel, 4 x 1 tiles
 ]
 
 
@@ -317,12 +318,14 @@ def test_winograd_z_halo_geometry(cuda, D, OD, pz):
 
 @pytest.mark.parametrize("nb,M,K,N", [(3, 200, 64, 96), (2, 1000, 128, 36), (64, 512, 256, 512),
                                      (2, 1000, 320, 260), (1, 37, 192, 196), (3, 4099, 512, 256),
-                                     (9, 4096, 256, 512), (5, 4000, 256, 256)])
+                                     (9, 4096, 256, 512), (5, 4000, 256, 256), (2, 1000, 64, 200),
+                                     (1, 5000, 48, 136)])
 def test_batched_wgrad_gemm_f32(cuda, nb, M, K, N):
     """m3d_gemm_wgrad_f32 (the Winograd weight-gradient GEMM launch bench.py
     prices): C[b] += A[b]^T B[b] against a float64 torch bmm, ragged M/K/N tiles.
-    The last two cut tiles across stream-K workgroup ranges at odd steps
-    (x3_wgrad_tr_kernel<0, true>: 18 and ~16 steps per workgroup)."""
+    (9, 4096, ...) and (5, 4000, ...) cut tiles across stream-K workgroup ranges
+    at odd steps (x3_wgrad_tr_kernel<0, true>: 18 and ~16 steps per workgroup);
+    K <= 64 runs x3_wgrad64_kernel's 64x64 tiles, ragged K / N."""
     from m3d import _lib
     L = _lib.load()
     g = torch.Generator().manual_seed(11)
