@@ -129,6 +129,12 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off)
     return *reinterpret_cast<float4*>(&v);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float a, float b, float c, float d) {
+    u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
+}
+
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
@@ -3046,65 +3052,85 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
 #endif
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(g.c + bz * g.bsc + m0 * g.N, (uint64_t)(g.M - m0) * g.N * 4);
     if constexpr (EPI == 2) {
-        // fused BN-ReLU backward (X3Epi on == 2): per accumulator tile its 16 y / z
-        // values loaded before its stores; rows past M load zeros (masked, summed
-        // as 0) and their stores are dropped
+        // fused BN-ReLU backward (X3Epi on == 2), staged per wave through LDS:
+        // each wave writes one 32-row block of its 128 x 64 accumulator tile into
+        // a private LDS slot (no barrier: only the wave reads it back), reads it
+        // row-major as float4 and applies the BN backward with float4 y / z loads
+        // and float4 dz / dres stores.  The accumulators die block by block, so
+        // the epilogue needs few registers (the per-element form held the tile,
+        // 32 loads and their lane offsets at once and spilled ~140 registers).
+        // Rows past M load zeros (masked, summed as 0) and their stores are
+        // dropped; an absent y / z / dres has an empty descriptor.
         const X3Epi& E = g.ep;
         const uint64_t rbytes = (uint64_t)(g.M - m0) * g.N * 4;
         const __amdgpu_buffer_rsrc_t ry = make_rsrc(E.fy ? E.fy + m0 * g.N : g.c, E.frelu ? rbytes : 0);
         const __amdgpu_buffer_rsrc_t rzz = make_rsrc(E.fz ? E.fz + m0 * g.N : g.c, E.fz ? rbytes : 0);
         const __amdgpu_buffer_rsrc_t rd = make_rsrc(E.fdres ? E.fdres + m0 * g.N : g.c, E.fdres ? rbytes : 0);
-        float sums[2][3];
+        const bool relu = __builtin_amdgcn_readfirstlane(E.frelu) != 0;
+        constexpr int WLD = 68;                           // staging row pitch (floats)
+        __syncthreads();                                  // every wave's last stage reads are done
+        char* const slot0 = (wave % 6 == 0) ? sA0 : (wave % 6 == 1) ? sA1 : (wave % 6 == 2) ? sA2
+                          : (wave % 6 == 3) ? sB0 : (wave % 6 == 4) ? sB1 : sB2;
+        float* const Tw = reinterpret_cast<float*>(slot0 + (wave / 6) * (32 * WLD * 4));
+        const int c4 = lane & 15, rq = lane >> 4;
+        const int col = (int)n0 + wn * 64 + c4 * 4;
+        float sc[4], mu[4], rs[4], sp[4], sx[4], sz[4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = (int)n0 + wn * 64 + j * 32 + l32;
-            const float sc = E.fscale ? E.fscale[col] : 1.0f;
-            const float mu = E.fz ? E.fmean[col] : 0.0f, rs = E.fz ? E.frstd[col] : 1.0f;
-            float sp = 0.f, sx = 0.f, sz = 0.f;
+        for (int e = 0; e < 4; ++e) {
+            sc[e] = E.fscale ? E.fscale[col + e] : 1.0f;
+            mu[e] = E.fz ? E.fmean[col + e] : 0.0f;
+            rs[e] = E.fz ? E.frstd[col + e] : 1.0f;
+            sp[e] = sx[e] = sz[e] = 0.0f;
+        }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float yv[16], zv[16];
+        for (int i = 0; i < 4; ++i) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int off = (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u);
-                    yv[r] = E.frelu ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, off, 0, 0)) : 1.0f;
-                    zv[r] = E.fz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rzz, off, 0, 0)) : 0.0f;
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    Tw[((r & 3) + 8 * (r >> 2) + 4 * h) * WLD + j * 32 + l32] = acc[i][j][r];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int lr = rq + 4 * q;
+                const float4 a = *reinterpret_cast<const float4*>(Tw + lr * WLD + c4 * 4);
+                const uint32_t off = ((uint32_t)(wm * 128 + i * 32 + lr) * (uint32_t)g.N + (uint32_t)col) * 4u;
+                const float4 y4 = bload4(ry, off), z4 = bload4(rzz, off);
+                float gv[4], d[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    gv[e] = (relu && !(f4get(y4, e) > 0.f)) ? 0.f : f4get(a, e);
+                    d[e] = gv[e] * sc[e];
+                    sp[e] += gv[e];
+                    sx[e] += gv[e] * ((f4get(z4, e) - mu[e]) * rs[e]);
+                    sz[e] += d[e];
                 }
+                bstore4(rc, off, d[0], d[1], d[2], d[3]);
+                bstore4(rd, off, gv[0], gv[1], gv[2], gv[3]);
+                // the running sums pinned here: left free, the scheduler deferred
+                // the 96 serial adds of a block behind all its loads and kept every
+                // row's gv / d live until then (spills)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int off = (int)(((uint32_t)row * (uint32_t)g.N + (uint32_t)col) * 4u);
-                    float gv = acc[i][j][r];
-                    if (E.frelu && !(yv[r] > 0.f)) gv = 0.f;
-                    const float d = gv * sc;
-                    sp += gv;
-                    sx += gv * ((zv[r] - mu) * rs);
-                    sz += d;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d), rc, off, 0, 0);
-                    if (E.fdres) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rd, off, 0, 0);
-                }
-                // one tile's 32 loads in flight at a time (hoisting every tile's
-                // loads above the stores spilled hundreds of registers)
-                __builtin_amdgcn_sched_barrier(0);
+                for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(sp[e]), "+v"(sx[e]), "+v"(sz[e]));
             }
-            sums[j][0] = sp; sums[j][1] = sx; sums[j][2] = sz;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // block i read back before block i+1 is staged
         }
         if (!E.fpart) return;
-        // column sums of each 128-row half tile (wave row wm): the two lane halves
-        // (rows 4 apart) combined, one partial row per half tile (no block barrier)
+        // column sums of each 128-row half tile (wave row wm): the four lane groups
+        // (rows rq + 4q) combined, one partial row per half tile (no block barrier)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int a = 0; a < 3; ++a) sums[j][a] += __shfl_xor(sums[j][a], 32);
-        if (h == 0) {
+        for (int e = 0; e < 4; ++e) {
+            sp[e] += __shfl_xor(sp[e], 16); sx[e] += __shfl_xor(sx[e], 16); sz[e] += __shfl_xor(sz[e], 16);
+            sp[e] += __shfl_xor(sp[e], 32); sx[e] += __shfl_xor(sx[e], 32); sz[e] += __shfl_xor(sz[e], 32);
+        }
+        if (rq == 0) {
             const int64_t prow = (m0 / 256) * 2 + wm;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int col = (int)n0 + wn * 64 + j * 32 + l32;
-#pragma unroll
-                for (int a = 0; a < 3; ++a) E.fpart[((int64_t)a * E.fprows + prow) * g.N + col] = sums[j][a];
-            }
+            float* const f0 = E.fpart + ((int64_t)0 * E.fprows + prow) * g.N + col;
+            float* const f1 = E.fpart + ((int64_t)1 * E.fprows + prow) * g.N + col;
+            float* const f2 = E.fpart + ((int64_t)2 * E.fprows + prow) * g.N + col;
+            *reinterpret_cast<float4*>(f0) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+            *reinterpret_cast<float4*>(f1) = make_float4(sx[0], sx[1], sx[2], sx[3]);
+            *reinterpret_cast<float4*>(f2) = make_float4(sz[0], sz[1], sz[2], sz[3]);
         }
         return;
     }

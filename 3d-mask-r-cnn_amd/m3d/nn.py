@@ -683,11 +683,12 @@ def _link_park(link, dx, acc):
 # BN_FUSE = False runs bn_act_bwd everywhere (A/B; tests/test_gpu_bnfuse.py).
 BN_FUSE = True
 # ... and in the bf16-split 1x1x1 data gradient (m3d_conv3d_bwd_data_x3_bn;
-# False: that GEMM's plain store, then the producer's bn_act_bwd).  Off: the
-# fused epilogue's per-half-tile BN sums spill in x3_gemm256_af_kernel<2>
-# (484 us per P2 launch), and the step is faster unfused -- 25.05 / 25.15 vs
-# 25.49 / 25.53 ms at 128^3, same box (scripts/archive/gpu_r05_fuse_ab.sh).
-X3_BN_FUSE = False
+# False: that GEMM's plain store, then the producer's bn_act_bwd).  Round 5
+# had it off (the epilogue spilled: 25.49 vs 25.05 ms at 128^3); round 6's
+# spill-free x3_gemm256_af_kernel<2> (per-wave LDS staging, float4 rows):
+# 128^3 24.54 vs 24.60 ms, 256^3 148.1 vs 148.8 ms, same box
+# (scripts/r06/gpu_fuse.sh, profiles/r06_x3_bn_fuse_ab.txt).
+X3_BN_FUSE = True
 
 
 class BNFuse:
