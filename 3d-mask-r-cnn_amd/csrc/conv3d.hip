@@ -2559,6 +2559,7 @@ struct X3Epi {
     float* fpart = nullptr;
     int64_t fprows = 0;
     int frelu = 0;
+    int facc = 0;                 // on == 2: the gradient is accumulator + C (C holds the parked gradient)
 };
 
 struct X3G {
@@ -3067,6 +3068,8 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
         const __amdgpu_buffer_rsrc_t rzz = make_rsrc(E.fz ? E.fz + m0 * g.N : g.c, E.fz ? rbytes : 0);
         const __amdgpu_buffer_rsrc_t rd = make_rsrc(E.fdres ? E.fdres + m0 * g.N : g.c, E.fdres ? rbytes : 0);
         const bool relu = __builtin_amdgcn_readfirstlane(E.frelu) != 0;
+        const bool accum = __builtin_amdgcn_readfirstlane(E.facc) != 0;
+        const __amdgpu_buffer_rsrc_t rca = make_rsrc(g.c + m0 * g.N, accum ? rbytes : 0);
         constexpr int WLD = 68;                           // staging row pitch (floats)
         __syncthreads();                                  // every wave's last stage reads are done
         char* const slot0 = (wave % 6 == 0) ? sA0 : (wave % 6 == 1) ? sA1 : (wave % 6 == 2) ? sA2
@@ -3095,11 +3098,13 @@ __global__ __launch_bounds__(512, 1) void x3_gemm256_af_kernel(X3G g) {
                 const int lr = rq + 4 * q;
                 const float4 a = *reinterpret_cast<const float4*>(Tw + lr * WLD + c4 * 4);
                 const uint32_t off = ((uint32_t)(wm * 128 + i * 32 + lr) * (uint32_t)g.N + (uint32_t)col) * 4u;
-                const float4 y4 = bload4(ry, off), z4 = bload4(rzz, off);
+                const float4 y4 = bload4(ry, off), z4 = bload4(rzz, off), c4v = bload4(rca, off);
                 float gv[4], d[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    gv[e] = (relu && !(f4get(y4, e) > 0.f)) ? 0.f : f4get(a, e);
+                    // the implicit GEMM's accumulate (C += conv^T dz): one fp32 add, then the mask
+                    const float t = accum ? f4get(a, e) + f4get(c4v, e) : f4get(a, e);
+                    gv[e] = (relu && !(f4get(y4, e) > 0.f)) ? 0.f : t;
                     d[e] = gv[e] * sc[e];
                     sp[e] += gv[e];
                     sx[e] += gv[e] * ((f4get(z4, e) - mu[e]) * rs[e]);
@@ -4553,9 +4558,9 @@ extern "C" int m3d_conv3d_bwd_data_x3(const float* dz, const uint16_t* planes, i
 // x (m3d_conv3d_bwd_data_bn's contract, accumulate 0): the GEMM's epilogue
 // applies it to each element (dz into dx, dpre into bn->dres) and writes the
 // channel sums of each 128-row half tile; bn_sums_reduce folds them in row order.
-extern "C" int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W,
-                                         int64_t D, int64_t Cin, int64_t Cout, float* dx, const m3d_bn_bwd_t* bn,
-                                         void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s) {
+static int bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
+                          int64_t Cin, int64_t Cout, float* dx, int32_t accumulate, const m3d_bn_bwd_t* bn,
+                          void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s) {
     if (B <= 0 || H <= 0 || W <= 0 || D <= 0) return einval("conv3d x3: tensor dimensions must be positive");
     const int64_t M = B * H * W * D;
     if (Cout % 32 || Cin % 256) return einval("conv1 x3: K must be a multiple of 32 and N of 256");
@@ -4574,12 +4579,25 @@ extern "C" int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes
     q.ep.on = 2;
     q.ep.fy = e.fy; q.ep.fz = e.fz; q.ep.fscale = e.fscale; q.ep.fmean = e.fmean; q.ep.frstd = e.frstd;
     q.ep.fdres = e.fdres; q.ep.fpart = e.fpart; q.ep.fprows = rows; q.ep.frelu = e.frelu;
+    q.ep.facc = accumulate ? 1 : 0;
     const int64_t t256 = (rows / 2) * (Cin / 256);
     const dim3 grid((unsigned)(t256 < 65536 ? t256 : 65536), (unsigned)((t256 + 65535) / 65536));
     hipLaunchKernelGGL(x3_gemm256_af_kernel<2>, grid, dim3(512), 0, st(s), q);
     rc = check_launch("x3_gemm256_af_kernel(conv1 bwd-data, fused BN backward)");
     if (rc || !e.fpart) return rc;
     return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, st(s));
+}
+
+extern "C" int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W,
+                                         int64_t D, int64_t Cin, int64_t Cout, float* dx, const m3d_bn_bwd_t* bn,
+                                         void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s) {
+    return bwd_data_x3_bn(dz, planes, B, H, W, D, Cin, Cout, dx, 0, bn, bn_ws, bn_ws_bytes, s);
+}
+
+extern "C" int m3d_conv3d_bwd_data_x3_bna(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W,
+                                          int64_t D, int64_t Cin, int64_t Cout, float* dx, int32_t accumulate,
+                                          const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s) {
+    return bwd_data_x3_bn(dz, planes, B, H, W, D, Cin, Cout, dx, accumulate, bn, bn_ws, bn_ws_bytes, s);
 }
 
 extern "C" size_t m3d_conv3d_wino_u_bytes(int64_t B, int64_t H, int64_t W, int64_t OD, int64_t Cin) {

@@ -81,6 +81,8 @@ _SIGS = {
                           c_p, c_p, c_p],
     "m3d_conv3d_bwd_data_x3": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_conv3d_bwd_data_x3_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_x3_bna": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p, c_sz,
+                                   c_p],
     "m3d_conv3d_fwd_wino_v": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p,
                               c_i32, c_p, c_p, c_p, c_sz, c_i32, c_p],
     "m3d_conv3d_bwd_data_wino_v": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p,

@@ -205,6 +205,13 @@ def _log(kind, direct_flops, exec_flops, nbytes, phase="fwd", name="", t0=None, 
                           engine))
 
 
+# (2,2,1)-strided 1x1x1 convs' weight gradients (the stage-first blocks' 2a and
+# shortcut) as subsample + the stride-1 split-GEMM gradient instead of the f32
+# implicit-GEMM gradient (round 6; same box: 256^3 146.35 -> 145.93 ms, 128^3
+# 23.89 vs 23.94 ms, profiles/r06_wgrad1_strided_ab.txt)
+WGRAD1_STRIDED_X3 = True
+
+
 def _wgrad1_x3(geo, cin, cout, in_sp):
     """Does m3d_conv3d_bwd_weight run this conv's weight gradient on the x3
     GEMM?  (1x1x1 stride-1 convs with Cin % 4 == 0 and Cout >= 65:
@@ -316,9 +323,17 @@ CONV1_X3_FWD_TILES = 128
 CONV1_X3_DGRAD_TILES = 256
 CONV1_X3_MIN_K = 32             # forward; round 4: 256 (and 256 tiles)
 CONV1_X3_DGRAD_MIN_K = 256
+# the data gradient with the producer's BN-ReLU backward fused into the split
+# GEMM (m3d_conv3d_bwd_data_x3_bna): its own K floor, and whether it also takes
+# the accumulating (identity blocks' 2a) gradients.  Round 6 A/B of K >= 32 with
+# accumulate against the round-5 rule (K >= 256, no accumulate), same box
+# (scripts/r06/gpu_bna.sh, profiles/r06_x3_bna_ab.txt): 128^3 24.58 vs 24.50 ms,
+# 256^3 148.4 vs 148.9 ms -- neutral, so the round-5 rule stays.
+CONV1_X3_DGRAD_FUSED_MIN_K = 256
+X3_BN_FUSE_ACC = False
 
 
-def _conv1_x3(xshape, geo, K, N, bwd_data=False):
+def _conv1_x3(xshape, geo, K, N, bwd_data=False, fused=False):
     """Run a 1x1x1 stride-1 conv (forward: K = Cin, N = Cout; data gradient:
     K = Cout, N = Cin) as one GEMM on the exact bf16 split (m3d_conv3d_fwd_x3 /
     _bwd_data_x3)?  When N is a multiple of 256 and its 256x256 tiles number
@@ -328,7 +343,8 @@ def _conv1_x3(xshape, geo, K, N, bwd_data=False):
     if not CONV1_X3 or geo.k != (1, 1, 1) or geo.stride != (1, 1, 1) or geo.pad != (0, 0, 0):
         return False
     B, H, W, D = xshape[:4]
-    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < (CONV1_X3_DGRAD_MIN_K if bwd_data else CONV1_X3_MIN_K):
+    kmin = (CONV1_X3_DGRAD_FUSED_MIN_K if fused else CONV1_X3_DGRAD_MIN_K) if bwd_data else CONV1_X3_MIN_K
+    if tuple(geo.out) != (H, W, D) or K % 32 or N % 256 or K < kmin:
         return False
     sg = slab.current()
     Dg = sg.D if sg is not None else D
@@ -913,7 +929,8 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.geo, ctx.relu, ctx.res_mode, ctx.grads, ctx.need_dx = geo, relu, res_mode, grads, need_dx
         # the data gradient's split planes of this forward's refresh (X3Planes), if any
         ctx.x3_bwd = None
-        if geo.k == (1, 1, 1) and need_dx and halo is None and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True):
+        if (geo.k == (1, 1, 1) and need_dx and halo is None
+                and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True, fused=X3_BN_FUSE)):
             ctx.x3_bwd = X3_PLANES.cached(w, False)
             if ctx.x3_bwd is None:
                 X3_PLANES.ensure(w, Cin, Cout)
@@ -1091,6 +1108,10 @@ class _ConvBNAct(torch.autograd.Function):
                     None, None, None, None)
         if halo is not None and ctx.need_dx:
             raise ValueError("the stem's halo form has no data gradient (its input is the volume)")
+        strided_x3 = (WGRAD1_STRIDED_X3 and halo is None and geo.k == (1, 1, 1) and geo.stride == (2, 2, 1)
+                      and geo.pad == (0, 0, 0) and (OH, OW, OD) == ((H + 1) // 2, (W + 1) // 2, D)
+                      and Cin % 4 == 0 and Cout >= 65)      # (_wgrad1_x3 of the stride-1 form)
+
         def wgrad_d():
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 tw = _span()
@@ -1099,6 +1120,15 @@ class _ConvBNAct(torch.autograd.Function):
                                                        ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH, OW, OD,
                                                        *geo.stride, *geo.pad, ptr(grads["kernel"]), stream()),
                           "conv3d_bwd_weight_halo")
+                elif strided_x3:
+                    # the stage-first blocks' (2,2,1)-strided 1x1x1 convs: their input rows
+                    # gathered once (x[:, ::2, ::2]), then the stride-1 split-GEMM gradient
+                    xs = torch.empty((B, OH, OW, OD, Cin), device=x.device, dtype=torch.float32)
+                    check(L.m3d_subsample221_fwd(ptr(x), B, H, W, D, Cin, ptr(xs), stream()), "subsample221")
+                    check(L.m3d_conv3d_bwd_weight(ptr(xs), ptr(dz), B, OH, OW, OD, Cin, 1, 1, 1, Cout, OH, OW, OD,
+                                                  1, 1, 1, 0, 0, 0, ptr(grads["kernel"]), stream()),
+                          "conv3d_bwd_weight")
+                    del xs
                 else:
                     check(L.m3d_conv3d_bwd_weight(ptr(x), ptr(dz), B, H, W, D, Cin, kh, kw, kd, Cout, OH,
                                                   OW, OD, *geo.stride, *geo.pad, ptr(grads["kernel"]),
@@ -1106,7 +1136,7 @@ class _ConvBNAct(torch.autograd.Function):
                 if logging:
                     _log(f"conv{kh}_wgrad", direct, direct, 4.0 * (x.numel() + dz.numel() + w.numel()),
                          "bwd_weight", ctx.name, tw,
-                         "x3" if halo is None and _wgrad1_x3(geo, Cin, Cout, (H, W, D)) else "f32")
+                         "x3" if halo is None and (strided_x3 or _wgrad1_x3(geo, Cin, Cout, (H, W, D))) else "f32")
         has_w = grads.get("kernel") is not None
         if has_w and not WGRAD_LAST:
             wgrad_d()
@@ -1130,15 +1160,18 @@ class _ConvBNAct(torch.autograd.Function):
                 dzd[..., :Cout] = dz
             nsk = _splitk(x.shape, geo, Cin, cpad, 1)
             dx_x3 = cpad == Cout and not acc and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True)
-            if dx_x3 and X3_BN_FUSE and rec is not None and rec.armed and _fuse_final(link, x, acc):
-                # the producer's BN-ReLU backward in the split GEMM's epilogue
+            dx_x3f = (cpad == Cout and X3_BN_FUSE and rec is not None and rec.armed and (X3_BN_FUSE_ACC or not acc)
+                      and _conv1_x3(x.shape, geo, Cout, Cin, bwd_data=True, fused=True))
+            if dx_x3f and _fuse_final(link, x, acc):
+                # the producer's BN-ReLU backward in the split GEMM's epilogue (+ the parked gradient)
+                dx_x3 = True
                 planes = ctx.x3_bwd if ctx.x3_bwd is not None else _x3_planes(w, Cin, Cout, False)
                 dres_f = torch.empty_like(x) if rec.need_res else None
                 bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
                 d = rec.descriptor(dres_f)
-                check(L.m3d_conv3d_bwd_data_x3_bn(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx),
-                                                  ctypes.addressof(d), ptr(bws), bwsb, stream()),
-                      "conv3d_bwd_data_x3_bn")
+                check(L.m3d_conv3d_bwd_data_x3_bna(ptr(dz), ptr(planes), B, H, W, D, Cin, Cout, ptr(dx), acc,
+                                                   ctypes.addressof(d), ptr(bws), bwsb, stream()),
+                      "conv3d_bwd_data_x3_bna")
                 rec.buf, rec.dres, rec.done = dx, dres_f, True
                 fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
             elif dx_x3:

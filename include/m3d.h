@@ -483,6 +483,13 @@ int m3d_conv3d_bwd_data_wino_bny(const float* dz, const float* w, int64_t B, int
 int m3d_conv3d_bwd_data_x3_bn(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
                               int64_t Cin, int64_t Cout, float* dx, const m3d_bn_bwd_t* bn, void* bn_ws,
                               size_t bn_ws_bytes, m3d_stream_t s);
+/* The same with accumulate (the identity blocks' 2a data gradient,
+ * core/models.py:157-189: dx holds the residual's parked gradient, and the
+ * fused epilogue takes t = conv^T(dz) + dx before the BN-ReLU backward, as
+ * m3d_conv3d_bwd_data_bn with accumulate 1). */
+int m3d_conv3d_bwd_data_x3_bna(const float* dz, const uint16_t* planes, int64_t B, int64_t H, int64_t W, int64_t D,
+                               int64_t Cin, int64_t Cout, float* dx, int32_t accumulate, const m3d_bn_bwd_t* bn,
+                               void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s);
 int m3d_conv3d_bwd_data_splitk_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                                   int64_t Cin, int64_t Cout, float* dx, int32_t accumulate, int32_t splits,
                                   void* workspace, size_t ws_bytes, const m3d_bn_bwd_t* bn, void* bn_ws,

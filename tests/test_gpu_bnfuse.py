@@ -73,6 +73,8 @@ CASES = [
     ("x3", 1, 512, 256, 1, 16, 16, 8, 0, True, True, False),         # rpn_conv_shared1 <- shared2 (bf16-split GEMM)
     ("x3", 1, 256, 512, 1, 10, 6, 9, 0, True, True, True),           # ragged last 256-row tile, dres
     ("x3", 1, 768, 1024, 2, 8, 8, 8, 0, False, False, True),         # no ReLU / gamma sum, 3 N-tiles
+    ("x3", 1, 256, 64, 1, 16, 16, 8, 1, True, True, True),           # identity 2a: K = 64, accumulated (_bna)
+    ("x3", 1, 512, 128, 1, 10, 6, 9, 1, True, True, False),          # ragged last tile, accumulated
 ]
 
 
@@ -124,14 +126,21 @@ def test_fused_matches_unfused(cuda, alg, k, cin, cout, B, H, W, D, acc, relu, w
         _lib.check(L.m3d_conv1_x3_planes(w.data_ptr(), cin, cout, 0, planes.data_ptr(), st), "planes")
 
         def conv(dx, a):
-            assert a == 0
+            # accumulate: the split GEMM into a temporary, then dx + t (one fp32 add,
+            # the fused epilogue's t = acc + dx: IEEE addition commutes bit for bit)
+            t = torch.empty_like(dx) if a else dx
             _lib.check(L.m3d_conv3d_bwd_data_x3(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
-                                                dx.data_ptr(), st), "dgrad x3")
+                                                t.data_ptr(), st), "dgrad x3")
+            if a:
+                dx.add_(t)
 
         def conv_bn(dx, a, d, bws, bwsb):
-            assert a == 0
-            _lib.check(L.m3d_conv3d_bwd_data_x3_bn(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
-                                                   dx.data_ptr(), d, bws, bwsb, st), "dgrad x3 bn")
+            if a:
+                _lib.check(L.m3d_conv3d_bwd_data_x3_bna(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
+                                                        dx.data_ptr(), a, d, bws, bwsb, st), "dgrad x3 bna")
+            else:
+                _lib.check(L.m3d_conv3d_bwd_data_x3_bn(dz_in.data_ptr(), planes.data_ptr(), B, H, W, D, cin, cout,
+                                                       dx.data_ptr(), d, bws, bwsb, st), "dgrad x3 bn")
     else:
         def conv(dx, a):
             _lib.check(L.m3d_conv3d_bwd_data(dz_in.data_ptr(), w.data_ptr(), B, H, W, D, cin, k, k, k, cout, H, W,
