@@ -1727,22 +1727,30 @@ __global__ __launch_bounds__(512, 1) void x3_wgrad_tr_kernel(const float* __rest
                                                              int64_t bsb, int64_t bsc, WgOut wo, X3wSK sk) {
     __shared__ __attribute__((aligned(16))) char smem[2 * W2_STAGE];
     if constexpr (SK) {
-        // XCD-contiguous: the workgroups of one XCD take consecutive unit ranges
+        // XCD-contiguous: the workgroups of one XCD take consecutive unit ranges.
+        // The tn column tiles of one (batch, k tile) share their A rows, so they
+        // run in lockstep: workgroups form groups of tn adjacent ones, a group
+        // walks one range of (batch, k tile, step) units and member j takes
+        // column tile j of each.  (Ranges over whole tiles drifted the partner
+        // tiles' steps apart -- 288 steps per workgroup against 256 per tile --
+        // and every A row was fetched from HBM twice: PMC 2.55 vs 1.89 GB.)
         const int64_t G = gridDim.x, L = blockIdx.x;
         const int64_t xcd = L % 8, q8 = G / 8, r8 = G % 8;
         const int64_t g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
-        int64_t u = g * sk.units / G;
-        const int64_t ue = (g + 1) * sk.units / G;
-        const int64_t tpb = (int64_t)sk.tk * sk.tn;
+        const int64_t Gg = G / sk.tn, grp = g / sk.tn;
+        const int nj = (int)(g - grp * sk.tn);
+        const int64_t ug = sk.units / sk.tn;              // (batch, k tile, step) units
+        int64_t u = grp * ug / Gg;
+        const int64_t ue = (grp + 1) * ug / Gg;
         while (u < ue) {
-            const int64_t t = u / sk.nk;
+            const int64_t t = u / sk.nk;                  // batch * tk + k tile
             const int64_t s0 = u - t * sk.nk;
             const int64_t s1 = s0 + (ue - u) < sk.nk ? s0 + (ue - u) : sk.nk;
-            const int64_t batch = t / tpb;
-            const int r = (int)(t - batch * tpb);
+            const int64_t batch = t / sk.tk;
+            const int kt = (int)(t - batch * sk.tk);
             const int64_t me = s1 * W2_BK < M ? s1 * W2_BK : M;
             x3w_segment<DBG>(smem, A + batch * bsa, Bm + batch * bsb, C + batch * bsc, M, K, N, s0 * W2_BK, me,
-                             (r % sk.tk) * 256, (r / sk.tk) * 256, wo, nullptr, 0);
+                             kt * 256, nj * 256, wo, nullptr, 0);
             u += s1 - s0;
         }
         return;
@@ -1787,7 +1795,8 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
         const int64_t min_steps = (minm + W2_BK - 1) / W2_BK;
         int64_t G = (sk.units + min_steps - 1) / min_steps;
         if (G > cus) G = cus;
-        if (G < 1) G = 1;
+        G = G / sk.tn * sk.tn;                        // whole groups of the tn column tiles
+        if (G < sk.tn) G = sk.tn;
         hipLaunchKernelGGL((x3_wgrad_tr_kernel<0, true>), dim3((unsigned)G), dim3(512), 0, s, A, Bm, C, M, K, N,
                            (int64_t)0, bsa, bsb, bsc, WgOut{nullptr, 0, 0}, sk);
         return;
