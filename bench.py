@@ -81,7 +81,9 @@ def log(*a):
 # ---------------------------------------------------------------- dominant kernel
 def _event_time(fn, reps):
     """Average seconds per call of fn(), HIP events on torch's current stream
-    (the stream every libm3d launch of fn() is enqueued on)."""
+    (the stream every libm3d launch of fn() is enqueued on).  The priced GEMM
+    legs take 20 launches, as their rocprofv3 runs (scripts/kernels_for_pmc.py)
+    do: with 5 the average sat 5-9 % above rocprof's on the same box."""
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -133,7 +135,7 @@ def wino_gemm_shape(S):
     return (ny + 2) * 4 * (nz + 2), T, 256, 512
 
 
-def time_wino_gemm(S, reps=5):
+def time_wino_gemm(S, reps=20):
     """The Winograd point GEMMs of rpn_conv_shared1 on P2 in the form the step
     runs them (M3D_GEMM_X3 bit 4): U in fp32 split inside x3_gemm256_af_kernel,
     the weight planes split once, untimed, as the weight transform does in the
@@ -168,7 +170,7 @@ def time_wino_gemm(S, reps=5):
             "direct_conv_equivalent_tflops": round(2.0 * (S // 4) ** 2 * S * 27 * K * N / t / 1e12, 2)}
 
 
-def time_wgrad_gemm(S, reps=5):
+def time_wgrad_gemm(S, reps=20):
     """The Winograd weight-gradient GEMMs of rpn_conv_shared1 on P2 through
     m3d_gemm_wgrad_f32 (x3_wgrad_tr_kernel by default)."""
     from m3d import _lib
