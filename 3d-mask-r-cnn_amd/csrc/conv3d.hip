@@ -4620,7 +4620,7 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
                     const float* bn_scale, const float* bn_shift, const float* residual,
                     int32_t relu, float* z_out, float* y, float* u_keep, void* workspace,
                     size_t ws_bytes, hipStream_t s, const float* halo = nullptr, int hlo = 0, int hhi = 0,
-                    bool v_ready = false, int phase = 0) {
+                    bool v_ready = false, int phase = 0, const void* v_ext = nullptr) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (ws_bytes < m3d_conv3d_wino_workspace_bytes(B, H, W, D, OD, Cin, Cout))
@@ -4634,7 +4634,7 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
             rc = fwd_wino(x + b * H * W * D * Cin, 1, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift,
                           residual ? residual + b * os : nullptr, relu, z_out ? z_out + b * os : nullptr, y + b * os,
                           nullptr, workspace, ws_bytes, s, halo ? halo + b * H * W * 2 * Cin : nullptr, hlo, hhi,
-                          v_ready || b > 0);
+                          v_ready || b > 0, 0, v_ext);
             if (rc) return rc;
         }
         return M3D_OK;
@@ -4653,8 +4653,9 @@ static int fwd_wino(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, 
     if (gemm_x3_env() && (!u_keep || x3_af32_env())) {
         // (the fp32-A GEMM reads U in fp32: a kept U is written in place for the weight gradient)
         if (u_keep) ws.U = u_keep;
+        if (v_ext) ws.V = static_cast<float*>(const_cast<void*>(v_ext));   // transformed by m3d_conv3d_wino_weight_v
         float* wt = ws.WT;
-        if (!v_ready && phase != 2) {     // v_ready: V already holds this w's transform (an earlier call, same workspace)
+        if (!v_ready && !v_ext && phase != 2) {   // v_ready: V already holds this w's transform (an earlier call, same workspace)
             hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
                                dim3(256), 0, s, w, (int)Cin, (int)Cout, wt);
             WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, dim3(grid_for(Cin * Cout, 256)), dim3(256), 0, s, wt,
@@ -4726,7 +4727,8 @@ extern "C" int m3d_conv3d_fwd_wino_keep(const float* x, int64_t B, int64_t H, in
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t s, float* dx_halo = nullptr,
-                         int hlo = 0, bool v_ready = false, const Epi* fb = nullptr, int ny = 0);
+                         int hlo = 0, bool v_ready = false, const Epi* fb = nullptr, int ny = 0,
+                         const void* v_ext = nullptr);
 
 // The same two entry points for convs that share one kernel across calls (the
 // RPN head's rpn_conv_shared1 on P2..P6, core/models.py:512-557): with
@@ -4779,7 +4781,7 @@ extern "C" int m3d_conv3d_bwd_data_wino(const float* dz, const float* w, int64_t
 static int bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                             int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                             void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn, void* bn_ws,
-                            size_t bn_ws_bytes, int ny, hipStream_t hs) {
+                            size_t bn_ws_bytes, int ny, hipStream_t hs, const void* v_ext = nullptr) {
     if (Cin % 256 != 0 && 256 % Cin != 0)
         return einval("conv3d winograd bwd-data (fused BN backward): Cin must divide 256 or be a multiple of it");
     if (wino_per_item(B, H, W, D, OD, Cin, Cout))
@@ -4790,7 +4792,7 @@ static int bwd_data_wino_bn(const float* dz, const float* w, int64_t B, int64_t 
     int rc = bn_fuse_epi(bn, Cin, bn_ws, bn_ws_bytes, rows, e);
     if (rc) return rc;
     rc = bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, hs, nullptr, 0,
-                       v_ready != 0, &e, ny);
+                       v_ready != 0, &e, ny, v_ext);
     if (rc) return rc;
     return bn_sums_reduce(e.fpart, rows, Cin, bn->sum_dpre, bn->sum_dpre_xhat, bn->sum_dz, hs);
 }
@@ -4814,6 +4816,80 @@ extern "C" int m3d_conv3d_bwd_data_wino_bny(const float* dz, const float* w, int
     if (rc) return rc;
     return bwd_data_wino_bn(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, v_ready, bn,
                             bn_ws, bn_ws_bytes, ny, st(s));
+}
+
+// ---- Winograd weight transforms into caller memory ----------------------------
+// The transformed weights depend only on w, so a caller can produce them ahead
+// of the convs (e.g. on a side stream at the start of a model's forward) and
+// hand them to m3d_conv3d_fwd_wino_kv / m3d_conv3d_bwd_data_wino_xv.  Layout:
+// the bf16-split planes the point GEMMs read, [3][points][n'][k'] uint16, at
+// offset 0; the forward's form also uses a 27*Cin*Cout fp32 scratch behind them
+// (the transposed weights, x3_wt_kernel).
+static size_t wino_v_planes_bytes(int64_t Cin, int64_t Cout, int dgrad, int ny) {
+    const int P = dgrad ? wino_points(wino_dgrad_nz(), ny) : wino_points();
+    return (6 * (size_t)P * (size_t)Cin * (size_t)Cout + 255) & ~(size_t)255;
+}
+static int wino_v_tile(int32_t dgrad, int32_t tile_y, int& ny) {
+    if (!gemm_x3_env()) return einval("conv3d winograd: external transformed weights need the bf16-split GEMMs");
+    if (dgrad) return dgrad_tile_arg(tile_y, ny);
+    ny = WNY;
+    return M3D_OK;
+}
+extern "C" size_t m3d_conv3d_wino_v_bytes(int64_t Cin, int64_t Cout, int32_t dgrad, int32_t tile_y) {
+    int ny;
+    if (Cin <= 0 || Cout <= 0 || wino_v_tile(dgrad, tile_y, ny)) return 0;
+    return wino_v_planes_bytes(Cin, Cout, dgrad, ny) + (dgrad ? 0 : sizeof(float) * 27 * (size_t)Cin * Cout);
+}
+extern "C" int m3d_conv3d_wino_weight_v(const float* w, int64_t Cin, int64_t Cout, int32_t dgrad, int32_t tile_y,
+                                        void* v, size_t v_bytes, m3d_stream_t s) {
+    int ny;
+    if (Cin <= 0 || Cout <= 0) return einval("conv3d winograd: channel counts must be positive");
+    if (int rc = wino_v_tile(dgrad, tile_y, ny)) return rc;
+    if (!w || !v || v_bytes < m3d_conv3d_wino_v_bytes(Cin, Cout, dgrad, tile_y))
+        return einval("conv3d winograd: transformed-weight buffer missing or too small (m3d_conv3d_wino_v_bytes)");
+    const dim3 grid(grid_for(Cin * Cout, 256));
+    if (!dgrad) {
+        float* wt = reinterpret_cast<float*>(static_cast<char*>(v) + wino_v_planes_bytes(Cin, Cout, 0, ny));
+        hipLaunchKernelGGL(x3_wt_kernel, dim3((unsigned)((Cout + 31) / 32), (unsigned)((Cin + 31) / 32), 27),
+                           dim3(256), 0, st(s), w, (int)Cin, (int)Cout, wt);
+        WINO_LAUNCH_NZ_X3(wino_nz(), wino_weight_kernel, grid, dim3(256), 0, st(s), wt, (int)Cin, (int)Cout, 0,
+                          static_cast<float*>(v));
+        return check_launch("conv3d winograd weight transform (fwd)");
+    }
+    const int nz = wino_dgrad_nz();
+    float* V = static_cast<float*>(v);
+    if (nz == 4 && ny == 4) hipLaunchKernelGGL((wino_weight_kernel<4, true, 4>), grid, dim3(256), 0, st(s), w, (int)Cin, (int)Cout, 1, V);
+    else if (nz == 4) hipLaunchKernelGGL((wino_weight_kernel<4, true, 2>), grid, dim3(256), 0, st(s), w, (int)Cin, (int)Cout, 1, V);
+    else if (ny == 4) hipLaunchKernelGGL((wino_weight_kernel<2, true, 4>), grid, dim3(256), 0, st(s), w, (int)Cin, (int)Cout, 1, V);
+    else hipLaunchKernelGGL((wino_weight_kernel<2, true, 2>), grid, dim3(256), 0, st(s), w, (int)Cin, (int)Cout, 1, V);
+    return check_launch("conv3d winograd weight transform (dgrad)");
+}
+extern "C" int m3d_conv3d_fwd_wino_kv(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin,
+                                      const float* w, int64_t Cout, int64_t OD, int32_t pz, const float* bias,
+                                      const float* bn_scale, const float* bn_shift, const float* residual,
+                                      int32_t relu, float* z_out, float* y, float* u_keep, const void* v,
+                                      void* workspace, size_t ws_bytes, m3d_stream_t s) {
+    int ny;
+    if (int rc = wino_v_tile(0, 0, ny)) return rc;
+    if (!v) return einval("conv3d winograd: v must not be NULL (m3d_conv3d_wino_weight_v)");
+    if (u_keep && wino_nz() != wino_wgrad_nz())
+        return einval("conv3d winograd: forward and weight-gradient tiles differ (m3d_conv3d_wino_u_bytes == 0)");
+    return fwd_wino(x, B, H, W, D, Cin, w, Cout, OD, pz, bias, bn_scale, bn_shift, residual, relu, z_out, y, u_keep,
+                    workspace, ws_bytes, st(s), nullptr, 0, 0, false, 0, v);
+}
+extern "C" int m3d_conv3d_bwd_data_wino_xv(const float* dz, const float* w, int64_t B, int64_t H, int64_t W,
+                                           int64_t D, int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx,
+                                           int32_t accumulate, void* workspace, size_t ws_bytes, const void* v,
+                                           int32_t tile_y, const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes,
+                                           m3d_stream_t s) {
+    int ny;
+    if (int rc = wino_v_tile(1, tile_y, ny)) return rc;
+    if (!v) return einval("conv3d winograd bwd-data: v must not be NULL (m3d_conv3d_wino_weight_v)");
+    if (bn)
+        return bwd_data_wino_bn(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, 0, bn, bn_ws,
+                                bn_ws_bytes, ny, st(s), v);
+    return bwd_data_wino(dz, w, B, H, W, D, Cin, Cout, OD, pz, dx, accumulate, workspace, ws_bytes, st(s), nullptr, 0,
+                         false, nullptr, ny, v);
 }
 
 // the data-gradient output transform: dx over the (halo-extended) grid, or,
@@ -4869,7 +4945,7 @@ static void bwd_data_wino_launch(const float* dz, const float* w, const WinoGeom
 static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
                          int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                          void* workspace, size_t ws_bytes, hipStream_t hs, float* dx_halo, int hlo, bool v_ready,
-                         const Epi* fb, int ny_arg) {
+                         const Epi* fb, int ny_arg, const void* v_ext) {
     int rc = wino_check(B, H, W, D, OD, pz, Cin, Cout);
     if (rc) return rc;
     if (wino_per_item(B, H, W, D, OD, Cin, Cout)) {
@@ -4878,7 +4954,7 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
             rc = bwd_data_wino(dz + b * H * W * OD * Cout, w, 1, H, W, D, Cin, Cout, OD, pz, dx + b * H * W * dxd * Cin,
                                accumulate, workspace, ws_bytes, hs,
                                dx_halo ? dx_halo + b * H * W * 2 * Cin : nullptr, hlo, v_ready || b > 0, nullptr,
-                               ny_arg);
+                               ny_arg, v_ext);
             if (rc) return rc;
         }
         return M3D_OK;
@@ -4889,7 +4965,11 @@ static int bwd_data_wino(const float* dz, const float* w, int64_t B, int64_t H, 
     if (ws_bytes < wino_ws_need(g, Cout, Cin, nz, ny))
         return einval("conv3d winograd: workspace too small");
     // same layout with the roles of Cin/Cout swapped (V'[P][Cout][Cin], U'[P][T][Cout])
-    const WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz, ny);
+    WinoWs ws = wino_ws(workspace, g, Cout, Cin, nz, ny);
+    if (v_ext) {                        // transformed by m3d_conv3d_wino_weight_v (dgrad 1, this tile_y)
+        ws.V = static_cast<float*>(const_cast<void*>(v_ext));
+        v_ready = true;
+    }
     const int ci = (int)Cin, co = (int)Cout, dl = (int)OD;
     if (nz == 4 && ny == 4)
         bwd_data_wino_launch<4, 4>(dz, w, g, ws, ci, co, dx, accumulate, dx_halo, hlo, dl, v_ready, fb, hs);

@@ -81,6 +81,12 @@ _SIGS = {
                           c_p, c_p, c_p],
     "m3d_conv3d_bwd_data_x3": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
     "m3d_conv3d_bwd_data_x3_bn": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_wino_v_bytes": [c_i64, c_i64, c_i32, c_i32],
+    "m3d_conv3d_wino_weight_v": [c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_sz, c_p],
+    "m3d_conv3d_fwd_wino_kv": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p,
+                               c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p],
+    "m3d_conv3d_bwd_data_wino_xv": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32,
+                                    c_p, c_sz, c_p, c_i32, c_p, c_p, c_sz, c_p],
     "m3d_conv3d_bwd_data_x3_bna": [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p, c_sz,
                                    c_p],
     "m3d_conv3d_fwd_wino_v": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p,
@@ -198,7 +204,7 @@ _RESTYPES = {"m3d_last_error": ctypes.c_char_p, "m3d_nms3d_workspace_bytes": c_s
              "m3d_pyramid_roi_align3d_fwd_workspace_bytes": c_sz,
              "m3d_detection_targets_workspace_bytes": c_sz, "m3d_rpn_targets_workspace_bytes": c_sz,
              "m3d_rpn_loss_workspace_bytes": c_sz,
-             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz, "m3d_conv3d_wino_dgrad_workspace_bytes": c_sz,
+             "m3d_bn_act_bwd_workspace_bytes": c_sz, "m3d_bn_bwd_fused_workspace_bytes": c_sz, "m3d_conv3d_splitk_count": c_i32, "m3d_conv3d_wino_workspace_bytes": c_sz, "m3d_conv3d_wino_dgrad_workspace_bytes": c_sz, "m3d_conv3d_wino_v_bytes": c_sz,
              "m3d_conv3d_wino_u_bytes": c_sz, "m3d_conv3d_wino_tile_z": c_i32, "m3d_conv3d_wino_wgrad_tile_z": c_i32,
              "m3d_conv3d_wino_tile_y": c_i32, "m3d_conv3d_wino_dgrad_tile_y": c_i32,
              "m3d_conv3d_wino_dgrad_tile_z": c_i32, "m3d_col_sums_batched_workspace_bytes": c_sz}

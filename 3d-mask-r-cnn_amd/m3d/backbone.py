@@ -219,11 +219,12 @@ class RPNHead:
     def finish_backward(self):
         """Join the side-stream weight gradients (m3d.nn.join_wgrad) and fold the
         padded combined-head gradients into rpn_class_raw / rpn_bbox_pred."""
-        from .nn import check_fuses, check_links, join_wgrad
+        from .nn import WINO_V, check_fuses, check_links, join_wgrad
         batch, self.bias_batch = getattr(self, "bias_batch", None), None
         if batch is not None:
             batch.flush()          # the batched bias gradients (nn.BiasSums), on the compute stream
         join_wgrad()
+        WINO_V.join()              # the Winograd weight pre-pass's side stream (nn.WinoVPrep)
         check_fuses(self.fuse_records)
         if self.backbone is not None:
             check_links(self.backbone.links)

@@ -467,6 +467,100 @@ X3_PLANES_BATCHED = True
 X3_PLANES = X3Planes()
 
 
+class WinoVPrep:
+    """The Winograd-domain weights of every 3x3x3 conv (the forward's and the
+    data gradient's transform, m3d_conv3d_wino_weight_v), produced at the start
+    of each model forward on a side stream instead of inside each conv on the
+    compute stream.  They depend on the kernel only, so the ~75 small transform
+    launches of a step (x3_wt_kernel + wino_weight_kernel per conv and data
+    gradient) leave the critical path and overlap the stem / early layers.
+
+    Registration and lifetime follow X3Planes: a conv registers its kernel (and
+    the data-gradient tile it will use) the first time it runs, transforming
+    inline that time; each RPN.forward refreshes every registered kernel
+    (``refresh``: the side stream first waits for the compute stream, so the
+    previous step's optimizer update and data gradients are ordered before the
+    overwrite) and the convs of that forward take the buffers while ``live``,
+    each after waiting for its own entry's event.  A unit's forward hands the
+    data-gradient buffer, its event and the refresh generation to its backward
+    (checked: a backward after another forward raises).  Buffers persist per
+    kernel (~3 GB for the RPN's 3x3x3 convs)."""
+
+    def __init__(self):
+        self.entries = {}            # key -> [weakref(w), cin, cout, dgrad, ty, buf, nbytes, event, valid]
+        self.live = False
+        self.active = False          # this forward registers / takes (RPN.forward: volumes >= WINO_V_PREPASS_MIN_VOXELS)
+        self.gen = 0
+        self.streams = {}
+        self.pending = set()         # devices whose pre-pass stream the next join() waits for
+
+    def refresh(self, dev):
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.device(dev).index is None \
+            else torch.device(dev)
+        for k in [k for k, e in self.entries.items() if e[0]() is None]:
+            del self.entries[k]
+        es = [e for e in self.entries.values() if e[0]().device == dev]
+        if not es:
+            self.live = True
+            return
+        side = self.streams.get(dev)
+        if side is None:
+            side = self.streams[dev] = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        L = _L()
+        with torch.cuda.stream(side):
+            for e in es:
+                check(L.m3d_conv3d_wino_weight_v(ptr(e[0]()), e[1], e[2], e[3], e[4], ptr(e[5]), e[6], stream()),
+                      "conv3d_wino_weight_v")
+                e[7].record(side)
+                e[8] = True
+        self.pending.add(dev)
+        self.gen += 1
+        self.live = True
+
+    def invalidate(self):
+        self.live = False
+
+    def join(self):
+        """The compute stream waits for the pre-pass stream (every entry a
+        backward did not take is then ordered too; a HIP-graph capture needs the
+        side stream joined before it ends)."""
+        for dev in self.pending:
+            torch.cuda.current_stream(dev).wait_stream(self.streams[dev])
+        self.pending = set()
+
+    def ensure(self, w, cin, cout, dgrad, ty):
+        key = (w.data_ptr(), w.numel(), dgrad, ty)
+        e = self.entries.get(key)
+        if (e is None or e[0]() is None) and not torch.cuda.is_current_stream_capturing():
+            nb = int(_L().m3d_conv3d_wino_v_bytes(cin, cout, dgrad, ty))
+            if nb > 0:
+                self.entries[key] = [weakref.ref(w), cin, cout, dgrad, ty,
+                                     torch.empty(nb // 4 + 1, device=w.device, dtype=torch.float32), nb,
+                                     torch.cuda.Event(), False]
+
+    def take(self, w, dgrad, ty):
+        """(buffer, event, gen) of w's refreshed transform, None when not live /
+        not registered yet.  The caller waits on the event before using it."""
+        if not self.live:
+            return None
+        e = self.entries.get((w.data_ptr(), w.numel(), dgrad, ty))
+        if e is None or not e[8] or e[0]() is None:
+            return None
+        return e[5], e[7], self.gen
+
+
+# (the RPN's) Winograd weight transforms on a side stream at the start of the
+# forward, for volumes of at least WINO_V_PREPASS_MIN_VOXELS voxels.  Same box
+# (scripts/r06/gpu_prepass.sh, gpu_prepass256.sh, profiles/r06_wino_prepass_ab.txt):
+# 128^3 graph step 24.52 -> 24.25 ms, 256^3 147.4 -> 146.9 ms; at 64^3 the
+# replay is slower (9.92 -> 10.40 ms: the fast forward catches up with the side
+# stream and waits on every layer's event), so small volumes transform inline.
+WINO_V_PREPASS = True
+WINO_V_PREPASS_MIN_VOXELS = 128 ** 3
+WINO_V = WinoVPrep()
+
+
 def _x3_planes(w, cin, cout, transpose):
     return X3_PLANES.get(w, cin, cout, transpose)
 
@@ -844,6 +938,7 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.bn = None
             ctx.aff_gen = None
         ctx.wino = use_winograd(geo, Cin, Cout, (H, W, D)) and res_mode != 2
+        ctx.vd = None
         if halo is not None and not ctx.wino and not _stem_halo(geo, Cin, Cout, res_mode):
             raise ValueError("halo planes are read by the Winograd kernels and the stem only")
         ctx.u = None
@@ -864,6 +959,17 @@ class _ConvBNAct(torch.autograd.Function):
                 and min(Cin, Cout) >= WINO_WGRAD_MIN_C else 0
             if nu * 4 > WINO_KEEP_MAX_BYTES:
                 nu = 0          # too large to hold until the backward: the weight gradient re-transforms x
+            vf = None
+            ctx.vd = None
+            if WINO_V_PREPASS and WINO_V.active and halo is None:
+                ty = _dgrad_tile_y(name)
+                WINO_V.ensure(w, Cin, Cout, 0, 0)
+                if need_dx:
+                    WINO_V.ensure(w, Cin, Cout, 1, ty)
+                vf = WINO_V.take(w, 0, 0)
+                if vf is not None:
+                    torch.cuda.current_stream().wait_event(vf[1])
+                    ctx.vd = WINO_V.take(w, 1, ty) if need_dx else None
             if pending is not None:
                 # phase 1 (weights + interior z tiles) overlaps the halo transfer
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
@@ -880,6 +986,13 @@ class _ConvBNAct(torch.autograd.Function):
                                                     ptr(w), Cout, ptr(b), ptr(scale), ptr(shift), ptr(residual),
                                                     1 if relu else 0, ptr(z), ptr(y), ptr(ctx.u), ptr(ws), wsb,
                                                     stream()), "conv3d_fwd_wino_halo")
+            elif vf is not None:
+                # the transformed weights from this forward's side-stream pre-pass (WinoVPrep)
+                ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None
+                check(_L().m3d_conv3d_fwd_wino_kv(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
+                                                  ptr(b), ptr(scale), ptr(shift), ptr(residual), 1 if relu else 0,
+                                                  ptr(z), ptr(y), ptr(ctx.u), ptr(vf[0]), ptr(ws), wsb, stream()),
+                      "conv3d_fwd_wino_kv")
             elif nu > 0:
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32)
                 check(_L().m3d_conv3d_fwd_wino_keep(ptr(x), B, H, W, D, Cin, ptr(w), Cout, OD, geo.pad[2],
@@ -1073,9 +1186,18 @@ class _ConvBNAct(torch.autograd.Function):
                           "conv3d_bwd_data_wino_halo")
                     slab.return_halo_grads(dx, dh)
                 else:
-                    if ctx.wshare is not None:      # may be held across calls: not the arena
-                        ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
-                    ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout, ty))
+                    vd = ctx.vd                     # the forward pre-pass's data-gradient transform (WinoVPrep)
+                    if vd is not None:
+                        if vd[2] != WINO_V.gen:
+                            raise RuntimeError(f"{ctx.name}: conv backward after another model forward: the "
+                                               "pre-transformed Winograd weights were refreshed (run each backward "
+                                               "before the next forward)")
+                        torch.cuda.current_stream().wait_event(vd[1])
+                        v_ready = 0
+                    else:
+                        if ctx.wshare is not None:      # may be held across calls: not the arena
+                            ws, wsb = _wino_ws(B, H, W, dext, OD, Cin, Cout, x.device, dedicated=True)
+                        ws, wsb, v_ready = _shared_wino_ws(ctx.wshare, "bwd", ws, wsb, (w.data_ptr(), Cin, Cout, ty))
                     rec = ctx.fuse_in
                     if (rec is not None and rec.armed and (Cin % 256 == 0 or 256 % Cin == 0)
                             and not _per_item(B, H * W * max(D, OD), max(Cin, Cout), 0, 0)
@@ -1083,11 +1205,22 @@ class _ConvBNAct(torch.autograd.Function):
                         dres_f = torch.empty_like(x) if rec.need_res else None
                         bws, bwsb = _bn_fuse_ws(rec, B, H, W, D, Cin, x.device)
                         d = rec.descriptor(dres_f)
-                        check(L.m3d_conv3d_bwd_data_wino_bny(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD, geo.pad[2],
-                                                             ptr(dx), acc, ptr(ws), wsb, v_ready, ctypes.addressof(d),
-                                                             ptr(bws), bwsb, ty, stream()), "conv3d_bwd_data_wino_bn")
+                        if vd is not None:
+                            check(L.m3d_conv3d_bwd_data_wino_xv(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                                geo.pad[2], ptr(dx), acc, ptr(ws), wsb, ptr(vd[0]), ty,
+                                                                ctypes.addressof(d), ptr(bws), bwsb, stream()),
+                                  "conv3d_bwd_data_wino_xv(bn)")
+                        else:
+                            check(L.m3d_conv3d_bwd_data_wino_bny(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
+                                                                 geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready,
+                                                                 ctypes.addressof(d), ptr(bws), bwsb, ty, stream()),
+                                  "conv3d_bwd_data_wino_bn")
                         rec.buf, rec.dres, rec.done = dx, dres_f, True
                         fused_nel = x.numel() * (1 + (rec.z is not None) + rec.need_res)
+                    elif vd is not None:
+                        check(L.m3d_conv3d_bwd_data_wino_xv(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD, geo.pad[2],
+                                                            ptr(dx), acc, ptr(ws), wsb, ptr(vd[0]), ty, None, None, 0,
+                                                            stream()), "conv3d_bwd_data_wino_xv")
                     else:
                         check(L.m3d_conv3d_bwd_data_wino_vy(ptr(dz), ptr(w), B, H, W, D, Cin, Cout, OD,
                                                             geo.pad[2], ptr(dx), acc, ptr(ws), wsb, v_ready, ty,

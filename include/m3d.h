@@ -477,6 +477,25 @@ int m3d_conv3d_bwd_data_wino_bny(const float* dz, const float* w, int64_t B, int
                                  int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
                                  void* workspace, size_t ws_bytes, int32_t v_ready, const m3d_bn_bwd_t* bn, void* bn_ws,
                                  size_t bn_ws_bytes, int32_t tile_y, m3d_stream_t s);
+/* Winograd weight transforms into caller memory: the transformed weights
+ * depend on w only, so a caller may produce them ahead of the convs (a side
+ * stream at the start of the forward) and pass them to the _kv / _xv entries,
+ * which then skip their own transform (same kernels, same bits).  dgrad 0: the
+ * forward's operand; 1: the data gradient's at tile_y (0 = library default, 2,
+ * 4).  Requires the bf16-split GEMMs (0 bytes / M3D_EINVAL otherwise). */
+size_t m3d_conv3d_wino_v_bytes(int64_t Cin, int64_t Cout, int32_t dgrad, int32_t tile_y);
+int m3d_conv3d_wino_weight_v(const float* w, int64_t Cin, int64_t Cout, int32_t dgrad, int32_t tile_y, void* v,
+                             size_t v_bytes, m3d_stream_t s);
+/* m3d_conv3d_fwd_wino_keep (u_keep may be NULL) with the transformed weights v */
+int m3d_conv3d_fwd_wino_kv(const float* x, int64_t B, int64_t H, int64_t W, int64_t D, int64_t Cin, const float* w,
+                           int64_t Cout, int64_t OD, int32_t pz, const float* bias, const float* bn_scale,
+                           const float* bn_shift, const float* residual, int32_t relu, float* z_out, float* y,
+                           float* u_keep, const void* v, void* workspace, size_t ws_bytes, m3d_stream_t s);
+/* m3d_conv3d_bwd_data_wino_vy (bn NULL) / _bny (bn set) with the transformed weights v */
+int m3d_conv3d_bwd_data_wino_xv(const float* dz, const float* w, int64_t B, int64_t H, int64_t W, int64_t D,
+                                int64_t Cin, int64_t Cout, int64_t OD, int32_t pz, float* dx, int32_t accumulate,
+                                void* workspace, size_t ws_bytes, const void* v, int32_t tile_y,
+                                const m3d_bn_bwd_t* bn, void* bn_ws, size_t bn_ws_bytes, m3d_stream_t s);
 /* m3d_conv3d_bwd_data_x3 (a 1x1x1 stride-1 conv's data gradient on the
  * bf16-split GEMM, accumulate 0) with m3d_conv3d_bwd_data_bn's fused BN-ReLU
  * backward in the GEMM's epilogue; bn_ws: m3d_bn_bwd_fused_workspace_bytes. */
