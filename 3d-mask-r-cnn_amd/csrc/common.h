@@ -122,6 +122,10 @@ int rank_sort_u64(const uint64_t* u, const int64_t* pos, int64_t n, bool desc, b
 #ifndef M3D_TUNE_X3W_SK
 #define M3D_TUNE_X3W_SK 1
 #endif
+// ... for weight-gradient GEMMs whose tiles have at least this many 16-row steps
+#ifndef M3D_TUNE_X3W_SK_MIN_STEPS
+#define M3D_TUNE_X3W_SK_MIN_STEPS 32
+#endif
 // (Measured-slower variants and their switches were removed in round 6:
 // DESIGN.md section 8 lists them, docs/DESIGN_HISTORY.md has their numbers.)
 // Winograd output tile along y: F(2,3) (2) or F(4,3) (4), as NZ is along z.

@@ -1783,7 +1783,7 @@ static void launch_wgrad_tr(const float* A, const float* Bm, float* C, int64_t M
     const int64_t tiles = (int64_t)((K + 255) / 256) * ((N + 255) / 256) * nbatch;
     const int64_t cus = num_cus();
     static constexpr int64_t minm = M3D_TUNE_X3W_TR_MINM;
-    if (M3D_TUNE_X3W_SK && !det().on && M >= 32 * W2_BK) {
+    if (M3D_TUNE_X3W_SK && !det().on && M >= (int64_t)M3D_TUNE_X3W_SK_MIN_STEPS * W2_BK) {
         // stream-K (X3wSK): one balanced round of workgroups, each >= minm rows
         // (only for tiles of >= 32 steps: with short tiles the minm floor would
         // give one workgroup a run of tiles, each with its own atomic epilogue)
