@@ -283,9 +283,9 @@ class RPN:
         prev, _nn.BIAS_BATCH = _nn.BIAS_BATCH, batch
         if _nn.X3_PLANES_BATCHED:
             _nn.X3_PLANES.refresh(self.device)   # live for this forward (nn.X3Planes)
-        _nn.WINO_V.active = (_nn.WINO_V_PREPASS and torch.is_grad_enabled()
-                             and image[0].numel() >= _nn.WINO_V_PREPASS_MIN_VOXELS)
-        if _nn.WINO_V.active:
+        _nn.WINO_V.active_fwd = _nn.WINO_V.active_dgrad = (
+            _nn.WINO_V_PREPASS and torch.is_grad_enabled() and image[0].numel() >= _nn.WINO_V_PREPASS_MIN_VOXELS)
+        if _nn.WINO_V.active_dgrad:
             _nn.WINO_V.refresh(self.device)     # Winograd weight transforms on a side stream (nn.WinoVPrep)
         try:
             fmaps = self.features(image)
@@ -294,7 +294,7 @@ class RPN:
             _nn.BIAS_BATCH = prev
             _nn.X3_PLANES.invalidate()          # the backward takes its planes through ctx
             _nn.WINO_V.invalidate()
-            _nn.WINO_V.active = False
+            _nn.WINO_V.active_fwd = _nn.WINO_V.active_dgrad = False
         if batch is not None:
             self.rpn.bias_batch = batch         # flushed by RPNHead.finish_backward
         rois = None

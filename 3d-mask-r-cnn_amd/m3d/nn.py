@@ -489,7 +489,9 @@ class WinoVPrep:
     def __init__(self):
         self.entries = {}            # key -> [weakref(w), cin, cout, dgrad, ty, buf, nbytes, event, valid]
         self.live = False
-        self.active = False          # this forward registers / takes (RPN.forward: volumes >= WINO_V_PREPASS_MIN_VOXELS)
+        self.active_fwd = False      # this forward registers / takes the forward transforms (RPN.forward:
+                                     # volumes >= WINO_V_PREPASS_MIN_VOXELS) ...
+        self.active_dgrad = False    # ... and the data-gradient ones (every training forward)
         self.gen = 0
         self.streams = {}
         self.pending = set()         # devices whose pre-pass stream the next join() waits for
@@ -499,7 +501,8 @@ class WinoVPrep:
             else torch.device(dev)
         for k in [k for k, e in self.entries.items() if e[0]() is None]:
             del self.entries[k]
-        es = [e for e in self.entries.values() if e[0]().device == dev]
+        es = [e for e in self.entries.values() if e[0]().device == dev
+              and (self.active_dgrad if e[3] else self.active_fwd)]
         if not es:
             self.live = True
             return
@@ -552,10 +555,13 @@ class WinoVPrep:
 
 # (the RPN's) Winograd weight transforms on a side stream at the start of the
 # forward, for volumes of at least WINO_V_PREPASS_MIN_VOXELS voxels.  Same box
-# (scripts/r06/gpu_prepass.sh, gpu_prepass256.sh, profiles/r06_wino_prepass_ab.txt):
-# 128^3 graph step 24.52 -> 24.25 ms, 256^3 147.4 -> 146.9 ms; at 64^3 the
-# replay is slower (9.92 -> 10.40 ms: the fast forward catches up with the side
-# stream and waits on every layer's event), so small volumes transform inline.
+# (scripts/r06/gpu_prepass.sh, gpu_prepass256.sh, gpu_prepass2.sh,
+# profiles/r06_wino_prepass_ab.txt): 128^3 graph step 24.52 -> 24.25 and 24.39
+# -> 24.10 ms, 256^3 147.4 -> 146.9 ms; at 64^3 the replay is slower with the
+# side stream in the graph -- 9.92 -> 10.40 ms with both transforms on it, 9.88
+# -> 10.76 ms with the data gradient's alone (configs[0] 10.6 -> 11.4 ms) -- so
+# smaller volumes transform inline.  (active_fwd / active_dgrad stay separate
+# switches for such A/Bs.)
 WINO_V_PREPASS = True
 WINO_V_PREPASS_MIN_VOXELS = 128 ** 3
 WINO_V = WinoVPrep()
@@ -961,15 +967,16 @@ class _ConvBNAct(torch.autograd.Function):
                 nu = 0          # too large to hold until the backward: the weight gradient re-transforms x
             vf = None
             ctx.vd = None
-            if WINO_V_PREPASS and WINO_V.active and halo is None:
-                ty = _dgrad_tile_y(name)
-                WINO_V.ensure(w, Cin, Cout, 0, 0)
-                if need_dx:
+            if WINO_V_PREPASS and halo is None:
+                if WINO_V.active_fwd:
+                    WINO_V.ensure(w, Cin, Cout, 0, 0)
+                    vf = WINO_V.take(w, 0, 0)
+                    if vf is not None:
+                        torch.cuda.current_stream().wait_event(vf[1])
+                if need_dx and WINO_V.active_dgrad:
+                    ty = _dgrad_tile_y(name)
                     WINO_V.ensure(w, Cin, Cout, 1, ty)
-                vf = WINO_V.take(w, 0, 0)
-                if vf is not None:
-                    torch.cuda.current_stream().wait_event(vf[1])
-                    ctx.vd = WINO_V.take(w, 1, ty) if need_dx else None
+                    ctx.vd = WINO_V.take(w, 1, ty)      # waited on in the backward
             if pending is not None:
                 # phase 1 (weights + interior z tiles) overlaps the halo transfer
                 ctx.u = torch.empty(nu, device=x.device, dtype=torch.float32) if nu > 0 else None

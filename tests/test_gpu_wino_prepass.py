@@ -10,13 +10,22 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _steps(cuda, prepass, monkeypatch, n=3, graph=False):
+def _dgrad_only_refresh(refresh):
+    def wrapped(self, dev):
+        self.active_fwd = False          # RPN.forward set both: keep the data gradient's only
+        return refresh(self, dev)
+    return wrapped
+
+
+def _steps(cuda, prepass, monkeypatch, n=3, graph=False, fwd=True):
     from m3d import _lib
     from m3d import nn as mnn
     from m3d.config import synthetic_rpn_config
     from m3d.model import RPN, RPNTargets, synthetic_rpn_targets, synthetic_volume
     monkeypatch.setattr(mnn, "WINO_V_PREPASS", prepass)
     monkeypatch.setattr(mnn, "WINO_V_PREPASS_MIN_VOXELS", 0)     # the test volume is small
+    if not fwd:   # the data gradient's transforms alone on the pre-pass
+        monkeypatch.setattr(mnn.WinoVPrep, "refresh", _dgrad_only_refresh(mnn.WinoVPrep.refresh))
     cfg = synthetic_rpn_config(64, depth=32, PRE_NMS_LIMIT=2000, POST_NMS_ROIS_TRAINING=200)
     image = synthetic_volume(64, 32, seed=3).to(cuda)
     model = RPN(cfg, device=cuda, seed=7)
@@ -35,15 +44,16 @@ def _steps(cuda, prepass, monkeypatch, n=3, graph=False):
     return losses, model.store.flat.clone()
 
 
+@pytest.mark.parametrize("fwd", [True, False], ids=["fwd+dgrad", "dgrad"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_wino_prepass_step_bitwise(cuda, monkeypatch, graph):
+def test_wino_prepass_step_bitwise(cuda, monkeypatch, graph, fwd):
     from m3d import _lib
     from m3d import nn as mnn
     _lib.set_deterministic(True)
     try:
         l0, w0 = _steps(cuda, False, monkeypatch, graph=graph)
         g0 = mnn.WINO_V.gen
-        l1, w1 = _steps(cuda, True, monkeypatch, graph=graph)
+        l1, w1 = _steps(cuda, True, monkeypatch, graph=graph, fwd=fwd)
     finally:
         _lib.set_deterministic(False)
     assert mnn.WINO_V.gen > g0 and len(mnn.WINO_V.entries) > 0
